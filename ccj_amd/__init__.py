@@ -1,0 +1,258 @@
+"""ccj_amd — MI355X-native CCJ pseudoknot MFE engine (host mirror of the reference API).
+
+The reference exposes CCJ through a C++ class and a free function:
+
+    W_final(std::string seq, int dangle);  double W_final::ccj();  std::string W_final::structure
+        (reference src/W_final.hh:18-71, src/W_final.cc:20-105)
+    std::string ccj(std::string seq, double &energy, int dangle)       (reference src/CCJ.cc:44-49)
+
+This package mirrors that surface in Python on top of libccj_hip.so (include/ccj.h).  The fill
+always runs on the GPU through hand-written HIP kernels; there is no CPU fallback — if the
+extension is missing or no GPU is visible the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+__all__ = [
+    "W_final", "ccj", "load_params", "param_path", "CCJError", "BacktrackExit", "lib", "MAT4", "MAT2",
+    "num_cells",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+# CCJ_LIB_VARIANT=dbg selects the bounds-checked debug build (libccj_hip_dbg.so)
+_LIB_PATH = os.path.join(_HERE, "lib", "libccj_hip_dbg.so" if os.environ.get("CCJ_LIB_VARIANT") == "dbg"
+                         else "libccj_hip.so")
+PARAM_DIR = os.path.join(_HERE, "params")
+
+# ccj.h enums
+MAT4 = ["PK", "PL", "PR", "PM", "PO", "PfromL", "PfromR", "PfromM", "PfromMprime", "PfromO",
+        "PLmloop00", "PLmloop01", "PLmloop10", "PRmloop00", "PRmloop01", "PRmloop10",
+        "PMmloop00", "PMmloop01", "PMmloop10", "POmloop00", "POmloop01", "POmloop10"]
+MAT2 = ["P", "WBP", "WPP", "V", "Vtype", "WM", "WMv", "WMp"]
+HASH_NAMES = MAT4 + MAT2 + ["W"]
+
+CCJ_OK, CCJ_E_ARG, CCJ_E_OOM, CCJ_E_HIP, CCJ_E_PARAMS, CCJ_E_BACKTRACK, CCJ_E_STATE, CCJ_E_INTER_EXIT = range(8)
+
+# name -> blob file (the reference's params/*.par sets, dumped to our table format)
+PARAM_SETS = {
+    "Turner04": "Turner04.ccjp", "rna_Turner04": "Turner04.ccjp",
+    "DirksPierce09": "DirksPierce09.ccjp", "rna_DirksPierce09": "DirksPierce09.ccjp",
+    "DirksPierce03": "DirksPierce03.ccjp", "rna_DirksPierce03": "DirksPierce03.ccjp",
+    "CaoChen06": "CaoChen06.ccjp", "rna_CaoChen06": "CaoChen06.ccjp",
+    "CaoChen09": "CaoChen09.ccjp", "rna_CaoChen09": "CaoChen09.ccjp",
+    "Matthews04": "Matthews04.ccjp", "dna_Matthews04": "Matthews04.ccjp",
+    "DNA_Mathews2004": "DNA_Mathews2004.ccjp", "default": "default.ccjp",
+}
+
+
+class CCJError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ccj error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class BacktrackExit(CCJError):
+    """The reference would have terminated inside its backtrack (stderr text + exit code)."""
+
+    def __init__(self, code: int, msg: str, exit_code: int, stdout: str):
+        super().__init__(code, msg)
+        self.exit_code = exit_code
+        self.stdout = stdout
+
+
+class _Problem(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_char_p), ("dangles", ctypes.c_int), ("noGU", ctypes.c_int),
+                ("params", ctypes.c_void_p), ("pen", ctypes.c_void_p)]
+
+
+class _Options(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("overlap_d2h", ctypes.c_int)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libccj_hip.so (raises if it has not been built — no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise CCJError(CCJ_E_STATE, f"{_LIB_PATH} missing: run __graft_entry__.build() first")
+    L = ctypes.CDLL(_LIB_PATH)
+    vp, ip, cp = ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p
+    L.ccj_create.argtypes = [ctypes.POINTER(_Problem), ctypes.POINTER(_Options), ctypes.POINTER(vp)]
+    L.ccj_create.restype = ip
+    for fn in ("ccj_fill", "ccj_fill_device", "ccj_sync_host", "ccj_n"):
+        getattr(L, fn).argtypes = [vp]
+        getattr(L, fn).restype = ip
+    L.ccj_result.argtypes = [vp, cp, ctypes.POINTER(ctypes.c_double), cp, ip]
+    L.ccj_result.restype = ip
+    L.ccj_get4.argtypes = [vp, ip, ip, ip, ip, ip]
+    L.ccj_get4.restype = ip
+    L.ccj_get2.argtypes = [vp, ip, ip, ip]
+    L.ccj_get2.restype = ip
+    L.ccj_getW.argtypes = [vp, ip]
+    L.ccj_getW.restype = ip
+    L.ccj_hashes.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    L.ccj_hashes.restype = ip
+    L.ccj_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    L.ccj_last_timing.restype = ip
+    L.ccj_last_error.argtypes = [vp]
+    L.ccj_last_error.restype = cp
+    L.ccj_destroy.argtypes = [vp]
+    L.ccj_destroy.restype = None
+    L.ccj_num_cells.argtypes = [ip]
+    L.ccj_num_cells.restype = ctypes.c_uint64
+    _lib = L
+    return L
+
+
+def num_cells(n: int) -> int:
+    """4-D DP cells C(n+1,4) — the unit of work."""
+    if n < 3:
+        return 0
+    m = n + 1
+    return m * (m - 1) * (m - 2) * (m - 3) // 24
+
+
+def param_path(name_or_path: str) -> str:
+    if os.path.exists(name_or_path) and name_or_path.endswith(".ccjp"):
+        return name_or_path
+    base = os.path.basename(name_or_path)
+    for suf in (".par", ".ccjp"):
+        if base.endswith(suf):
+            base = base[: -len(suf)]
+    if base in PARAM_SETS:
+        return os.path.join(PARAM_DIR, PARAM_SETS[base])
+    raise CCJError(CCJ_E_ARG, f"unknown parameter set {name_or_path!r}")
+
+
+_PARAM_CACHE: dict = {}
+
+
+def load_params(name_or_path: str = "DirksPierce09") -> bytes:
+    """Scaled 37 C energy tables (include/ccj_params.h) for one of the reference parameter sets."""
+    p = param_path(name_or_path)
+    if p not in _PARAM_CACHE:
+        with open(p, "rb") as f:
+            _PARAM_CACHE[p] = f.read()
+    return _PARAM_CACHE[p]
+
+
+class W_final:
+    """Mirror of the reference class W_final (src/W_final.hh:18-71).
+
+    ``W_final(seq, dangle).ccj()`` fills every matrix on the GPU, runs W + backtrack on the host
+    mirror and returns the MFE in kcal/mol; ``structure`` holds the dot-bracket string.
+    """
+
+    def __init__(self, seq: str, dangle: int = 2, params: str | bytes = "DirksPierce09",
+                 noGU: bool = False, device: int = 0, overlap_d2h: bool = True):
+        self.seq = seq
+        self.n = len(seq)
+        self.dangle = dangle
+        self._blob = params if isinstance(params, (bytes, bytearray)) else load_params(params)
+        self._blob_buf = ctypes.create_string_buffer(bytes(self._blob), len(self._blob))
+        self._seq_buf = ctypes.create_string_buffer(seq.encode())
+        L = lib()
+        prob = _Problem(ctypes.cast(self._seq_buf, ctypes.c_char_p), dangle, 1 if noGU else 0,
+                        ctypes.cast(self._blob_buf, ctypes.c_void_p), None)
+        opts = _Options(device, 1 if overlap_d2h else 0)
+        h = ctypes.c_void_p()
+        rc = L.ccj_create(ctypes.byref(prob), ctypes.byref(opts), ctypes.byref(h))
+        if rc != CCJ_OK:
+            msg = L.ccj_last_error(h).decode() if h.value else "ccj_create failed"
+            if h.value:
+                L.ccj_destroy(h)
+            raise CCJError(rc, msg)
+        self._h = h
+        self.structure: Optional[str] = None
+        self.energy: Optional[float] = None
+        self.stdout_msgs = ""
+
+    def _check(self, rc: int):
+        if rc != CCJ_OK:
+            raise CCJError(rc, lib().ccj_last_error(self._h).decode())
+
+    def fill(self):
+        self._check(lib().ccj_fill(self._h))
+
+    def fill_device(self):
+        self._check(lib().ccj_fill_device(self._h))
+
+    def sync_host(self):
+        self._check(lib().ccj_sync_host(self._h))
+
+    def result(self):
+        L = lib()
+        buf = ctypes.create_string_buffer(self.n + 1)
+        msgs = ctypes.create_string_buffer(1 << 16)
+        e = ctypes.c_double()
+        rc = L.ccj_result(self._h, buf, ctypes.byref(e), msgs, 1 << 16)
+        self.stdout_msgs = msgs.value.decode()
+        if rc == CCJ_E_BACKTRACK or rc == CCJ_E_INTER_EXIT:
+            err = L.ccj_last_error(self._h).decode()
+            exit_code = 0 if rc == CCJ_E_INTER_EXIT else (134 if "Assertion" in err else 1)
+            raise BacktrackExit(rc, err, exit_code, self.stdout_msgs)
+        self._check(rc)
+        self.structure = buf.value.decode()
+        self.energy = e.value
+        return self.energy
+
+    def ccj(self) -> float:
+        """reference W_final::ccj (W_final.cc:58-105)"""
+        self.fill()
+        return self.result()
+
+    # ---- matrix access (reference getter semantics) ----
+    def get4(self, mat, i, j, k, l) -> int:
+        m = MAT4.index(mat) if isinstance(mat, str) else mat
+        return lib().ccj_get4(self._h, m, i, j, k, l)
+
+    def get2(self, mat, i, j) -> int:
+        m = MAT2.index(mat) if isinstance(mat, str) else mat
+        return lib().ccj_get2(self._h, m, i, j)
+
+    def W(self, j) -> int:
+        return lib().ccj_getW(self._h, j)
+
+    def hashes(self) -> dict:
+        out = (ctypes.c_uint64 * len(HASH_NAMES))()
+        self._check(lib().ccj_hashes(self._h, out))
+        return {name: "%016x" % out[x] for x, name in enumerate(HASH_NAMES)}
+
+    def timing(self) -> dict:
+        f = ctypes.c_double()
+        k = (ctypes.c_double * 3)()
+        lib().ccj_last_timing(self._h, ctypes.byref(f), k)
+        return {"fill_ms": f.value, "level4d_ms": k[0], "diag2d_ms": k[1], "precompute_ms": k[2]}
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().ccj_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def ccj(seq: str, dangle: int = 2, params: str | bytes = "DirksPierce09", noGU: bool = False,
+        device: int = 0):
+    """reference ``std::string ccj(std::string seq, double &energy, int dangle)`` (CCJ.cc:44-49).
+
+    Returns (structure, energy_kcal_per_mol).
+    """
+    wf = W_final(seq, dangle, params=params, noGU=noGU, device=device)
+    try:
+        energy = wf.ccj()
+        return wf.structure, energy
+    finally:
+        wf.close()

