@@ -166,10 +166,7 @@ class W_final:
         h = ctypes.c_void_p()
         rc = L.ccj_create(ctypes.byref(prob), ctypes.byref(opts), ctypes.byref(h))
         if rc != CCJ_OK:
-            msg = L.ccj_last_error(h).decode() if h.value else "ccj_create failed"
-            if h.value:
-                L.ccj_destroy(h)
-            raise CCJError(rc, msg)
+            raise CCJError(rc, L.ccj_last_error(None).decode())
         self._h = h
         self.structure: Optional[str] = None
         self.energy: Optional[float] = None

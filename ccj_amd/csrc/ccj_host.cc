@@ -1337,10 +1337,9 @@ extern "C" uint64_t ccj_num_cells(int n) {
     return m * (m - 1) * (m - 2) * (m - 3) / 24;
 }
 
-extern "C" int ccj_create(const ccj_problem *prob, const ccj_options *opts, ccj_ctx **out) {
-    if (!prob || !out || !prob->seq || !prob->params) return CCJ_E_ARG;
-    *out = nullptr;
-    std::unique_ptr<ccj_ctx> c(new ccj_ctx());
+static thread_local std::string g_create_err;
+
+static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::unique_ptr<ccj_ctx> &c, ccj_ctx **out) {
     c->seq = prob->seq;
     c->n = (int)c->seq.size();
     c->dangles = prob->dangles;
@@ -1511,6 +1510,24 @@ extern "C" int ccj_create(const ccj_problem *prob, const ccj_options *opts, ccj_
     T.err = c->d_err;
     *out = c.release();
     return CCJ_OK;
+}
+
+extern "C" int ccj_create(const ccj_problem *prob, const ccj_options *opts, ccj_ctx **out) {
+    if (!out) return CCJ_E_ARG;
+    *out = nullptr;
+    g_create_err.clear();
+    if (!prob || !prob->seq || !prob->params) {
+        g_create_err = "null problem / sequence / params";
+        return CCJ_E_ARG;
+    }
+    std::unique_ptr<ccj_ctx> c(new ccj_ctx());
+    const int rc = create_impl(prob, opts, c, out);
+    if (rc != CCJ_OK) {
+        g_create_err = c ? c->err : std::string("ccj_create failed");
+        if (g_create_err.empty()) g_create_err = "invalid problem (sequence alphabet, length or parameter blob)";
+        if (c) ccj_destroy(c.release());
+    }
+    return rc;
 }
 
 extern "C" int ccj_fill_device(ccj_ctx *c) {
@@ -1772,7 +1789,7 @@ extern "C" int ccj_work_model_seq(const char *seq, int noGU, double *out) {
 }
 
 extern "C" int ccj_n(const ccj_ctx *c) { return c ? c->n : 0; }
-extern "C" const char *ccj_last_error(const ccj_ctx *c) { return c ? c->err.c_str() : "null context"; }
+extern "C" const char *ccj_last_error(const ccj_ctx *c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
 extern "C" void ccj_destroy(ccj_ctx *c) {
     if (!c) return;

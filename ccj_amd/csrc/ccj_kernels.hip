@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
         const int tc = ptype(T, i, l);
         int best_int = INF;
         const int max_k = imin(l - TURN - 2, i + MAXLOOP + 1);
-        const int off = imax(2, sigma - MAXLOOP - 2);  // min_l = k + off  (:292)
+        const int off = imax(TURN + 1, sigma - MAXLOOP - 2);  // min_l = k + off  (:292)
         const int nk = max_k - i;
         for (int idx = tid; idx < nk * 32; idx += 256) {
             const int k = i + 1 + (idx >> 5);
@@ -277,8 +277,9 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
         const Penalties &pe = T.pen;
         int bb = INF, bw = INF;
         for (int d = i + tid; d < l; d += 256) {
-            const int wb = (d == i) ? 0 : T.WB[(d - 1 - i) * rs + i];
-            const int wp = (d == i) ? 0 : T.WP[(d - 1 - i) * rs + i];
+            // get_WB(i, i-1) is 0, except get_WB(1, 0) which is INF (j <= 0 test first, :648)
+            const int wb = (d == i) ? (i == 1 ? INF : 0) : T.WB[(d - 1 - i) * rs + i];
+            const int wp = (d == i) ? (i == 1 ? INF : 0) : T.WP[(d - 1 - i) * rs + i];
             const int vd = (d == i) ? v_il : T.V[(l - d) * rs + d];
             const int pd = (d == i) ? p_il : T.P[(l - d) * rs + d];
             bb = imin(bb, imin(wb + vd + pe.bp + pe.PPS, wb + pd + pe.PSM + pe.PPS));
