@@ -57,6 +57,8 @@ struct DevTables {
     int16_t *ie;                   // [u1][u2][w][p] e_intP, saturated at 32767
     int *V; int8_t *Vt; int *WM, *WMv, *WMp, *P, *WBP, *WPP, *WB, *WP;  // [w][p]
     const LevelDesc *lv;           // per level t
+    int16_t *d4;                   // 4-D storage base
+    const long long *lb;           // element offset of level t in d4
     int *err;                      // device error word
 };
 
@@ -73,4 +75,5 @@ int ccjk_init2d(const ccj::DevTables *T, void *stream);
 int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
 int ccjk_diag2d(const ccj::DevTables *T, int sigma, void *stream);
 int ccjk_level4d(const ccj::DevTables *T, int t, void *stream);
+int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
 }

@@ -101,9 +101,12 @@ struct ccj_ctx {
     short *d_S = nullptr, *d_S1 = nullptr;
     ccj_energy_params *d_prm = nullptr;
     LevelDesc *d_lv = nullptr;
+    long long *d_lb = nullptr;
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
     int8_t *d_vt = nullptr;
-    hipStream_t st = nullptr, st_copy = nullptr;
+    hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr;
+    std::vector<hipEvent_t> p_done;  // P(sigma) reduced
+    std::vector<double> lev_ms_v, diag_ms_v;
     std::vector<hipEvent_t> lev_done;
     std::vector<hipEvent_t> tev;  // timing events: 2 per level kernel + 2 per diag kernel
     hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_pre = nullptr;
@@ -1402,11 +1405,14 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipSetDevice(c->device));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking));
+    HIPCHK(cp, hipStreamCreateWithFlags(&c->st_p, hipStreamNonBlocking));
     HIPCHK(cp, hipEventCreate(&c->ev_start));
     HIPCHK(cp, hipEventCreate(&c->ev_end));
     HIPCHK(cp, hipEventCreate(&c->ev_pre));
     c->lev_done.resize(n + 1);
     for (auto &e : c->lev_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->p_done.resize(n + 1);
+    for (auto &e : c->p_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->tev.resize(4 * (size_t)n + 4);
     for (auto &e : c->tev) HIPCHK(cp, hipEventCreate(&e));
 
@@ -1426,6 +1432,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipMalloc(&c->d_S1, (n + 2) * sizeof(short)));
     HIPCHK(cp, hipMalloc(&c->d_prm, sizeof(ccj_energy_params)));
     HIPCHK(cp, hipMalloc(&c->d_lv, c->lv_host.size() * sizeof(LevelDesc)));
+    HIPCHK(cp, hipMalloc(&c->d_lb, c->lv_off.size() * sizeof(long long)));
     HIPCHK(cp, hipMalloc(&c->d2i, A2_N * plane * sizeof(int)));
     HIPCHK(cp, hipMalloc(&c->d_vt, plane));
     if (c->total4 > 0 && hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
@@ -1477,6 +1484,10 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipMemcpy(c->d_S1, c->S1.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_prm, &c->prm, sizeof(ccj_energy_params), hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_lv, c->lv_host.data(), c->lv_host.size() * sizeof(LevelDesc), hipMemcpyHostToDevice));
+    {
+        std::vector<long long> lb(c->lv_off.begin(), c->lv_off.end());
+        HIPCHK(cp, hipMemcpy(c->d_lb, lb.data(), lb.size() * sizeof(long long), hipMemcpyHostToDevice));
+    }
 
     DevTables &T = c->T;
     T.n = n;
@@ -1507,6 +1518,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.WP = c->d2i + A2_WP * plane;
     T.Vt = c->d_vt;
     T.lv = c->d_lv;
+    T.d4 = c->d4;
+    T.lb = c->d_lb;
     T.err = c->d_err;
     *out = c.release();
     return CCJ_OK;
@@ -1542,7 +1555,17 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     HIPCHK(c, (hipError_t)ccjk_init2d(&c->T, st));
     HIPCHK(c, (hipError_t)ccjk_precompute_ie(&c->T, st));
     HIPCHK(c, hipEventRecord(c->ev_pre, st));
+    // P(sigma) only needs PK levels <= sigma-3: reduce it on a side stream three levels ahead
+    HIPCHK(c, hipEventRecord(c->lev_done[n], st));  // "init done" for the side stream
+    auto launch_p = [&](int sig) -> int {
+        if (sig < 3 || sig >= n) return CCJ_OK;
+        HIPCHK(c, hipStreamWaitEvent(c->st_p, sig - 3 < c->nlev ? c->lev_done[sig - 3] : c->lev_done[n], 0));
+        HIPCHK(c, (hipError_t)ccjk_pterm(&c->T, sig, c->st_p));
+        HIPCHK(c, hipEventRecord(c->p_done[sig], c->st_p));
+        return CCJ_OK;
+    };
     for (int s = 0; s < n; ++s) {
+        if (s >= 3) HIPCHK(c, hipStreamWaitEvent(st, c->p_done[s], 0));
         HIPCHK(c, hipEventRecord(c->tev[4 * s + 0], st));
         HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, s, st));
         HIPCHK(c, hipEventRecord(c->tev[4 * s + 1], st));
@@ -1550,18 +1573,20 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
             HIPCHK(c, hipEventRecord(c->tev[4 * s + 2], st));
             HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, st));
             HIPCHK(c, hipEventRecord(c->tev[4 * s + 3], st));
+            HIPCHK(c, hipEventRecord(c->lev_done[s], st));
             if (c->overlap && c->h4) {
                 // stream the finished level to the pinned host mirror while later levels run
-                HIPCHK(c, hipEventRecord(c->lev_done[s], st));
                 HIPCHK(c, hipStreamWaitEvent(c->st_copy, c->lev_done[s], 0));
                 const size_t bytes = (size_t)NMAT4 * c->lv_host[s].C * sizeof(int16_t);
                 HIPCHK(c, hipMemcpyAsync(c->h4 + c->lv_off[s], c->d4 + c->lv_off[s], bytes, hipMemcpyDeviceToHost,
                                          c->st_copy));
             }
         }
+        if (int rc = launch_p(s + 3)) return rc;
     }
     HIPCHK(c, hipEventRecord(c->ev_end, st));
     HIPCHK(c, hipStreamSynchronize(st));
+    HIPCHK(c, hipStreamSynchronize(c->st_p));
     int herr = 0;
     HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (herr & 1) return set_err(c, CCJ_E_PARAMS, "e_intP table value outside int16 range (flags %d)", herr);
@@ -1572,12 +1597,16 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev_start, c->ev_pre));
     c->pre_ms = ms;
     double lsum = 0, dsum = 0;
+    c->lev_ms_v.assign(n, 0.0);
+    c->diag_ms_v.assign(n, 0.0);
     for (int s = 0; s < n; ++s) {
         HIPCHK(c, hipEventElapsedTime(&ms, c->tev[4 * s + 0], c->tev[4 * s + 1]));
         dsum += ms;
+        c->diag_ms_v[s] = ms;
         if (s < c->nlev) {
             HIPCHK(c, hipEventElapsedTime(&ms, c->tev[4 * s + 2], c->tev[4 * s + 3]));
             lsum += ms;
+            c->lev_ms_v[s] = ms;
         }
     }
     c->level_ms = lsum;
@@ -1788,6 +1817,15 @@ extern "C" int ccj_work_model_seq(const char *seq, int noGU, double *out) {
     return work_model(n, S.data(), pairt, out);
 }
 
+extern "C" int ccj_level_times(const ccj_ctx *c, double *level_ms, double *diag_ms, int cap) {
+    if (!c) return CCJ_E_ARG;
+    for (int t = 0; t < cap && t < (int)c->lev_ms_v.size(); ++t) {
+        if (level_ms) level_ms[t] = c->lev_ms_v[t];
+        if (diag_ms) diag_ms[t] = c->diag_ms_v[t];
+    }
+    return CCJ_OK;
+}
+
 extern "C" int ccj_n(const ccj_ctx *c) { return c ? c->n : 0; }
 extern "C" const char *ccj_last_error(const ccj_ctx *c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
@@ -1796,6 +1834,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipSetDevice(c->device);
     if (c->st) hipStreamSynchronize(c->st);
     if (c->st_copy) hipStreamSynchronize(c->st_copy);
+    if (c->st_p) hipStreamSynchronize(c->st_p);
     hipFree(c->d4);
     hipFree(c->d_ie);
     hipFree(c->d_est);
@@ -1809,10 +1848,13 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_S1);
     hipFree(c->d_prm);
     hipFree(c->d_lv);
+    hipFree(c->d_lb);
     hipFree(c->d2i);
     hipFree(c->d_vt);
     if (c->h4) hipHostFree(c->h4);
     for (auto e : c->lev_done) hipEventDestroy(e);
+    for (auto e : c->p_done) hipEventDestroy(e);
+    if (c->st_p) hipStreamDestroy(c->st_p);
     for (auto e : c->tev) hipEventDestroy(e);
     if (c->ev_start) hipEventDestroy(c->ev_start);
     if (c->ev_end) hipEventDestroy(c->ev_end);

@@ -29,13 +29,18 @@ __device__ __forceinline__ int ld4(const DevTables &T, int x, int tp, int ap, in
         return 0;
     }
 #endif
-    const LevelDesc &L = T.lv[tp];
-    const int off = x * L.C + ap * L.M + hp * L.m - ((hp * (hp - 1)) >> 1) + ip - 1;
-    return (int)L.base[off];
+    const int mp = T.n - tp - 2;
+    const int Mp = (mp * (mp + 1)) >> 1;
+    const int off = x * (tp + 1) * Mp + ap * Mp + hp * mp - ((hp * (hp - 1)) >> 1) + ip - 1;
+    return (int)T.d4[T.lb[tp] + off];
 }
 
 #ifdef CCJ_DEBUG_BOUNDS
 __device__ int *g_dbg_err;
+#define IE_CHECK(u1_, u2_, w_, p_) \
+    if ((u1_) < 0 || (u1_) >= IE_U || (u2_) < 0 || (u2_) >= IE_U || (w_) < 0 || (w_) > n || (p_) < 1 || (p_) + (w_) > n) atomicOr(T.err, 16)
+#else
+#define IE_CHECK(u1_, u2_, w_, p_)
 #endif
 
 template <class TT>
@@ -56,6 +61,7 @@ __device__ __forceinline__ int gWMv(const DevTables &T, int i, int j) { return i
 __device__ __forceinline__ int gWMp(const DevTables &T, int i, int j) { return i >= j ? INF : at2(T.WMp, T.rs, i, j); }
 
 __device__ __forceinline__ int ptype(const DevTables &T, int i, int j) { return T.pt[(j - i) * T.rs + i]; }
+#define W2E(A, p, q) ((int)(A)[((q) - (p)) * rs + (p)])
 
 __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
@@ -246,30 +252,9 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
         }
     }
 
-    // ---- P(i,l): pseudo_loop.cc:166-179 (PK of levels <= sigma-3 only)
-    {
-        int best = INF;
-        const int sq = sigma * sigma;
-        for (int idx = tid; idx < sq; idx += 256) {
-            const int j = i + idx / sigma;
-            const int d = i + idx % sigma;
-            if (!(j < d && d <= l - 2)) continue;
-            const int a1 = j - i, h1 = d - 1 - j;  // PK(i, j, d+1, k)
-            const int a2 = d - j - 1;              // PK(j+1, d, k+1, l)
-            for (int k = d + 1; k < l; ++k) {
-                const int b1 = k - d - 1, h2 = k - 1 - d, b2 = l - k - 1;
-                const int v = ld4(T, PK, a1 + b1, a1, h1, i) + ld4(T, PK, a2 + b2, a2, h2, j + 1);
-                best = imin(best, v);
-            }
-        }
-        best = block_min(best, red);
-        if (tid == 0) {
-            int p = INF + 1;
-            if (best < INF / 2) { p = best; T.P[cell] = p; }
-            sh_p = p;
-        }
-        __syncthreads();
-    }
+    // ---- P(i,l) was reduced into T.P by k_pterm(sigma) (ordered before this kernel by an event)
+    if (tid == 0) sh_p = T.P[cell];
+    __syncthreads();
     const int v_il = sh_v, p_il = sh_p;
 
     // ---- WBP / WPP: pseudo_loop.cc:134-164 (+ the WB/WP getters :647-661)
@@ -327,9 +312,66 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
 }
 
 // ------------------------------------------------------------------------------------------
-// 4-D level t: one lane per cell (i,j,k,l); all lanes of a wave share (t, a) so every loop
-// bound is wave-uniform.  pseudo_loop.cc:181-644, 663-808.
+// P(i, i+sigma) = min over i<=j<d<k<l of PK(i,j,d+1,k) + PK(j+1,d,k+1,l)   (pseudo_loop.cc:166-179)
+// One wave = (jo = j-i, a chunk of do = d-i, a group of 64 consecutive intervals i): for fixed
+// offsets the two PK cells of neighbouring intervals are neighbours in HBM, so every load is
+// coalesced.  Each lane min-reduces its interval's candidates and does one atomicMin into T.P
+// (initialised INF+1 = "never set"; every candidate is <= 65534 < INF/2, A-Q4).  Needs PK levels
+// <= sigma-3 only, so it runs on a side stream three levels ahead of k_diag2d(sigma).
 // ------------------------------------------------------------------------------------------
+constexpr int PT_CHUNK = 16;
+
+__global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngroups, int nchunks) {
+    const int n = T.n;
+    const int lane = threadIdx.x & 63;
+    const int jo = blockIdx.y;
+    const int wr = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int chunk = wr / ngroups;
+    const int grp = wr - chunk * ngroups;
+    if (chunk >= nchunks) return;
+    const int d0 = jo + 1 + chunk * PT_CHUNK;
+    const int d1 = imin(d0 + PT_CHUNK, sigma - 1);  // do <= sigma-2
+    if (d0 >= d1) return;
+    const int i = grp * 64 + lane + 1;
+    if (i + sigma > n) return;
+    int best = INF + 1;
+    for (int dd = d0; dd < d1; ++dd) {
+        const int a1 = jo, h1 = dd - jo - 1;   // PK(i, j, d+1, k)
+        const int a2 = dd - jo - 1;            // PK(j+1, d, k+1, l)
+#pragma unroll 4
+        for (int ko = dd + 1; ko < sigma; ++ko) {
+            const int b1 = ko - dd - 1, h2 = ko - dd - 1, b2 = sigma - ko - 1;
+            const int v = ld4(T, PK, a1 + b1, a1, h1, i) + ld4(T, PK, a2 + b2, a2, h2, i + jo + 1);
+            best = imin(best, v);
+        }
+    }
+    atomicMin(T.P + sigma * T.rs + i, best);
+}
+
+// ------------------------------------------------------------------------------------------
+// 4-D level t: one lane per cell (i,j,k,l); all lanes of a wave share (t, a) so every loop bound
+// is wave-uniform.  pseudo_loop.cc:181-644, 663-808.
+//
+// Addressing: a neighbour at (t-dt, a', h+dh, i+di) of matrix x lives at
+//     d4[ LB[t-dt] + x*C' + a'*M' + dh*m + dh*dt - dh(dh-1)/2 + di ]  (wave-uniform, SGPRs)
+//       + L0 + h*(dt-dh)                                              (per lane, VGPR)
+// with L0 = G_t(h) + i - 1 the cell's own in-block offset; every read is a coalesced global load.
+//
+// The 22 recurrences' split-point loops are fused into one loop over the (i,j) gap ("a-loop")
+// and one over the (k,l) gap ("b-loop"): each neighbour value is loaded once and feeds every
+// recurrence that reads it (11a + 13b int16 loads per cell instead of 14a + 16b).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ const int16_t *nb_base(const DevTables &T, int x, int t, int m, int dt, int ap, int dh,
+                                                  int di) {
+    const int tp = t - dt;
+    const int mp = m + dt;
+    const int Mp = (mp * (mp + 1)) >> 1;
+    const int Cp = (tp + 1) * Mp;
+    const long long off = T.lb[tp] + (long long)x * Cp + (long long)ap * Mp + (long long)(dh * m + dh * dt) -
+                          ((dh * (dh - 1)) >> 1) + di;
+    return T.d4 + off;
+}
+
 __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPerA) {
 #ifdef CCJ_DEBUG_BOUNDS
     g_dbg_err = T.err;
@@ -355,100 +397,133 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
     const int i = c - Gh + 1;
     const int g = h + 2;
     const int j = i + a, k = j + g, l = k + b;
+    const unsigned L0 = (unsigned)(Gh + i - 1);
 
     const Penalties pe = T.pen;
     const int bp = pe.bp, cp = pe.cp, PB = pe.PB, apbp2 = pe.ap + 2 * pe.bp;
-    const int *WB = T.WB, *WP = T.WP, *WBPr = T.WBP;
-#define L4(x, dt, ap_, dh, di) ld4(T, (x), t - (dt), (ap_), h + (dh), i + (di))
+    const int *__restrict__ WB = T.WB;
+    const int *__restrict__ WP = T.WP;
+    const int *__restrict__ WBPr = T.WBP;
+// neighbour read: matrix x at (t-dt, ap, h+dh, i+di); lane offset L0 + h*(dt-dh)
+#define RD(x, dt, ap_, dh, di) \
+    ((int)nb_base(T, (x), t, m, (dt), (ap_), (dh), (di))[L0 + (unsigned)h * (unsigned)((dt) - (dh))])
 #ifdef CCJ_DEBUG_BOUNDS
-#define IE_CHECK(u1_, u2_, w_, p_) \
-    if ((u1_) < 0 || (u1_) >= IE_U || (u2_) < 0 || (u2_) >= IE_U || (w_) < 0 || (w_) > n || (p_) < 1 || (p_) + (w_) > n) atomicOr(T.err, 16)
+#define CHK(dt, ap_, dh, di) \
+    if ((dt) < 1 || (dt) > t || (ap_) < 0 || (ap_) > t - (dt) || h + (dh) >= m + (dt) || i + (di) < 1 || \
+        i + (di) > m + (dt) - h - (dh)) atomicOr(T.err, 4)
 #else
-#define IE_CHECK(u1_, u2_, w_, p_)
+#define CHK(dt, ap_, dh, di)
 #endif
-#define W2(A, p, q) at2((A), rs, (p), (q))
 
-    int mv;
-    // ---- multiloop-spanning-band recurrences (pseudo_loop.cc:445-644) ----
-    // PLmloop00 (:445-463): seed PL(i,j,k,l) is the not-yet-computed 32767
-    mv = INTERN_INF + bp;
+    // ---- fused a-loop: split point d inside [i, j] ----
+    int pLm00 = INTERN_INF + bp, pLm01 = INF, pLm10 = INF, pMm00 = INTERN_INF + bp, pMm10 = INF;
+    int pOm00 = INTERN_INF + bp, pOm10 = INF;
+    int fL1 = INF, fL2 = INF, fM = INF, fO1 = INF, pK1 = INF;
+#pragma unroll 2
     for (int s = 1; s <= a; ++s) {
-        mv = imin(mv, W2(WB, i, i + s - 1) + L4(PLmloop00, s, a - s, 0, s));
-        mv = imin(mv, L4(PLmloop00, s, a - s, s, 0) + W2(WB, j - s + 1, j));
+        const int r2 = (s - 1) * rs;
+        const int wb_i = WB[r2 + i], wbp_i = WBPr[r2 + i], wp_i = WP[r2 + i];               // (i, i+s-1)
+        const int jl = j - s + 1;
+        const int wb_j = WB[r2 + jl], wbp_j = WBPr[r2 + jl], wp_j = WP[r2 + jl];             // (j-s+1, j)
+        CHK(s, a - s, 0, s);
+        CHK(s, a - s, s, 0);
+        const int xLm00i = RD(PLmloop00, s, a - s, 0, s);  // X(d,j,k,l), d = i+s
+        const int xMm00i = RD(PMmloop00, s, a - s, 0, s);
+        const int xOm00i = RD(POmloop00, s, a - s, 0, s);
+        const int xLm00j = RD(PLmloop00, s, a - s, s, 0);  // X(i,d,k,l), d = j-s
+        const int xMm00j = RD(PMmloop00, s, a - s, s, 0);
+        pLm00 = imin(pLm00, imin(wb_i + xLm00i, xLm00j + wb_j));   // :449-458
+        pLm01 = imin(pLm01, xLm00j + wbp_j);                        // :468-471
+        pLm10 = imin(pLm10, wbp_i + xLm00i);                        // :481-483
+        pMm00 = imin(pMm00, xMm00j + wb_j);                         // :548-551
+        pMm10 = imin(pMm10, wbp_i + xMm00i);                        // :581-584
+        pOm00 = imin(pOm00, wb_i + xOm00i);                         // :599-602
+        pOm10 = imin(pOm10, wbp_i + xOm00i);                        // :632-635
+        if (s < a) {
+            const int xfLi = RD(PfromL, s, a - s, 0, s);
+            const int xfOi = RD(PfromO, s, a - s, 0, s);
+            const int xLm10j = RD(PLmloop10, s, a - s, s, 0);
+            const int xfLj = RD(PfromL, s, a - s, s, 0);
+            const int xfMpj = RD(PfromMprime, s, a - s, s, 0);
+            const int xKj = RD(PK, s, a - s, s, 0);
+            fL1 = imin(fL1, xfLi + wp_i);        // PfromL(d,j,k,l) + WP(i,d-1)  :357-359
+            fO1 = imin(fO1, xfOi + wp_i);        // PfromO(d,j,k,l) + WP(i,d-1)  :425-427
+            pLm10 = imin(pLm10, xLm10j + wb_j);  // PLmloop10(i,d,k,l) + WB(d+1,j) :484-486
+            fL2 = imin(fL2, xfLj + wp_j);        // PfromL(i,d,k,l) + WP(d+1,j)  :360-361
+            fM = imin(fM, xfMpj + wp_j);         // PfromMprime(i,d,k,l) + WP(d+1,j) :399-401
+            pK1 = imin(pK1, xKj + wp_j);         // PK(i,d,k,l) + WP(d+1,j)      :184-187
+        }
     }
-    const int vPLm00 = mv;
-    // PLmloop01 (:465-476)
-    mv = INF;
-    for (int s = 1; s <= a; ++s) mv = imin(mv, L4(PLmloop00, s, a - s, s, 0) + W2(WBPr, j - s + 1, j));
-    const int vPLm01 = mv;
-    // PLmloop10 (:478-493)
-    mv = INF;
-    for (int s = 1; s <= a; ++s) {
-        mv = imin(mv, W2(WBPr, i, i + s - 1) + L4(PLmloop00, s, a - s, 0, s));
-        if (s < a) mv = imin(mv, L4(PLmloop10, a - s, s, a - s, 0) + W2(WB, i + s + 1, j));
+    // ---- fused b-loop: split point d inside [k, l] ----
+    int pRm00 = INTERN_INF + bp, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
+    int fR1 = INF, fR2 = INF, fMp = INF, fO2 = INF, pK2 = INF;
+#pragma unroll 2
+    for (int s = 1; s <= b; ++s) {
+        const int r2 = (s - 1) * rs;
+        const int wb_k = WB[r2 + k], wbp_k = WBPr[r2 + k], wp_k = WP[r2 + k];               // (k, k+s-1)
+        const int ll = l - s + 1;
+        const int wb_l = WB[r2 + ll], wbp_l = WBPr[r2 + ll], wp_l = WP[r2 + ll];             // (l-s+1, l)
+        CHK(s, a, s, 0);
+        CHK(s, a, 0, 0);
+        const int xRm00k = RD(PRmloop00, s, a, s, 0);  // X(i,j,d,l), d = k+s
+        const int xMm00k = RD(PMmloop00, s, a, s, 0);
+        const int xRm00l = RD(PRmloop00, s, a, 0, 0);  // X(i,j,k,d), d = l-s
+        const int xMm00l = RD(PMmloop00, s, a, 0, 0);
+        const int xOm00l = RD(POmloop00, s, a, 0, 0);
+        pRm00 = imin(pRm00, imin(wb_k + xRm00k, xRm00l + wb_l));   // :499-508
+        pRm10 = imin(pRm10, wbp_k + xRm00k);                        // :534-537
+        pRm01 = imin(pRm01, xRm00l + wbp_l);                        // :520-523
+        pMm00 = imin(pMm00, xMm00k + wb_k);                         // :552-555
+        pMm01 = imin(pMm01, xMm00l + wbp_l);                        // :567-570
+        pOm00 = imin(pOm00, xOm00l + wb_l);                         // :603-606
+        pOm01 = imin(pOm01, xOm00l + wbp_l);                        // :618-621
+        if (s < b) {
+            const int xfRk = RD(PfromR, s, a, s, 0);
+            const int xPLk = RD(PL, s, a, s, 0);
+            const int xPRk = RD(PR, s, a, s, 0);
+            const int xKk = RD(PK, s, a, s, 0);
+            const int xMm10l = RD(PMmloop10, s, a, 0, 0);
+            const int xOm10l = RD(POmloop10, s, a, 0, 0);
+            const int xfRl = RD(PfromR, s, a, 0, 0);
+            const int xfOl = RD(PfromO, s, a, 0, 0);
+            fR1 = imin(fR1, xfRk + wp_k);                     // PfromR(i,j,d,l) + WP(k,d-1)  :379-381
+            fMp = imin(fMp, imin(xPLk, xPRk) + PB + wp_k);    // PfromM'' (:663-679) + WP(k,d-1) :412-414
+            pK2 = imin(pK2, xKk + wp_k);                      // PK(i,j,d,l) + WP(k,d-1)      :189-192
+            pMm10 = imin(pMm10, xMm10l + wb_l);               // PMmloop10(i,j,k,d) + WB(d+1,l) :585-588
+            pOm10 = imin(pOm10, xOm10l + wb_l);               // POmloop10(i,j,k,d) + WB(d+1,l) :636-639
+            fR2 = imin(fR2, xfRl + wp_l);                     // PfromR(i,j,k,d) + WP(d+1,l)  :382-383
+            fO2 = imin(fO2, xfOl + wp_l);                     // PfromO(i,j,k,d) + WP(d+1,l)  :429-431
+        }
     }
-    const int vPLm10 = mv;
-    // PRmloop00 (:495-513)
-    mv = INTERN_INF + bp;
-    for (int s = 1; s <= b; ++s) mv = imin(mv, W2(WB, k, k + s - 1) + L4(PRmloop00, s, a, s, 0));
-    for (int s = 0; s < b; ++s) mv = imin(mv, L4(PRmloop00, b - s, a, 0, 0) + W2(WB, k + s + 1, l));
-    const int vPRm00 = mv;
-    // PRmloop01 (:516-528)
-    mv = (b >= 1 ? L4(PRmloop01, 1, a, 0, 0) : INF) + cp;
-    for (int s = 0; s < b; ++s) mv = imin(mv, L4(PRmloop00, b - s, a, 0, 0) + W2(WBPr, k + s + 1, l));
-    const int vPRm01 = mv;
-    // PRmloop10 (:530-542)
-    mv = (b >= 1 ? L4(PRmloop10, 1, a, 1, 0) : INF) + cp;
-    for (int s = 1; s <= b; ++s) mv = imin(mv, W2(WBPr, k, k + s - 1) + L4(PRmloop00, s, a, s, 0));
-    const int vPRm10 = mv;
-    // PMmloop00 (:544-560)
-    mv = INTERN_INF + bp;
-    for (int s = 1; s <= a; ++s) mv = imin(mv, L4(PMmloop00, s, a - s, s, 0) + W2(WB, j - s + 1, j));
-    for (int s = 1; s <= b; ++s) mv = imin(mv, L4(PMmloop00, s, a, s, 0) + W2(WB, k, k + s - 1));
-    const int vPMm00 = mv;
-    // PMmloop01 (:563-575)
-    mv = (b >= 1 ? L4(PMmloop01, 1, a, 1, 0) : INF) + cp;
-    for (int s = 0; s < b; ++s) mv = imin(mv, L4(PMmloop00, b - s, a, 0, 0) + W2(WBPr, k + s + 1, l));
-    const int vPMm01 = mv;
-    // PMmloop10 (:577-593)
-    mv = (a >= 1 ? L4(PMmloop10, 1, a - 1, 1, 0) : INF) + cp;
-    for (int s = 1; s <= a; ++s) mv = imin(mv, W2(WBPr, i, i + s - 1) + L4(PMmloop00, s, a - s, 0, s));
-    for (int s = 1; s < b; ++s) mv = imin(mv, L4(PMmloop10, b - s, a, 0, 0) + W2(WB, k + s + 1, l));
-    const int vPMm10 = mv;
-    // POmloop00 (:595-612)
-    mv = INTERN_INF + bp;
-    for (int s = 1; s <= a; ++s) mv = imin(mv, W2(WB, i, i + s - 1) + L4(POmloop00, s, a - s, 0, s));
-    for (int s = 0; s < b; ++s) mv = imin(mv, L4(POmloop00, b - s, a, 0, 0) + W2(WB, k + s + 1, l));
-    const int vPOm00 = mv;
-    // POmloop01 (:615-627)
-    mv = INF;
-    for (int s = 0; s < b; ++s) mv = imin(mv, L4(POmloop00, b - s, a, 0, 0) + W2(WBPr, k + s + 1, l));
-    const int vPOm01 = mv;
-    // POmloop10 (:629-644)
-    mv = INF;
-    for (int s = 1; s <= a; ++s) mv = imin(mv, W2(WBPr, i, i + s - 1) + L4(POmloop00, s, a - s, 0, s));
-    for (int s = 1; s < b; ++s) mv = imin(mv, L4(POmloop10, b - s, a, 0, 0) + W2(WB, k + s + 1, l));
-    const int vPOm10 = mv;
+    // ---- single-step seeds (:519, :533, :566, :580)
+    const int vPRm01 = imin((b >= 1 ? RD(PRmloop01, 1, a, 0, 0) : INF) + cp, pRm01);
+    const int vPRm10 = imin((b >= 1 ? RD(PRmloop10, 1, a, 1, 0) : INF) + cp, pRm10);
+    const int vPMm01 = imin((b >= 1 ? RD(PMmloop01, 1, a, 1, 0) : INF) + cp, pMm01);
+    const int vPMm10 = imin((a >= 1 ? RD(PMmloop10, 1, a - 1, 1, 0) : INF) + cp, pMm10);
+    const int vPLm00 = pLm00, vPLm01 = pLm01, vPLm10 = pLm10, vPRm00 = pRm00, vPMm00 = pMm00;
+    const int vPOm00 = pOm00, vPOm01 = pOm01, vPOm10 = pOm10;
 
-    const size_t ie_w = (size_t)(n + 1) * rs;  // stride between (u1,u2) planes of IE
+    const int ie_w = (n + 1) * rs;  // stride between (u1,u2) planes of IE
     // ---- PL (:232-253) with get_PLiloop (:682-703), get_PLmloop (:705-715)
     int vPL = INF;
     if (ptype(T, i, j) > 0) {
         int b1 = INF;
         if (a > TURN) {
-            if (a > TURN + 2) b1 = L4(PL, 2, a - 2, 1, 1) + W2(T.est, i, j);
+            if (a > TURN + 2) b1 = RD(PL, 2, a - 2, 1, 1) + W2E(T.est, i, j);
             const int mu1 = imin(a, MAXLOOP) - 2;
             for (int u1 = 0; u1 <= mu1; ++u1) {
                 const int mu2 = imin(a - u1 - 6, MAXLOOP - 2);
-                const int16_t *ie = T.ie + (size_t)(u1 * IE_U) * ie_w + (size_t)a * rs + i;
+                const int16_t *ie = T.ie + (u1 * IE_U * ie_w + a * rs + i);
+#pragma unroll 4
                 for (int u2 = 0; u2 <= mu2; ++u2) {
                     IE_CHECK(u1, u2, a, i);
-                    b1 = imin(b1, (int)ie[u2 * ie_w] + L4(PL, 2 + u1 + u2, a - 2 - u1 - u2, u2 + 1, 1 + u1));
+                    CHK(2 + u1 + u2, a - 2 - u1 - u2, u2 + 1, 1 + u1);
+                    b1 = imin(b1, (int)ie[u2 * ie_w] + RD(PL, 2 + u1 + u2, a - 2 - u1 - u2, u2 + 1, 1 + u1));
                 }
             }
         }
-        const int b2 = (a >= 2) ? imin(L4(PLmloop10, 2, a - 2, 1, 1), L4(PLmloop01, 2, a - 2, 1, 1)) + apbp2 : INF;
-        const int b3 = (a >= TURN + 1) ? L4(PfromL, 2, a - 2, 1, 1) : INF;
+        const int b2 = (a >= 2) ? imin(RD(PLmloop10, 2, a - 2, 1, 1), RD(PLmloop01, 2, a - 2, 1, 1)) + apbp2 : INF;
+        const int b3 = (a >= TURN + 1) ? RD(PfromL, 2, a - 2, 1, 1) : INF;
         vPL = imin(imin(b1, b2), b3);
     }
     // ---- PR (:255-275) with get_PRiloop (:717-738), get_PRmloop (:740-750)
@@ -456,19 +531,21 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
     if (ptype(T, k, l) > 0) {
         int b1 = INF;
         if (b > TURN) {
-            if (b > TURN + 2) b1 = L4(PR, 2, a, 1, 0) + W2(T.est, k, l);
+            if (b > TURN + 2) b1 = RD(PR, 2, a, 1, 0) + W2E(T.est, k, l);
             const int mu1 = imin(b, MAXLOOP) - 2;
             for (int u1 = 0; u1 <= mu1; ++u1) {
                 const int mu2 = imin(b - u1 - 6, MAXLOOP - 2);
-                const int16_t *ie = T.ie + (size_t)(u1 * IE_U) * ie_w + (size_t)b * rs + k;
+                const int16_t *ie = T.ie + (u1 * IE_U * ie_w + b * rs + k);
+#pragma unroll 4
                 for (int u2 = 0; u2 <= mu2; ++u2) {
                     IE_CHECK(u1, u2, b, k);
-                    b1 = imin(b1, (int)ie[u2 * ie_w] + L4(PR, 2 + u1 + u2, a, 1 + u1, 0));
+                    CHK(2 + u1 + u2, a, 1 + u1, 0);
+                    b1 = imin(b1, (int)ie[u2 * ie_w] + RD(PR, 2 + u1 + u2, a, 1 + u1, 0));
                 }
             }
         }
-        const int b2 = (b >= 2) ? imin(L4(PRmloop10, 2, a, 1, 0), L4(PRmloop01, 2, a, 1, 0)) + apbp2 : INF;
-        const int b3 = (b >= TURN + 1) ? L4(PfromR, 2, a, 1, 0) : INF;
+        const int b2 = (b >= 2) ? imin(RD(PRmloop10, 2, a, 1, 0), RD(PRmloop01, 2, a, 1, 0)) + apbp2 : INF;
+        const int b3 = (b >= TURN + 1) ? RD(PfromR, 2, a, 1, 0) : INF;
         vPR = imin(imin(b1, b2), b3);
     }
     // ---- PM (:277-300) with get_PMiloop (:752-773), get_PMmloop (:775-785)
@@ -477,20 +554,21 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
         int b1 = INF;
         const bool inner = (a >= 1 && b >= 1);
         if (g > TURN) {
-            if (inner) b1 = L4(PM, 2, a - 1, 2, 0) + W2(T.est, j - 1, k + 1);
+            if (inner) b1 = RD(PM, 2, a - 1, 2, 0) + W2E(T.est, j - 1, k + 1);
             const int mu1 = imin(a - 2, MAXLOOP - 2);
             const int mu2 = imin(b - 2, MAXLOOP - 2);
             for (int u1 = 0; u1 <= mu1; ++u1) {
-                const int16_t *ie = T.ie + (size_t)(u1 * IE_U) * ie_w + (size_t)(g + 2 + u1) * rs + (j - 1 - u1);
+                const int16_t *ie = T.ie + (u1 * IE_U * ie_w + (g + 2 + u1) * rs + (j - 1 - u1));
+#pragma unroll 4
                 for (int u2 = 0; u2 <= mu2; ++u2) {
                     IE_CHECK(u1, u2, g + 2 + u1 + u2, j - 1 - u1);
-                    b1 = imin(b1, (int)ie[(size_t)u2 * ie_w + (size_t)u2 * rs] +
-                                      L4(PM, 2 + u1 + u2, a - 1 - u1, 2 + u1 + u2, 0));
+                    CHK(2 + u1 + u2, a - 1 - u1, 2 + u1 + u2, 0);
+                    b1 = imin(b1, (int)ie[u2 * (ie_w + rs)] + RD(PM, 2 + u1 + u2, a - 1 - u1, 2 + u1 + u2, 0));
                 }
             }
         }
-        const int b2 = inner ? imin(L4(PMmloop10, 2, a - 1, 2, 0), L4(PMmloop01, 2, a - 1, 2, 0)) + apbp2 : INF;
-        const int b3 = inner ? L4(PfromM, 2, a - 1, 2, 0) : INF;
+        const int b2 = inner ? imin(RD(PMmloop10, 2, a - 1, 2, 0), RD(PMmloop01, 2, a - 1, 2, 0)) + apbp2 : INF;
+        const int b3 = inner ? RD(PfromM, 2, a - 1, 2, 0) : INF;
         const int b4 = (a == 0 && b == 0) ? 0 : INF;
         vPM = imin(imin(b1, b2), imin(b3, b4));
     }
@@ -499,58 +577,28 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
     if (ptype(T, i, l) > 0) {
         const bool inner = (a >= 1 && b >= 1);
         int b1 = INF;
-        if (l - i > TURN && inner) b1 = L4(PO, 2, a - 1, 0, 1) + W2(T.est, i, l);
-        const int b2 = inner ? imin(L4(POmloop10, 2, a - 1, 0, 1), L4(POmloop01, 2, a - 1, 0, 1)) + apbp2 : INF;
-        const int b3 = (inner && l - i >= TURN + 1) ? L4(PfromO, 2, a - 1, 0, 1) : INF;
+        if (l - i > TURN && inner) b1 = RD(PO, 2, a - 1, 0, 1) + W2E(T.est, i, l);
+        const int b2 = inner ? imin(RD(POmloop10, 2, a - 1, 0, 1), RD(POmloop01, 2, a - 1, 0, 1)) + apbp2 : INF;
+        const int b3 = (inner && l - i >= TURN + 1) ? RD(PfromO, 2, a - 1, 0, 1) : INF;
         vPO = imin(imin(b1, b2), b3);
     }
+#undef RD
+#undef CHK
     // values as stored (Matrix4D::set clamp / never-set 32767), read back by same-cell terms
     const int sPL = clamp_store(vPL), sPR = clamp_store(vPR), sPM = clamp_store(vPM), sPO = clamp_store(vPO);
-
-    // ---- PfromL (:354-374)
-    int b1 = INF, b2 = INF;
-    for (int s = 1; s < a; ++s) {
-        b1 = imin(b1, L4(PfromL, s, a - s, 0, s) + W2(WP, i, i + s - 1));
-        b2 = imin(b2, L4(PfromL, a - s, s, a - s, 0) + W2(WP, i + s + 1, j));
-    }
-    const int vPfromL = imin(imin(b1, b2), imin(imin(sPR, sPM), sPO) + PB);
-    // ---- PfromR (:376-394)
-    b1 = INF; b2 = INF;
-    for (int s = 1; s < b; ++s) {
-        b1 = imin(b1, L4(PfromR, s, a, s, 0) + W2(WP, k, k + s - 1));
-        b2 = imin(b2, L4(PfromR, b - s, a, 0, 0) + W2(WP, k + s + 1, l));
-    }
-    const int vPfromR = imin(imin(b1, b2), imin(sPM, sPO) + PB);
-    // ---- PfromM (:396-407)
-    mv = INF;
-    for (int s = 1; s < a; ++s) mv = imin(mv, L4(PfromMprime, a - s, s, a - s, 0) + W2(WP, i + s + 1, j));
-    const int vPfromM = mv;
-    // ---- PfromMprime (:409-420) with get_PfromMdoubleprime (:663-679); d < l so never the base case
-    mv = INF;
-    for (int s = 1; s < b; ++s)
-        mv = imin(mv, imin(L4(PL, s, a, s, 0), L4(PR, s, a, s, 0)) + PB + W2(WP, k, k + s - 1));
-    const int vPfromMp = mv;
-    // ---- PfromO (:422-443)
-    b1 = INF; b2 = INF;
-    for (int s = 1; s < a; ++s) b1 = imin(b1, L4(PfromO, s, a - s, 0, s) + W2(WP, i, i + s - 1));
-    for (int s = 1; s < b; ++s) b2 = imin(b2, L4(PfromO, b - s, a, 0, 0) + W2(WP, k + s + 1, l));
-    const int vPfromO = imin(imin(b1, b2), imin(sPL, sPR) + PB);
-    // ---- PK (:181-202)
-    b1 = INF; b2 = INF;
-    for (int s = 1; s < a; ++s) b1 = imin(b1, L4(PK, a - s, s, a - s, 0) + W2(WP, i + s + 1, j));
-    for (int s = 1; s < b; ++s) b2 = imin(b2, L4(PK, s, a, s, 0) + W2(WP, k, k + s - 1));
-    const int vPK = imin(imin(b1, b2), imin(imin(sPL, sPM), imin(sPR, sPO)) + PB);
-#undef L4
-#undef W2
-#undef IE_CHECK
+    const int vPfromL = imin(imin(fL1, fL2), imin(imin(sPR, sPM), sPO) + PB);   // :354-374
+    const int vPfromR = imin(imin(fR1, fR2), imin(sPM, sPO) + PB);             // :376-394
+    const int vPfromM = fM;                                                     // :396-407
+    const int vPfromMp = fMp;                                                   // :409-420
+    const int vPfromO = imin(imin(fO1, fO2), imin(sPL, sPR) + PB);             // :422-443
+    const int vPK = imin(imin(pK1, pK2), imin(imin(sPL, sPM), imin(sPR, sPO)) + PB);  // :181-202
 
     // ---- stores: one coalesced int16 per matrix
-    const LevelDesc &L = T.lv[t];
+    const int C = T.lv[t].C;
+    int16_t *dst = T.d4 + T.lb[t] + (long long)a * Mt + L0;
 #ifdef CCJ_DEBUG_BOUNDS
     if (i < 1 || i > m - h || h >= m) { atomicOr(T.err, 32); return; }
 #endif
-    int16_t *dst = L.base + a * L.M + Gh + (i - 1);
-    const int C = L.C;
     dst[PK * C] = (int16_t)clamp_store(vPK);
     dst[PL * C] = (int16_t)sPL;
     dst[PR * C] = (int16_t)sPR;
@@ -593,6 +641,18 @@ extern "C" int ccjk_diag2d(const DevTables *T, int sigma, void *stream) {
     const int nb = T->n - sigma;
     if (nb <= 0) return 0;
     hipLaunchKernelGGL(k_diag2d, dim3(nb), dim3(256), 0, (hipStream_t)stream, *T, sigma);
+    return (int)hipGetLastError();
+}
+
+extern "C" int ccjk_pterm(const DevTables *T, int sigma, void *stream) {
+    if (sigma < 3) return 0;
+    const int nint = T->n - sigma;
+    if (nint <= 0) return 0;
+    const int ngroups = (nint + 63) / 64;
+    const int nchunks = (sigma - 2 + PT_CHUNK - 1) / PT_CHUNK;
+    const int waves = nchunks * ngroups;
+    dim3 grid((waves + 3) / 4, sigma - 2);
+    hipLaunchKernelGGL(k_pterm, grid, dim3(256), 0, (hipStream_t)stream, *T, sigma, ngroups, nchunks);
     return (int)hipGetLastError();
 }
 

@@ -1,0 +1,26 @@
+"""Per-level kernel times of one n-nt fold (HIP events on the fill stream)."""
+import ctypes
+import json
+import os
+import random
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ccj_amd import W_final, lib  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+r = random.Random(5)
+seq = "".join(r.choice("ACGU") for _ in range(n))
+wf = W_final(seq, 2, params="Turner04")
+wf.fill()
+wf.fill()
+L = lib()
+L.ccj_level_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+lv = (ctypes.c_double * n)()
+dg = (ctypes.c_double * n)()
+L.ccj_level_times(wf._h, lv, dg, n)
+tm = wf.timing()
+print(json.dumps(tm))
+for t in range(0, n, max(1, n // 25)):
+    print(f"t={t:4d} level4d {lv[t]*1e3:9.1f} us   diag2d {dg[t]*1e3:8.1f} us")
+print("sum level", sum(lv), "sum diag", sum(dg))
