@@ -22,9 +22,10 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# CCJ_LIB_VARIANT=dbg selects the bounds-checked debug build (libccj_hip_dbg.so)
-_LIB_PATH = os.path.join(_HERE, "lib", "libccj_hip_dbg.so" if os.environ.get("CCJ_LIB_VARIANT") == "dbg"
-                         else "libccj_hip.so")
+# CCJ_LIB_VARIANT=dbg selects the bounds-checked debug build (libccj_hip_dbg.so); other variants
+# (libccj_hip_<name>.so) are timing-only ablation builds made by tools/ablate.sh.
+_VARIANT = os.environ.get("CCJ_LIB_VARIANT", "")
+_LIB_PATH = os.path.join(_HERE, "lib", f"libccj_hip_{_VARIANT}.so" if _VARIANT else "libccj_hip.so")
 PARAM_DIR = os.path.join(_HERE, "params")
 
 # ccj.h enums
@@ -108,6 +109,8 @@ def lib() -> ctypes.CDLL:
     L.ccj_destroy.restype = None
     L.ccj_num_cells.argtypes = [ip]
     L.ccj_num_cells.restype = ctypes.c_uint64
+    L.ccj_host_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+    L.ccj_host_timing.restype = ip
     _lib = L
     return L
 
@@ -227,7 +230,10 @@ class W_final:
         f = ctypes.c_double()
         k = (ctypes.c_double * 3)()
         lib().ccj_last_timing(self._h, ctypes.byref(f), k)
-        return {"fill_ms": f.value, "level4d_ms": k[0], "diag2d_ms": k[1], "precompute_ms": k[2]}
+        hst = (ctypes.c_double * 3)()
+        lib().ccj_host_timing(self._h, hst)
+        return {"fill_ms": f.value, "level4d_ms": k[0], "diag2d_ms": k[1], "precompute_ms": k[2],
+                "host_mirror_wait_ms": hst[0], "W_ms": hst[1], "backtrack_ms": hst[2]}
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

@@ -76,4 +76,5 @@ int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
 int ccjk_diag2d(const ccj::DevTables *T, int sigma, void *stream);
 int ccjk_level4d(const ccj::DevTables *T, int t, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
+int ccjk_pp_argmin(const ccj::DevTables *T, int i, int l, int target, unsigned long long *d_out, void *stream);
 }

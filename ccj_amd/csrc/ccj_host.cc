@@ -102,6 +102,7 @@ struct ccj_ctx {
     ccj_energy_params *d_prm = nullptr;
     LevelDesc *d_lv = nullptr;
     long long *d_lb = nullptr;
+    unsigned long long *d_key = nullptr;  // P_P argmin result
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
     int8_t *d_vt = nullptr;
     hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr;
@@ -121,6 +122,7 @@ struct ccj_ctx {
     std::vector<int> W;
 
     double fill_ms = 0, level_ms = 0, diag_ms = 0, pre_ms = 0;
+    double sync_ms = 0, w_ms = 0, bt_ms = 0;  // host side of the last fold
     std::string err;
 
     // ---- host accessors (reference getter semantics) ----
@@ -578,14 +580,23 @@ struct Backtracker {
             case P_P: {
                 const int i = cur.i, l = cur.j;
                 if (i >= l) die("border case: This should not have happened!, P_P");
-                int mn = INF, b1;
                 int best_d = 0, best_j = 0, best_k = 0;
-                for (int j = i; j < l; j++)
-                    for (int d = j + 1; d < l; d++)
-                        for (int k = d + 1; k < l; k++) {
-                            b1 = H.g4(PK, i, j, d + 1, k) + H.g4(PK, j + 1, d, k + 1, l);
-                            if (b1 < mn) { mn = b1; best_d = d; best_j = j; best_k = k; }
-                        }
+                // The O(sigma^3) argmin runs on the GPU, which still holds PK: first (j,d,k) in the
+                // reference's loop order whose sum equals the minimum P(i,l).
+                const int target = H.Pg(i, l);
+                if (l - i >= 3 && target < INF / 2) {
+                    unsigned long long key = ~0ull;
+                    const int sigma = l - i;
+                    hipError_t e = hipMemcpyAsync(c->d_key, &key, sizeof key, hipMemcpyHostToDevice, c->st);
+                    if (e == hipSuccess) e = (hipError_t)ccjk_pp_argmin(&c->T, i, l, target, c->d_key, c->st);
+                    if (e == hipSuccess) e = hipMemcpyAsync(&key, c->d_key, sizeof key, hipMemcpyDeviceToHost, c->st);
+                    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+                    if (e != hipSuccess) throw BacktrackExit{2, std::string("CCJ: HIP error in P_P argmin: ") + hipGetErrorString(e) + "\n"};
+                    if (key == ~0ull) throw BacktrackExit{2, "CCJ: P_P argmin found no split matching P(i,l)\n"};
+                    best_j = i + (int)(key / ((unsigned long long)sigma * sigma));
+                    best_d = i + (int)((key / sigma) % sigma);
+                    best_k = i + (int)(key % sigma);
+                }
                 push4(i, best_k, best_j, best_d + 1, P_PK);
                 push4(best_j + 1, l, best_d, best_k + 1, P_PK);
             } break;
@@ -1433,6 +1444,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipMalloc(&c->d_prm, sizeof(ccj_energy_params)));
     HIPCHK(cp, hipMalloc(&c->d_lv, c->lv_host.size() * sizeof(LevelDesc)));
     HIPCHK(cp, hipMalloc(&c->d_lb, c->lv_off.size() * sizeof(long long)));
+    HIPCHK(cp, hipMalloc(&c->d_key, sizeof(unsigned long long)));
     HIPCHK(cp, hipMalloc(&c->d2i, A2_N * plane * sizeof(int)));
     HIPCHK(cp, hipMalloc(&c->d_vt, plane));
     if (c->total4 > 0 && hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
@@ -1618,6 +1630,12 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
 
 extern "C" int ccj_sync_host(ccj_ctx *c) {
     if (!c || !c->filled) return CCJ_E_STATE;
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Rec {
+        ccj_ctx *c;
+        std::chrono::steady_clock::time_point t0;
+        ~Rec() { c->sync_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+    } rec{c, t0};
     HIPCHK(c, hipSetDevice(c->device));
     const size_t plane = (size_t)(c->n + 1) * c->rs;
     if (c->overlap) {
@@ -1640,16 +1658,24 @@ extern "C" int ccj_fill(ccj_ctx *c) {
 extern "C" int ccj_result(ccj_ctx *c, char *structure, double *energy_kcal, char *msgs, int msgs_cap) {
     if (!c) return CCJ_E_ARG;
     if (!c->mirrored) return set_err(c, CCJ_E_STATE, "ccj_result before ccj_fill");
+    const auto t0 = std::chrono::steady_clock::now();
     compute_W(c);
+    const auto t1 = std::chrono::steady_clock::now();
+    c->w_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     HostView H(c);
     Backtracker B(H, c);
     int rc = CCJ_OK;
+    struct Rec {
+        ccj_ctx *c;
+        std::chrono::steady_clock::time_point t1;
+        ~Rec() { c->bt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count(); }
+    } rec{c, t1};
     try {
         B.run();
         B.fill_structure();
     } catch (const BacktrackExit &e) {
         c->err = e.stderr_msg;
-        rc = e.code == 0 ? CCJ_E_INTER_EXIT : CCJ_E_BACKTRACK;
+        rc = e.code == 0 ? CCJ_E_INTER_EXIT : e.code == 2 ? CCJ_E_HIP : CCJ_E_BACKTRACK;
         if (e.code == 134 || e.code == 139) rc = CCJ_E_BACKTRACK;
     }
     if (msgs && msgs_cap > 0) {
@@ -1817,6 +1843,14 @@ extern "C" int ccj_work_model_seq(const char *seq, int noGU, double *out) {
     return work_model(n, S.data(), pairt, out);
 }
 
+extern "C" int ccj_host_timing(const ccj_ctx *c, double *out3) {
+    if (!c || !out3) return CCJ_E_ARG;
+    out3[0] = c->sync_ms;
+    out3[1] = c->w_ms;
+    out3[2] = c->bt_ms;
+    return CCJ_OK;
+}
+
 extern "C" int ccj_level_times(const ccj_ctx *c, double *level_ms, double *diag_ms, int cap) {
     if (!c) return CCJ_E_ARG;
     for (int t = 0; t < cap && t < (int)c->lev_ms_v.size(); ++t) {
@@ -1849,6 +1883,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_prm);
     hipFree(c->d_lv);
     hipFree(c->d_lb);
+    hipFree(c->d_key);
     hipFree(c->d2i);
     hipFree(c->d_vt);
     if (c->h4) hipHostFree(c->h4);

@@ -319,6 +319,35 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
 // (initialised INF+1 = "never set"; every candidate is <= 65534 < INF/2, A-Q4).  Needs PK levels
 // <= sigma-3 only, so it runs on a side stream three levels ahead of k_diag2d(sigma).
 // ------------------------------------------------------------------------------------------
+// Backtrack helper for the P_P case (pseudo_loop.cc:867-896): the first (j,d,k) in the reference
+// loop order (j, then d, then k ascending) whose PK(i,j,d+1,k) + PK(j+1,d,k+1,l) equals P(i,l).
+// Keys are lexicographic in (j,d,k), so an atomicMin over matching keys returns that first one.
+__global__ void k_pp_argmin(DevTables T, int i, int l, int target, unsigned long long *out) {
+    const int sigma = l - i;
+    const int jo = blockIdx.y;
+    const int d_o = jo + 1 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (d_o > sigma - 2) return;
+    const int j = i + jo, d = i + d_o;
+    for (int k = d + 1; k < l; ++k) {
+        const int v = ld4(T, PK, (j - i) + (k - d - 1), j - i, d - 1 - j, i) +
+                      ld4(T, PK, (d - j - 1) + (l - k - 1), d - j - 1, k - 1 - d, j + 1);
+        if (v == target) {
+            const unsigned long long key = ((unsigned long long)jo * (unsigned)sigma + (unsigned)d_o) * (unsigned)sigma +
+                                           (unsigned)(k - i);
+            atomicMin(out, key);
+            return;
+        }
+    }
+}
+
+extern "C" int ccjk_pp_argmin(const DevTables *T, int i, int l, int target, unsigned long long *d_out, void *stream) {
+    const int sigma = l - i;
+    if (sigma < 3) return 0;
+    dim3 grid((sigma + 255) / 256, sigma - 2);
+    hipLaunchKernelGGL(k_pp_argmin, grid, dim3(256), 0, (hipStream_t)stream, *T, i, l, target, d_out);
+    return (int)hipGetLastError();
+}
+
 constexpr int PT_CHUNK = 16;
 
 __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngroups, int nchunks) {
@@ -419,6 +448,9 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
     int pLm00 = INTERN_INF + bp, pLm01 = INF, pLm10 = INF, pMm00 = INTERN_INF + bp, pMm10 = INF;
     int pOm00 = INTERN_INF + bp, pOm10 = INF;
     int fL1 = INF, fL2 = INF, fM = INF, fO1 = INF, pK1 = INF;
+#ifdef CCJ_ABLATE_LINEAR
+    if (a < 0)
+#endif
 #pragma unroll 2
     for (int s = 1; s <= a; ++s) {
         const int r2 = (s - 1) * rs;
@@ -457,6 +489,9 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
     // ---- fused b-loop: split point d inside [k, l] ----
     int pRm00 = INTERN_INF + bp, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
     int fR1 = INF, fR2 = INF, fMp = INF, fO2 = INF, pK2 = INF;
+#ifdef CCJ_ABLATE_LINEAR
+    if (b < 0)
+#endif
 #pragma unroll 2
     for (int s = 1; s <= b; ++s) {
         const int r2 = (s - 1) * rs;
@@ -510,7 +545,11 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
         int b1 = INF;
         if (a > TURN) {
             if (a > TURN + 2) b1 = RD(PL, 2, a - 2, 1, 1) + W2E(T.est, i, j);
+#ifdef CCJ_ABLATE_ILOOP
+            const int mu1 = -1;
+#else
             const int mu1 = imin(a, MAXLOOP) - 2;
+#endif
             for (int u1 = 0; u1 <= mu1; ++u1) {
                 const int mu2 = imin(a - u1 - 6, MAXLOOP - 2);
                 const int16_t *ie = T.ie + (u1 * IE_U * ie_w + a * rs + i);
@@ -532,7 +571,11 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
         int b1 = INF;
         if (b > TURN) {
             if (b > TURN + 2) b1 = RD(PR, 2, a, 1, 0) + W2E(T.est, k, l);
+#ifdef CCJ_ABLATE_ILOOP
+            const int mu1 = -1;
+#else
             const int mu1 = imin(b, MAXLOOP) - 2;
+#endif
             for (int u1 = 0; u1 <= mu1; ++u1) {
                 const int mu2 = imin(b - u1 - 6, MAXLOOP - 2);
                 const int16_t *ie = T.ie + (u1 * IE_U * ie_w + b * rs + k);
@@ -555,7 +598,11 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
         const bool inner = (a >= 1 && b >= 1);
         if (g > TURN) {
             if (inner) b1 = RD(PM, 2, a - 1, 2, 0) + W2E(T.est, j - 1, k + 1);
+#ifdef CCJ_ABLATE_ILOOP
+            const int mu1 = -1;
+#else
             const int mu1 = imin(a - 2, MAXLOOP - 2);
+#endif
             const int mu2 = imin(b - 2, MAXLOOP - 2);
             for (int u1 = 0; u1 <= mu1; ++u1) {
                 const int16_t *ie = T.ie + (u1 * IE_U * ie_w + (g + 2 + u1) * rs + (j - 1 - u1));
@@ -645,6 +692,9 @@ extern "C" int ccjk_diag2d(const DevTables *T, int sigma, void *stream) {
 }
 
 extern "C" int ccjk_pterm(const DevTables *T, int sigma, void *stream) {
+#ifdef CCJ_ABLATE_PTERM
+    return 0;
+#endif
     if (sigma < 3) return 0;
     const int nint = T->n - sigma;
     if (nint <= 0) return 0;

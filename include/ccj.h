@@ -98,6 +98,8 @@ int  ccj_hashes(const ccj_ctx *ctx, uint64_t *out);
 /* Timing of the last ccj_fill_device (ms, HIP events on the fill stream) and of its dominant
  * kernel family: kernel_ms[0] = 4-D level kernels, [1] = 2-D diagonal kernels, [2] = precompute. */
 int  ccj_last_timing(const ccj_ctx *ctx, double *fill_ms, double *kernel_ms3);
+/* Host side of the last fold (ms): out3[0] = wait for the host mirror (D2H tail), [1] = W, [2] = backtrack. */
+int  ccj_host_timing(const ccj_ctx *ctx, double *out3);
 /* Per-level kernel times of the last fill (ms): level_ms[t] (4-D level t), diag_ms[s] (2-D span s). */
 int  ccj_level_times(const ccj_ctx *ctx, double *level_ms, double *diag_ms, int cap);
 

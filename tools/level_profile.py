@@ -12,8 +12,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 r = random.Random(5)
 seq = "".join(r.choice("ACGU") for _ in range(n))
 wf = W_final(seq, 2, params="Turner04")
-wf.fill()
-wf.fill()
+wf.ccj()
+wf.ccj()
 L = lib()
 L.ccj_level_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int]
 lv = (ctypes.c_double * n)()
