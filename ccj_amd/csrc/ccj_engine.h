@@ -35,6 +35,12 @@ struct LevelDesc {
     int pad;
 };
 
+struct Lvl16 {      // per-level descriptor read by the level kernel (one s_load_dwordx4)
+    long long lb;  // element offset of level t in the 4-D storage
+    int C;         // cells per matrix in level t = (t+1)*M
+    int M;         // cells per a-block = m(m+1)/2, m = n-t-2
+};
+
 struct Penalties {  // integer PK penalties, h_globals.hh:7-25
     int PS, PSM, PSP, PB, PUP, PPS, a, b, c, ap, bp, cp;
 };
@@ -59,6 +65,7 @@ struct DevTables {
     const LevelDesc *lv;           // per level t
     int16_t *d4;                   // 4-D storage base
     const long long *lb;           // element offset of level t in d4
+    const Lvl16 *ld;               // per-level descriptors
     int *err;                      // device error word
 };
 

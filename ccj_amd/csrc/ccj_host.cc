@@ -102,6 +102,7 @@ struct ccj_ctx {
     ccj_energy_params *d_prm = nullptr;
     LevelDesc *d_lv = nullptr;
     long long *d_lb = nullptr;
+    Lvl16 *d_ld = nullptr;
     unsigned long long *d_key = nullptr;  // P_P argmin result
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
     int8_t *d_vt = nullptr;
@@ -1444,6 +1445,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipMalloc(&c->d_prm, sizeof(ccj_energy_params)));
     HIPCHK(cp, hipMalloc(&c->d_lv, c->lv_host.size() * sizeof(LevelDesc)));
     HIPCHK(cp, hipMalloc(&c->d_lb, c->lv_off.size() * sizeof(long long)));
+    HIPCHK(cp, hipMalloc(&c->d_ld, c->lv_off.size() * sizeof(Lvl16)));
     HIPCHK(cp, hipMalloc(&c->d_key, sizeof(unsigned long long)));
     HIPCHK(cp, hipMalloc(&c->d2i, A2_N * plane * sizeof(int)));
     HIPCHK(cp, hipMalloc(&c->d_vt, plane));
@@ -1499,6 +1501,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     {
         std::vector<long long> lb(c->lv_off.begin(), c->lv_off.end());
         HIPCHK(cp, hipMemcpy(c->d_lb, lb.data(), lb.size() * sizeof(long long), hipMemcpyHostToDevice));
+        std::vector<Lvl16> ld(c->lv_off.size());
+        for (size_t t = 0; t < ld.size(); ++t) ld[t] = Lvl16{c->lv_off[t], c->lv_host[t].C, c->lv_host[t].M};
+        HIPCHK(cp, hipMemcpy(c->d_ld, ld.data(), ld.size() * sizeof(Lvl16), hipMemcpyHostToDevice));
     }
 
     DevTables &T = c->T;
@@ -1532,6 +1537,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.lv = c->d_lv;
     T.d4 = c->d4;
     T.lb = c->d_lb;
+    T.ld = c->d_ld;
     T.err = c->d_err;
     *out = c.release();
     return CCJ_OK;
@@ -1883,6 +1889,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_prm);
     hipFree(c->d_lv);
     hipFree(c->d_lb);
+    hipFree(c->d_ld);
     hipFree(c->d_key);
     hipFree(c->d2i);
     hipFree(c->d_vt);

@@ -381,26 +381,18 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
 // 4-D level t: one lane per cell (i,j,k,l); all lanes of a wave share (t, a) so every loop bound
 // is wave-uniform.  pseudo_loop.cc:181-644, 663-808.
 //
-// Addressing: a neighbour at (t-dt, a', h+dh, i+di) of matrix x lives at
-//     d4[ LB[t-dt] + x*C' + a'*M' + dh*m + dh*dt - dh(dh-1)/2 + di ]  (wave-uniform, SGPRs)
-//       + L0 + h*(dt-dh)                                              (per lane, VGPR)
-// with L0 = G_t(h) + i - 1 the cell's own in-block offset; every read is a coalesced global load.
+// Addressing.  A neighbour at (t-dt, a', h+dh, i+di) of matrix x is element
+//     x*C' + a'*M' + [dh*m + dh*dt - dh(dh-1)/2 + di]   (wave-uniform: SGPRs)
+//   + L0 + h*(dt-dh)                                   (per lane: VGPR)
+// of level t' = t-dt, whose base/C'/M' come from one 16-byte descriptor (T.ld[t']).  L0 is the
+// cell's own in-block offset.  Loops walk these terms incrementally, so a read costs ~one scalar
+// add plus one vector add; every read is a coalesced global load.
 //
-// The 22 recurrences' split-point loops are fused into one loop over the (i,j) gap ("a-loop")
+// The split-point loops of the 22 recurrences are fused into one loop over the (i,j) gap ("a-loop")
 // and one over the (k,l) gap ("b-loop"): each neighbour value is loaded once and feeds every
-// recurrence that reads it (11a + 13b int16 loads per cell instead of 14a + 16b).
+// recurrence that reads it (11a + 13b loads per cell instead of 14a + 16b).  The interior-loop
+// windows are walked by source level dt (outer) so the level descriptor is loaded once per dt.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ const int16_t *nb_base(const DevTables &T, int x, int t, int m, int dt, int ap, int dh,
-                                                  int di) {
-    const int tp = t - dt;
-    const int mp = m + dt;
-    const int Mp = (mp * (mp + 1)) >> 1;
-    const int Cp = (tp + 1) * Mp;
-    const long long off = T.lb[tp] + (long long)x * Cp + (long long)ap * Mp + (long long)(dh * m + dh * dt) -
-                          ((dh * (dh - 1)) >> 1) + di;
-    return T.d4 + off;
-}
-
 __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPerA) {
 #ifdef CCJ_DEBUG_BOUNDS
     g_dbg_err = T.err;
@@ -427,15 +419,16 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
     const int g = h + 2;
     const int j = i + a, k = j + g, l = k + b;
     const unsigned L0 = (unsigned)(Gh + i - 1);
+    const unsigned uh = (unsigned)h;
 
     const Penalties pe = T.pen;
     const int bp = pe.bp, cp = pe.cp, PB = pe.PB, apbp2 = pe.ap + 2 * pe.bp;
     const int *__restrict__ WB = T.WB;
     const int *__restrict__ WP = T.WP;
     const int *__restrict__ WBPr = T.WBP;
-// neighbour read: matrix x at (t-dt, ap, h+dh, i+di); lane offset L0 + h*(dt-dh)
-#define RD(x, dt, ap_, dh, di) \
-    ((int)nb_base(T, (x), t, m, (dt), (ap_), (dh), (di))[L0 + (unsigned)h * (unsigned)((dt) - (dh))])
+    const Lvl16 *__restrict__ LD = T.ld;
+    const int16_t *__restrict__ D4 = T.d4;
+#define LDX(lp, L, x, U, ln) ((int)(lp)[(unsigned)((x) * (L).C + (U)) + (ln)])
 #ifdef CCJ_DEBUG_BOUNDS
 #define CHK(dt, ap_, dh, di) \
     if ((dt) < 1 || (dt) > t || (ap_) < 0 || (ap_) > t - (dt) || h + (dh) >= m + (dt) || i + (di) < 1 || \
@@ -448,147 +441,199 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
     int pLm00 = INTERN_INF + bp, pLm01 = INF, pLm10 = INF, pMm00 = INTERN_INF + bp, pMm10 = INF;
     int pOm00 = INTERN_INF + bp, pOm10 = INF;
     int fL1 = INF, fL2 = INF, fM = INF, fO1 = INF, pK1 = INF;
+    {
+        unsigned lhs = L0;  // L0 + h*s
+        int sjm = 0;        // s*m + s(s+1)/2
 #ifdef CCJ_ABLATE_LINEAR
-    if (a < 0)
+        if (a < 0)
 #endif
 #pragma unroll 2
-    for (int s = 1; s <= a; ++s) {
-        const int r2 = (s - 1) * rs;
-        const int wb_i = WB[r2 + i], wbp_i = WBPr[r2 + i], wp_i = WP[r2 + i];               // (i, i+s-1)
-        const int jl = j - s + 1;
-        const int wb_j = WB[r2 + jl], wbp_j = WBPr[r2 + jl], wp_j = WP[r2 + jl];             // (j-s+1, j)
-        CHK(s, a - s, 0, s);
-        CHK(s, a - s, s, 0);
-        const int xLm00i = RD(PLmloop00, s, a - s, 0, s);  // X(d,j,k,l), d = i+s
-        const int xMm00i = RD(PMmloop00, s, a - s, 0, s);
-        const int xOm00i = RD(POmloop00, s, a - s, 0, s);
-        const int xLm00j = RD(PLmloop00, s, a - s, s, 0);  // X(i,d,k,l), d = j-s
-        const int xMm00j = RD(PMmloop00, s, a - s, s, 0);
-        pLm00 = imin(pLm00, imin(wb_i + xLm00i, xLm00j + wb_j));   // :449-458
-        pLm01 = imin(pLm01, xLm00j + wbp_j);                        // :468-471
-        pLm10 = imin(pLm10, wbp_i + xLm00i);                        // :481-483
-        pMm00 = imin(pMm00, xMm00j + wb_j);                         // :548-551
-        pMm10 = imin(pMm10, wbp_i + xMm00i);                        // :581-584
-        pOm00 = imin(pOm00, wb_i + xOm00i);                         // :599-602
-        pOm10 = imin(pOm10, wbp_i + xOm00i);                        // :632-635
-        if (s < a) {
-            const int xfLi = RD(PfromL, s, a - s, 0, s);
-            const int xfOi = RD(PfromO, s, a - s, 0, s);
-            const int xLm10j = RD(PLmloop10, s, a - s, s, 0);
-            const int xfLj = RD(PfromL, s, a - s, s, 0);
-            const int xfMpj = RD(PfromMprime, s, a - s, s, 0);
-            const int xKj = RD(PK, s, a - s, s, 0);
-            fL1 = imin(fL1, xfLi + wp_i);        // PfromL(d,j,k,l) + WP(i,d-1)  :357-359
-            fO1 = imin(fO1, xfOi + wp_i);        // PfromO(d,j,k,l) + WP(i,d-1)  :425-427
-            pLm10 = imin(pLm10, xLm10j + wb_j);  // PLmloop10(i,d,k,l) + WB(d+1,j) :484-486
-            fL2 = imin(fL2, xfLj + wp_j);        // PfromL(i,d,k,l) + WP(d+1,j)  :360-361
-            fM = imin(fM, xfMpj + wp_j);         // PfromMprime(i,d,k,l) + WP(d+1,j) :399-401
-            pK1 = imin(pK1, xKj + wp_j);         // PK(i,d,k,l) + WP(d+1,j)      :184-187
+        for (int s = 1; s <= a; ++s) {
+            lhs += uh;
+            sjm += m + s;
+            const int r2 = (s - 1) * rs;
+            const int wb_i = WB[r2 + i], wbp_i = WBPr[r2 + i], wp_i = WP[r2 + i];   // (i, i+s-1)
+            const int jl = j - s + 1;
+            const int wb_j = WB[r2 + jl], wbp_j = WBPr[r2 + jl], wp_j = WP[r2 + jl]; // (j-s+1, j)
+            CHK(s, a - s, 0, s);
+            CHK(s, a - s, s, 0);
+            const Lvl16 L = LD[t - s];
+            const int16_t *lp = D4 + L.lb;
+            const int Ui = (a - s) * L.M + s;    // X(d,j,k,l), d = i+s: lane L0 + h*s
+            const int Uj = (a - s) * L.M + sjm;  // X(i,d,k,l), d = j-s: lane L0
+            const int xLm00i = LDX(lp, L, PLmloop00, Ui, lhs);
+            const int xMm00i = LDX(lp, L, PMmloop00, Ui, lhs);
+            const int xOm00i = LDX(lp, L, POmloop00, Ui, lhs);
+            const int xLm00j = LDX(lp, L, PLmloop00, Uj, L0);
+            const int xMm00j = LDX(lp, L, PMmloop00, Uj, L0);
+            pLm00 = imin(pLm00, imin(wb_i + xLm00i, xLm00j + wb_j));   // :449-458
+            pLm01 = imin(pLm01, xLm00j + wbp_j);                        // :468-471
+            pLm10 = imin(pLm10, wbp_i + xLm00i);                        // :481-483
+            pMm00 = imin(pMm00, xMm00j + wb_j);                         // :548-551
+            pMm10 = imin(pMm10, wbp_i + xMm00i);                        // :581-584
+            pOm00 = imin(pOm00, wb_i + xOm00i);                         // :599-602
+            pOm10 = imin(pOm10, wbp_i + xOm00i);                        // :632-635
+            if (s < a) {
+                const int xfLi = LDX(lp, L, PfromL, Ui, lhs);
+                const int xfOi = LDX(lp, L, PfromO, Ui, lhs);
+                const int xLm10j = LDX(lp, L, PLmloop10, Uj, L0);
+                const int xfLj = LDX(lp, L, PfromL, Uj, L0);
+                const int xfMpj = LDX(lp, L, PfromMprime, Uj, L0);
+                const int xKj = LDX(lp, L, PK, Uj, L0);
+                fL1 = imin(fL1, xfLi + wp_i);        // PfromL(d,j,k,l) + WP(i,d-1)  :357-359
+                fO1 = imin(fO1, xfOi + wp_i);        // PfromO(d,j,k,l) + WP(i,d-1)  :425-427
+                pLm10 = imin(pLm10, xLm10j + wb_j);  // PLmloop10(i,d,k,l) + WB(d+1,j) :484-486
+                fL2 = imin(fL2, xfLj + wp_j);        // PfromL(i,d,k,l) + WP(d+1,j)  :360-361
+                fM = imin(fM, xfMpj + wp_j);         // PfromMprime(i,d,k,l) + WP(d+1,j) :399-401
+                pK1 = imin(pK1, xKj + wp_j);         // PK(i,d,k,l) + WP(d+1,j)      :184-187
+            }
         }
     }
     // ---- fused b-loop: split point d inside [k, l] ----
     int pRm00 = INTERN_INF + bp, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
     int fR1 = INF, fR2 = INF, fMp = INF, fO2 = INF, pK2 = INF;
+    {
+        unsigned lhs = L0;
+        int sjm = 0;
 #ifdef CCJ_ABLATE_LINEAR
-    if (b < 0)
+        if (b < 0)
 #endif
 #pragma unroll 2
-    for (int s = 1; s <= b; ++s) {
-        const int r2 = (s - 1) * rs;
-        const int wb_k = WB[r2 + k], wbp_k = WBPr[r2 + k], wp_k = WP[r2 + k];               // (k, k+s-1)
-        const int ll = l - s + 1;
-        const int wb_l = WB[r2 + ll], wbp_l = WBPr[r2 + ll], wp_l = WP[r2 + ll];             // (l-s+1, l)
-        CHK(s, a, s, 0);
-        CHK(s, a, 0, 0);
-        const int xRm00k = RD(PRmloop00, s, a, s, 0);  // X(i,j,d,l), d = k+s
-        const int xMm00k = RD(PMmloop00, s, a, s, 0);
-        const int xRm00l = RD(PRmloop00, s, a, 0, 0);  // X(i,j,k,d), d = l-s
-        const int xMm00l = RD(PMmloop00, s, a, 0, 0);
-        const int xOm00l = RD(POmloop00, s, a, 0, 0);
-        pRm00 = imin(pRm00, imin(wb_k + xRm00k, xRm00l + wb_l));   // :499-508
-        pRm10 = imin(pRm10, wbp_k + xRm00k);                        // :534-537
-        pRm01 = imin(pRm01, xRm00l + wbp_l);                        // :520-523
-        pMm00 = imin(pMm00, xMm00k + wb_k);                         // :552-555
-        pMm01 = imin(pMm01, xMm00l + wbp_l);                        // :567-570
-        pOm00 = imin(pOm00, xOm00l + wb_l);                         // :603-606
-        pOm01 = imin(pOm01, xOm00l + wbp_l);                        // :618-621
-        if (s < b) {
-            const int xfRk = RD(PfromR, s, a, s, 0);
-            const int xPLk = RD(PL, s, a, s, 0);
-            const int xPRk = RD(PR, s, a, s, 0);
-            const int xKk = RD(PK, s, a, s, 0);
-            const int xMm10l = RD(PMmloop10, s, a, 0, 0);
-            const int xOm10l = RD(POmloop10, s, a, 0, 0);
-            const int xfRl = RD(PfromR, s, a, 0, 0);
-            const int xfOl = RD(PfromO, s, a, 0, 0);
-            fR1 = imin(fR1, xfRk + wp_k);                     // PfromR(i,j,d,l) + WP(k,d-1)  :379-381
-            fMp = imin(fMp, imin(xPLk, xPRk) + PB + wp_k);    // PfromM'' (:663-679) + WP(k,d-1) :412-414
-            pK2 = imin(pK2, xKk + wp_k);                      // PK(i,j,d,l) + WP(k,d-1)      :189-192
-            pMm10 = imin(pMm10, xMm10l + wb_l);               // PMmloop10(i,j,k,d) + WB(d+1,l) :585-588
-            pOm10 = imin(pOm10, xOm10l + wb_l);               // POmloop10(i,j,k,d) + WB(d+1,l) :636-639
-            fR2 = imin(fR2, xfRl + wp_l);                     // PfromR(i,j,k,d) + WP(d+1,l)  :382-383
-            fO2 = imin(fO2, xfOl + wp_l);                     // PfromO(i,j,k,d) + WP(d+1,l)  :429-431
+        for (int s = 1; s <= b; ++s) {
+            lhs += uh;
+            sjm += m + s;
+            const int r2 = (s - 1) * rs;
+            const int wb_k = WB[r2 + k], wbp_k = WBPr[r2 + k], wp_k = WP[r2 + k];   // (k, k+s-1)
+            const int ll = l - s + 1;
+            const int wb_l = WB[r2 + ll], wbp_l = WBPr[r2 + ll], wp_l = WP[r2 + ll]; // (l-s+1, l)
+            CHK(s, a, s, 0);
+            CHK(s, a, 0, 0);
+            const Lvl16 L = LD[t - s];
+            const int16_t *lp = D4 + L.lb;
+            const int Uk = a * L.M + sjm;  // X(i,j,d,l), d = k+s: lane L0
+            const int Ul = a * L.M;        // X(i,j,k,d), d = l-s: lane L0 + h*s
+            const int xRm00k = LDX(lp, L, PRmloop00, Uk, L0);
+            const int xMm00k = LDX(lp, L, PMmloop00, Uk, L0);
+            const int xRm00l = LDX(lp, L, PRmloop00, Ul, lhs);
+            const int xMm00l = LDX(lp, L, PMmloop00, Ul, lhs);
+            const int xOm00l = LDX(lp, L, POmloop00, Ul, lhs);
+            pRm00 = imin(pRm00, imin(wb_k + xRm00k, xRm00l + wb_l));   // :499-508
+            pRm10 = imin(pRm10, wbp_k + xRm00k);                        // :534-537
+            pRm01 = imin(pRm01, xRm00l + wbp_l);                        // :520-523
+            pMm00 = imin(pMm00, xMm00k + wb_k);                         // :552-555
+            pMm01 = imin(pMm01, xMm00l + wbp_l);                        // :567-570
+            pOm00 = imin(pOm00, xOm00l + wb_l);                         // :603-606
+            pOm01 = imin(pOm01, xOm00l + wbp_l);                        // :618-621
+            if (s < b) {
+                const int xfRk = LDX(lp, L, PfromR, Uk, L0);
+                const int xPLk = LDX(lp, L, PL, Uk, L0);
+                const int xPRk = LDX(lp, L, PR, Uk, L0);
+                const int xKk = LDX(lp, L, PK, Uk, L0);
+                const int xMm10l = LDX(lp, L, PMmloop10, Ul, lhs);
+                const int xOm10l = LDX(lp, L, POmloop10, Ul, lhs);
+                const int xfRl = LDX(lp, L, PfromR, Ul, lhs);
+                const int xfOl = LDX(lp, L, PfromO, Ul, lhs);
+                fR1 = imin(fR1, xfRk + wp_k);                     // PfromR(i,j,d,l) + WP(k,d-1)  :379-381
+                fMp = imin(fMp, imin(xPLk, xPRk) + PB + wp_k);    // PfromM'' (:663-679) + WP(k,d-1) :412-414
+                pK2 = imin(pK2, xKk + wp_k);                      // PK(i,j,d,l) + WP(k,d-1)      :189-192
+                pMm10 = imin(pMm10, xMm10l + wb_l);               // PMmloop10(i,j,k,d) + WB(d+1,l) :585-588
+                pOm10 = imin(pOm10, xOm10l + wb_l);               // POmloop10(i,j,k,d) + WB(d+1,l) :636-639
+                fR2 = imin(fR2, xfRl + wp_l);                     // PfromR(i,j,k,d) + WP(d+1,l)  :382-383
+                fO2 = imin(fO2, xfOl + wp_l);                     // PfromO(i,j,k,d) + WP(d+1,l)  :429-431
+            }
         }
     }
-    // ---- single-step seeds (:519, :533, :566, :580)
-    const int vPRm01 = imin((b >= 1 ? RD(PRmloop01, 1, a, 0, 0) : INF) + cp, pRm01);
-    const int vPRm10 = imin((b >= 1 ? RD(PRmloop10, 1, a, 1, 0) : INF) + cp, pRm10);
-    const int vPMm01 = imin((b >= 1 ? RD(PMmloop01, 1, a, 1, 0) : INF) + cp, pMm01);
-    const int vPMm10 = imin((a >= 1 ? RD(PMmloop10, 1, a - 1, 1, 0) : INF) + cp, pMm10);
+    // ---- single-step seeds (:519, :533, :566, :580), level t-1
+    int vPRm01 = pRm01, vPRm10 = pRm10, vPMm01 = pMm01, vPMm10 = pMm10;
+    {
+        const int16_t *dummy = D4;
+        (void)dummy;
+        if (t >= 1) {
+            const Lvl16 L = LD[t - 1];
+            const int16_t *lp = D4 + L.lb;
+            if (b >= 1) {
+                vPRm01 = imin(vPRm01, LDX(lp, L, PRmloop01, a * L.M, L0 + uh) + cp);          // (i,j,k,l-1)
+                vPRm10 = imin(vPRm10, LDX(lp, L, PRmloop10, a * L.M + m + 1, L0) + cp);       // (i,j,k+1,l)
+                vPMm01 = imin(vPMm01, LDX(lp, L, PMmloop01, a * L.M + m + 1, L0) + cp);       // (i,j,k+1,l)
+            }
+            if (a >= 1) vPMm10 = imin(vPMm10, LDX(lp, L, PMmloop10, (a - 1) * L.M + m + 1, L0) + cp);  // (i,j-1,k,l)
+        }
+    }
     const int vPLm00 = pLm00, vPLm01 = pLm01, vPLm10 = pLm10, vPRm00 = pRm00, vPMm00 = pMm00;
     const int vPOm00 = pOm00, vPOm01 = pOm01, vPOm10 = pOm10;
 
+    // ---- level t-2 neighbours of PL/PR/PM/PO (stack terms, get_P?mloop, PfromX)
+    const Lvl16 L2 = LD[t >= 2 ? t - 2 : 0];
+    const int16_t *lp2 = D4 + L2.lb;
     const int ie_w = (n + 1) * rs;  // stride between (u1,u2) planes of IE
     // ---- PL (:232-253) with get_PLiloop (:682-703), get_PLmloop (:705-715)
     int vPL = INF;
     if (ptype(T, i, j) > 0) {
         int b1 = INF;
+        const int Uin = (a - 2) * L2.M + m + 3;  // (i+1, j-1, k, l): lane L0 + h
         if (a > TURN) {
-            if (a > TURN + 2) b1 = RD(PL, 2, a - 2, 1, 1) + W2E(T.est, i, j);
-#ifdef CCJ_ABLATE_ILOOP
-            const int mu1 = -1;
-#else
+            if (a > TURN + 2) b1 = LDX(lp2, L2, PL, Uin, L0 + uh) + W2E(T.est, i, j);
             const int mu1 = imin(a, MAXLOOP) - 2;
+#ifdef CCJ_ABLATE_ILOOP
+            if (a < 0)
 #endif
-            for (int u1 = 0; u1 <= mu1; ++u1) {
-                const int mu2 = imin(a - u1 - 6, MAXLOOP - 2);
-                const int16_t *ie = T.ie + (u1 * IE_U * ie_w + a * rs + i);
+            for (int dt = 2; dt <= a - 4; ++dt) {
+                const Lvl16 L = LD[t - dt];
+                const int16_t *lp = D4 + L.lb + (long long)PL * L.C;
+                const int u1lo = imax(0, dt - 30), u1hi = imin(dt - 2, mu1);
+                int dh = dt - 1 - u1lo;  // candidate (d,dp) = (i+1+u1, j-1-u2), u2 = dt-2-u1
+                int U = (a - dt) * L.M + dh * m + dh * dt - ((dh * (dh - 1)) >> 1) + 1 + u1lo;
+                unsigned ln = L0 + uh * (unsigned)(1 + u1lo);
+                int ieo = (u1lo * IE_U + (dt - 2 - u1lo)) * ie_w + a * rs;
 #pragma unroll 4
-                for (int u2 = 0; u2 <= mu2; ++u2) {
-                    IE_CHECK(u1, u2, a, i);
-                    CHK(2 + u1 + u2, a - 2 - u1 - u2, u2 + 1, 1 + u1);
-                    b1 = imin(b1, (int)ie[u2 * ie_w] + RD(PL, 2 + u1 + u2, a - 2 - u1 - u2, u2 + 1, 1 + u1));
+                for (int u1 = u1lo; u1 <= u1hi; ++u1) {
+                    IE_CHECK(u1, dt - 2 - u1, a, i);
+                    CHK(dt, a - dt, dh, 1 + u1);
+                    b1 = imin(b1, (int)T.ie[ieo + i] + (int)lp[(unsigned)U + ln]);
+                    U += dh - m - dt;
+                    --dh;
+                    ln += uh;
+                    ieo += (IE_U - 1) * ie_w;
                 }
             }
         }
-        const int b2 = (a >= 2) ? imin(RD(PLmloop10, 2, a - 2, 1, 1), RD(PLmloop01, 2, a - 2, 1, 1)) + apbp2 : INF;
-        const int b3 = (a >= TURN + 1) ? RD(PfromL, 2, a - 2, 1, 1) : INF;
+        const int b2 = (a >= 2) ? imin(LDX(lp2, L2, PLmloop10, Uin, L0 + uh), LDX(lp2, L2, PLmloop01, Uin, L0 + uh)) + apbp2 : INF;
+        const int b3 = (a >= TURN + 1) ? LDX(lp2, L2, PfromL, Uin, L0 + uh) : INF;
         vPL = imin(imin(b1, b2), b3);
     }
     // ---- PR (:255-275) with get_PRiloop (:717-738), get_PRmloop (:740-750)
     int vPR = INF;
     if (ptype(T, k, l) > 0) {
         int b1 = INF;
+        const int Uin = a * L2.M + m + 2;  // (i, j, k+1, l-1): lane L0 + h
         if (b > TURN) {
-            if (b > TURN + 2) b1 = RD(PR, 2, a, 1, 0) + W2E(T.est, k, l);
-#ifdef CCJ_ABLATE_ILOOP
-            const int mu1 = -1;
-#else
+            if (b > TURN + 2) b1 = LDX(lp2, L2, PR, Uin, L0 + uh) + W2E(T.est, k, l);
             const int mu1 = imin(b, MAXLOOP) - 2;
+#ifdef CCJ_ABLATE_ILOOP
+            if (b < 0)
 #endif
-            for (int u1 = 0; u1 <= mu1; ++u1) {
-                const int mu2 = imin(b - u1 - 6, MAXLOOP - 2);
-                const int16_t *ie = T.ie + (u1 * IE_U * ie_w + b * rs + k);
+            for (int dt = 2; dt <= b - 4; ++dt) {
+                const Lvl16 L = LD[t - dt];
+                const int16_t *lp = D4 + L.lb + (long long)PR * L.C;
+                const int u1lo = imax(0, dt - 30), u1hi = imin(dt - 2, mu1);
+                int dh = 1 + u1lo;  // candidate (d,dp) = (k+1+u1, l-1-u2)
+                int U = a * L.M + dh * m + dh * dt - ((dh * (dh - 1)) >> 1);
+                unsigned ln = L0 + uh * (unsigned)(dt - 1 - u1lo);
+                int ieo = (u1lo * IE_U + (dt - 2 - u1lo)) * ie_w + b * rs;
 #pragma unroll 4
-                for (int u2 = 0; u2 <= mu2; ++u2) {
-                    IE_CHECK(u1, u2, b, k);
-                    CHK(2 + u1 + u2, a, 1 + u1, 0);
-                    b1 = imin(b1, (int)ie[u2 * ie_w] + RD(PR, 2 + u1 + u2, a, 1 + u1, 0));
+                for (int u1 = u1lo; u1 <= u1hi; ++u1) {
+                    IE_CHECK(u1, dt - 2 - u1, b, k);
+                    CHK(dt, a, dh, 0);
+                    b1 = imin(b1, (int)T.ie[ieo + k] + (int)lp[(unsigned)U + ln]);
+                    U += m + dt - dh;
+                    ++dh;
+                    ln -= uh;
+                    ieo += (IE_U - 1) * ie_w;
                 }
             }
         }
-        const int b2 = (b >= 2) ? imin(RD(PRmloop10, 2, a, 1, 0), RD(PRmloop01, 2, a, 1, 0)) + apbp2 : INF;
-        const int b3 = (b >= TURN + 1) ? RD(PfromR, 2, a, 1, 0) : INF;
+        const int b2 = (b >= 2) ? imin(LDX(lp2, L2, PRmloop10, Uin, L0 + uh), LDX(lp2, L2, PRmloop01, Uin, L0 + uh)) + apbp2 : INF;
+        const int b3 = (b >= TURN + 1) ? LDX(lp2, L2, PfromR, Uin, L0 + uh) : INF;
         vPR = imin(imin(b1, b2), b3);
     }
     // ---- PM (:277-300) with get_PMiloop (:752-773), get_PMmloop (:775-785)
@@ -596,26 +641,35 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
     if (ptype(T, j, k) > 0) {
         int b1 = INF;
         const bool inner = (a >= 1 && b >= 1);
+        const int Uin = (a - 1) * L2.M + 2 * m + 3;  // (i, j-1, k+1, l): lane L0
         if (g > TURN) {
-            if (inner) b1 = RD(PM, 2, a - 1, 2, 0) + W2E(T.est, j - 1, k + 1);
-#ifdef CCJ_ABLATE_ILOOP
-            const int mu1 = -1;
-#else
+            if (inner) b1 = LDX(lp2, L2, PM, Uin, L0) + W2E(T.est, j - 1, k + 1);
             const int mu1 = imin(a - 2, MAXLOOP - 2);
-#endif
             const int mu2 = imin(b - 2, MAXLOOP - 2);
-            for (int u1 = 0; u1 <= mu1; ++u1) {
-                const int16_t *ie = T.ie + (u1 * IE_U * ie_w + (g + 2 + u1) * rs + (j - 1 - u1));
+#ifdef CCJ_ABLATE_ILOOP
+            if (a < 0)
+#endif
+            if (mu1 >= 0 && mu2 >= 0)
+                for (int dt = 2; dt <= 2 + mu1 + mu2; ++dt) {
+                    const Lvl16 L = LD[t - dt];
+                    const int16_t *lp = D4 + L.lb + (long long)PM * L.C;
+                    const int u1lo = imax(0, dt - 2 - mu2), u1hi = imin(dt - 2, mu1);
+                    // candidate (d,dp) = (j-1-u1, k+1+u2): PM(i,d,dp,l) = (t-dt, a-1-u1, h+dt, i), lane L0
+                    int U = (a - 1 - u1lo) * L.M + dt * m + dt * dt - ((dt * (dt - 1)) >> 1);
+                    const int lpm = (g + dt) * rs + j - 1;  // IE outer span g+dt, start j-1-u1
+                    int ieo = (u1lo * IE_U + (dt - 2 - u1lo)) * ie_w - u1lo;
 #pragma unroll 4
-                for (int u2 = 0; u2 <= mu2; ++u2) {
-                    IE_CHECK(u1, u2, g + 2 + u1 + u2, j - 1 - u1);
-                    CHK(2 + u1 + u2, a - 1 - u1, 2 + u1 + u2, 0);
-                    b1 = imin(b1, (int)ie[u2 * (ie_w + rs)] + RD(PM, 2 + u1 + u2, a - 1 - u1, 2 + u1 + u2, 0));
+                    for (int u1 = u1lo; u1 <= u1hi; ++u1) {
+                        IE_CHECK(u1, dt - 2 - u1, g + dt, j - 1 - u1);
+                        CHK(dt, a - 1 - u1, dt, 0);
+                        b1 = imin(b1, (int)T.ie[ieo + lpm] + (int)lp[(unsigned)U + L0]);
+                        U -= L.M;
+                        ieo += (IE_U - 1) * ie_w - 1;
+                    }
                 }
-            }
         }
-        const int b2 = inner ? imin(RD(PMmloop10, 2, a - 1, 2, 0), RD(PMmloop01, 2, a - 1, 2, 0)) + apbp2 : INF;
-        const int b3 = inner ? RD(PfromM, 2, a - 1, 2, 0) : INF;
+        const int b2 = inner ? imin(LDX(lp2, L2, PMmloop10, Uin, L0), LDX(lp2, L2, PMmloop01, Uin, L0)) + apbp2 : INF;
+        const int b3 = inner ? LDX(lp2, L2, PfromM, Uin, L0) : INF;
         const int b4 = (a == 0 && b == 0) ? 0 : INF;
         vPM = imin(imin(b1, b2), imin(b3, b4));
     }
@@ -623,13 +677,14 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
     int vPO = INF;
     if (ptype(T, i, l) > 0) {
         const bool inner = (a >= 1 && b >= 1);
+        const int Uin = (a - 1) * L2.M + 1;  // (i+1, j, k, l-1): lane L0 + 2h
         int b1 = INF;
-        if (l - i > TURN && inner) b1 = RD(PO, 2, a - 1, 0, 1) + W2E(T.est, i, l);
-        const int b2 = inner ? imin(RD(POmloop10, 2, a - 1, 0, 1), RD(POmloop01, 2, a - 1, 0, 1)) + apbp2 : INF;
-        const int b3 = (inner && l - i >= TURN + 1) ? RD(PfromO, 2, a - 1, 0, 1) : INF;
+        if (l - i > TURN && inner) b1 = LDX(lp2, L2, PO, Uin, L0 + 2 * uh) + W2E(T.est, i, l);
+        const int b2 = inner ? imin(LDX(lp2, L2, POmloop10, Uin, L0 + 2 * uh), LDX(lp2, L2, POmloop01, Uin, L0 + 2 * uh)) + apbp2 : INF;
+        const int b3 = (inner && l - i >= TURN + 1) ? LDX(lp2, L2, PfromO, Uin, L0 + 2 * uh) : INF;
         vPO = imin(imin(b1, b2), b3);
     }
-#undef RD
+#undef LDX
 #undef CHK
     // values as stored (Matrix4D::set clamp / never-set 32767), read back by same-cell terms
     const int sPL = clamp_store(vPL), sPR = clamp_store(vPR), sPM = clamp_store(vPM), sPO = clamp_store(vPO);
@@ -641,8 +696,9 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
     const int vPK = imin(imin(pK1, pK2), imin(imin(sPL, sPM), imin(sPR, sPO)) + PB);  // :181-202
 
     // ---- stores: one coalesced int16 per matrix
-    const int C = T.lv[t].C;
-    int16_t *dst = T.d4 + T.lb[t] + (long long)a * Mt + L0;
+    const Lvl16 Lt = LD[t];
+    const int C = Lt.C;
+    int16_t *dst = T.d4 + Lt.lb + (long long)a * Mt + L0;
 #ifdef CCJ_DEBUG_BOUNDS
     if (i < 1 || i > m - h || h >= m) { atomicOr(T.err, 32); return; }
 #endif
