@@ -313,10 +313,11 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
 
 // ------------------------------------------------------------------------------------------
 // P(i, i+sigma) = min over i<=j<d<k<l of PK(i,j,d+1,k) + PK(j+1,d,k+1,l)   (pseudo_loop.cc:166-179)
-// One wave = (jo = j-i, a chunk of do = d-i, a group of 64 consecutive intervals i): for fixed
+// One wave = (jo = j-i, do = d-i, a group of 64 consecutive intervals i), looping over k: for fixed
 // offsets the two PK cells of neighbouring intervals are neighbours in HBM, so every load is
-// coalesced.  Each lane min-reduces its interval's candidates and does one atomicMin into T.P
-// (initialised INF+1 = "never set"; every candidate is <= 65534 < INF/2, A-Q4).  Needs PK levels
+// coalesced.  The 4 waves of a workgroup (4 consecutive do) min-reduce in LDS, then one atomicMin
+// per interval into T.P (initialised INF+1 = "never set"; every candidate is <= 65534 < INF/2,
+// A-Q4).  Needs PK levels
 // <= sigma-3 only, so it runs on a side stream three levels ahead of k_diag2d(sigma).
 // ------------------------------------------------------------------------------------------
 // Backtrack helper for the P_P case (pseudo_loop.cc:867-896): the first (j,d,k) in the reference
@@ -348,33 +349,45 @@ extern "C" int ccjk_pp_argmin(const DevTables *T, int i, int l, int target, unsi
     return (int)hipGetLastError();
 }
 
-constexpr int PT_CHUNK = 16;
+constexpr int PT_WAVES = 4;  // waves per k_pterm workgroup = consecutive do values sharing jo
 
-__global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngroups, int nchunks) {
+__global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngroups) {
+    __shared__ int red[PT_WAVES][64];
     const int n = T.n;
     const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
     const int jo = blockIdx.y;
-    const int wr = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    const int chunk = wr / ngroups;
-    const int grp = wr - chunk * ngroups;
-    if (chunk >= nchunks) return;
-    const int d0 = jo + 1 + chunk * PT_CHUNK;
-    const int d1 = imin(d0 + PT_CHUNK, sigma - 1);  // do <= sigma-2
-    if (d0 >= d1) return;
+    const int ddc = blockIdx.x / ngroups;
+    const int grp = blockIdx.x - ddc * ngroups;
+    const int dd0 = jo + 1 + ddc * PT_WAVES;
+    if (dd0 > sigma - 2) return;  // whole workgroup
+    const int dd = dd0 + w;
     const int i = grp * 64 + lane + 1;
-    if (i + sigma > n) return;
     int best = INF + 1;
-    for (int dd = d0; dd < d1; ++dd) {
-        const int a1 = jo, h1 = dd - jo - 1;   // PK(i, j, d+1, k)
-        const int a2 = dd - jo - 1;            // PK(j+1, d, k+1, l)
+    if (dd <= sigma - 2 && i + sigma <= n) {
+        // PK(i, j, d+1, k): level jo+(ko-dd-1), a = jo, h = dd-jo-1, interval start i
+        // PK(j+1, d, k+1, l): level (dd-jo-1)+(sigma-ko-1), a = dd-jo-1, h = ko-dd-1, start i+jo+1
+        const int a1 = jo, h1 = dd - jo - 1, a2 = dd - jo - 1;
+        const int g1 = (h1 * (h1 - 1)) >> 1;
+        const int16_t *__restrict__ D4 = T.d4;
+        const Lvl16 *__restrict__ LD = T.ld;
 #pragma unroll 4
         for (int ko = dd + 1; ko < sigma; ++ko) {
-            const int b1 = ko - dd - 1, h2 = ko - dd - 1, b2 = sigma - ko - 1;
-            const int v = ld4(T, PK, a1 + b1, a1, h1, i) + ld4(T, PK, a2 + b2, a2, h2, i + jo + 1);
+            const int h2 = ko - dd - 1;
+            const int t1 = a1 + h2, t2 = a2 + (sigma - ko - 1);
+            const Lvl16 L1 = LD[t1], L2 = LD[t2];
+            const int o1 = PK * L1.C + a1 * L1.M + h1 * (n - t1 - 2) - g1 - 1;
+            const int o2 = PK * L2.C + a2 * L2.M + h2 * (n - t2 - 2) - ((h2 * (h2 - 1)) >> 1) + jo;
+            const int v = (int)(D4 + L1.lb + o1)[i] + (int)(D4 + L2.lb + o2)[i];
             best = imin(best, v);
         }
     }
-    atomicMin(T.P + sigma * T.rs + i, best);
+    red[w][lane] = best;
+    __syncthreads();
+    if (w == 0 && i + sigma <= n) {
+        int v = imin(imin(red[0][lane], red[1][lane]), imin(red[2][lane], red[3][lane]));
+        if (v <= INF) atomicMin(T.P + sigma * T.rs + i, v);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -393,12 +406,28 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
 // recurrence that reads it (11a + 13b loads per cell instead of 14a + 16b).  The interior-loop
 // windows are walked by source level dt (outer) so the level descriptor is loaded once per dt.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPerA) {
+#ifndef CCJ_LIN_UNROLL
+#define CCJ_LIN_UNROLL 2
+#endif
+#define CCJ_PRAGMA(x) _Pragma(#x)
+#define CCJ_UNROLL(n) CCJ_PRAGMA(unroll n)
+__global__ __launch_bounds__(256)
+#ifdef CCJ_WAVES_EU
+__attribute__((amdgpu_waves_per_eu(CCJ_WAVES_EU, CCJ_WAVES_EU)))
+#endif
+void k_level4d(DevTables T, int t, int wavesPerA) {
 #ifdef CCJ_DEBUG_BOUNDS
     g_dbg_err = T.err;
 #endif
     const int n = T.n, rs = T.rs;
-    const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    int bid = blockIdx.x;
+#ifdef CCJ_XCD_MAP
+    {   // workgroups are dealt round-robin to the 8 XCDs: give each XCD a contiguous run of blocks
+        const int nb = gridDim.x, x = bid & 7, q = bid >> 3, per = nb >> 3, rem = nb & 7;
+        bid = x * per + imin(x, rem) + q;
+    }
+#endif
+    const int gw = __builtin_amdgcn_readfirstlane((int)((bid * blockDim.x + threadIdx.x) >> 6));
     const int lane = threadIdx.x & 63;
     const int a = __builtin_amdgcn_readfirstlane(gw / wavesPerA);
     if (a > t) return;
@@ -447,7 +476,7 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
 #ifdef CCJ_ABLATE_LINEAR
         if (a < 0)
 #endif
-#pragma unroll 2
+        CCJ_UNROLL(CCJ_LIN_UNROLL)
         for (int s = 1; s <= a; ++s) {
             lhs += uh;
             sjm += m + s;
@@ -498,7 +527,7 @@ __global__ __launch_bounds__(256) void k_level4d(DevTables T, int t, int wavesPe
 #ifdef CCJ_ABLATE_LINEAR
         if (b < 0)
 #endif
-#pragma unroll 2
+        CCJ_UNROLL(CCJ_LIN_UNROLL)
         for (int s = 1; s <= b; ++s) {
             lhs += uh;
             sjm += m + s;
@@ -755,10 +784,9 @@ extern "C" int ccjk_pterm(const DevTables *T, int sigma, void *stream) {
     const int nint = T->n - sigma;
     if (nint <= 0) return 0;
     const int ngroups = (nint + 63) / 64;
-    const int nchunks = (sigma - 2 + PT_CHUNK - 1) / PT_CHUNK;
-    const int waves = nchunks * ngroups;
-    dim3 grid((waves + 3) / 4, sigma - 2);
-    hipLaunchKernelGGL(k_pterm, grid, dim3(256), 0, (hipStream_t)stream, *T, sigma, ngroups, nchunks);
+    const int nddc = (sigma - 2 + PT_WAVES - 1) / PT_WAVES;
+    dim3 grid(nddc * ngroups, sigma - 2);
+    hipLaunchKernelGGL(k_pterm, grid, dim3(64 * PT_WAVES), 0, (hipStream_t)stream, *T, sigma, ngroups);
     return (int)hipGetLastError();
 }
 

@@ -1,8 +1,9 @@
 #!/bin/bash
-# Timing-only ablation builds of the fill (results are WRONG by construction; never used by tests).
+# Timing-only variant builds of the fill.  CCJ_ABLATE_* variants give WRONG results by construction
+# (never used by tests); the others are tuning candidates.  usage: tools/ablate.sh name:flags ...
 cd "$(dirname "$0")/.."
-for v in iloop:-DCCJ_ABLATE_ILOOP linear:-DCCJ_ABLATE_LINEAR pterm:-DCCJ_ABLATE_PTERM; do
-  name=${v%%:*}; flag=${v#*:}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-value -Wno-unused-result $flag \
-    -Iinclude -Iccj_amd/csrc ccj_amd/csrc/ccj_host.cc ccj_amd/csrc/ccj_kernels.hip -o ccj_amd/lib/libccj_hip_abl_$name.so || exit 1
+for v in "$@"; do
+  name=${v%%:*}; flags=${v#*:}
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-value -Wno-unused-result $flags \
+    -Iinclude -Iccj_amd/csrc ccj_amd/csrc/ccj_host.cc ccj_amd/csrc/ccj_kernels.hip -o ccj_amd/lib/libccj_hip_$name.so || exit 1
 done
