@@ -14,6 +14,7 @@
 //     reading (i, i+w) for consecutive i touches consecutive words.
 #pragma once
 #include <stdint.h>
+#include <hip/hip_runtime.h>
 #include "ccj_params.h"
 
 namespace ccj {
@@ -26,6 +27,9 @@ enum Mat4 {
 };
 
 constexpr int IE_U = 29;  // u1,u2 in [0,28] for pseudoknot interior loops (pseudo_loop.cc:694-806)
+constexpr int IL_CAP = 856;  // candidate-list capacity per pair (>= 29*29 + IL_B null tail)
+constexpr int IL_B = 8;      // interior-loop candidates per load batch (k_iloop)
+constexpr int IL_SEG = 64;   // per pair: seg[dt] = first list entry of source-level distance dt
 
 struct LevelDesc {
     int16_t *base;  // first element of level t (matrix 0)
@@ -39,6 +43,11 @@ struct Lvl16 {      // per-level descriptor read by the level kernel (one s_load
     long long lb;  // element offset of level t in the 4-D storage
     int C;         // cells per matrix in level t = (t+1)*M
     int M;         // cells per a-block = m(m+1)/2, m = n-t-2
+};
+
+struct LvlX {        // per-level bases of the interior-loop copies
+    long long lbx;  // element offset of level t in d4x: PLx (C_t elements) then PRx (C_t)
+    long long pmb;  // element offset of level t in pmx: m_t * n * (t+1) elements
 };
 
 struct Penalties {  // integer PK penalties, h_globals.hh:7-25
@@ -66,6 +75,20 @@ struct DevTables {
     int16_t *d4;                   // 4-D storage base
     const long long *lb;           // element offset of level t in d4
     const Lvl16 *ld;               // per-level descriptors
+    // interior-loop copies of PL / PR / PM, laid out so that the lanes of one k_iloop wave share
+    // the loop's closing pair:
+    //   PLx(t,a,h,i) = lbx + a*M + G(i-1) + h               (h fastest: fixed (i,j), lanes k)
+    //   PRx(t,a,h,i) = lbx + C + a*M + q(q+1)/2 + i-1       (q = i+h-1: fixed (k,l), lanes i)
+    //   PMx(t,a,h,i) = pmb + (h*n + j-1)*(t+1) + a          (j = i+a: fixed (j,k), lanes a)
+    int16_t *d4x, *pmx;
+    long long nx, npm;             // elements of d4x / pmx (debug bounds checks)
+    const LvlX *ldx;
+    // interior-loop candidate lists (k_build_il): per pair [w][p], the (u1,u2) whose inner pair can
+    // pair, ordered by dt = 2+u1+u2 then u1; entry .x = dt << 21 | u1 << 16 | (uint16)energy,
+    // .y = 2*u1*dt (the address cross term); IL_B null entries (dt 63) follow the last one
+    uint2 *il, *ilm;               // il: pair (p,p+w) closes the loop (PL, PR); ilm: pair encloses (PM)
+    int16_t *dummy;                // n+64 values 32767: target of the null entries
+    uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
     int *err;                      // device error word
 };
 
@@ -80,6 +103,8 @@ inline int64_t cell_offset_host(const LevelDesc &L, int x, int a, int h, int i) 
 extern "C" {
 int ccjk_init2d(const ccj::DevTables *T, void *stream);
 int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
+int ccjk_build_il(const ccj::DevTables *T, void *stream);
+int ccjk_iloop(const ccj::DevTables *T, int t, void *stream);
 int ccjk_diag2d(const ccj::DevTables *T, int sigma, void *stream);
 int ccjk_level4d(const ccj::DevTables *T, int t, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);

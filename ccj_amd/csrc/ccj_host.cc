@@ -103,6 +103,12 @@ struct ccj_ctx {
     LevelDesc *d_lv = nullptr;
     long long *d_lb = nullptr;
     Lvl16 *d_ld = nullptr;
+    int16_t *d4x = nullptr, *pmx = nullptr;  // interior-loop copies of PL/PR and PM
+    long long nx = 0, npm = 0;
+    LvlX *d_ldx = nullptr;
+    uint2 *d_il = nullptr, *d_ilm = nullptr;
+    int16_t *d_dummy = nullptr;
+    uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
     unsigned long long *d_key = nullptr;  // P_P argmin result
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
     int8_t *d_vt = nullptr;
@@ -1447,6 +1453,35 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipMalloc(&c->d_lb, c->lv_off.size() * sizeof(long long)));
     HIPCHK(cp, hipMalloc(&c->d_ld, c->lv_off.size() * sizeof(Lvl16)));
     HIPCHK(cp, hipMalloc(&c->d_key, sizeof(unsigned long long)));
+    {
+        // interior-loop copies (ccj_engine.h): PLx+PRx mirror the level sizes, PMx is padded per (h, j)
+        std::vector<LvlX> ldx(c->lv_off.size(), LvlX{0, 0});
+        long long ox = 0, op = 0;
+        for (int t = 0; t < c->nlev; ++t) {
+            ldx[t] = LvlX{ox, op};
+            ox += 2LL * c->lv_host[t].C;
+            op += (long long)c->lv_host[t].m * n * (t + 1);
+        }
+        const size_t pad = 256;
+        c->nx = ox;
+        c->npm = op;
+        if (hipMalloc(&c->d4x, ((size_t)ox + pad) * sizeof(int16_t)) != hipSuccess ||
+            hipMalloc(&c->pmx, ((size_t)op + pad) * sizeof(int16_t)) != hipSuccess)
+            return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for interior-loop copies failed", (ox + op) * 2e-9);
+        HIPCHK(cp, hipMalloc(&c->d_ldx, ldx.size() * sizeof(LvlX)));
+        HIPCHK(cp, hipMemcpy(c->d_ldx, ldx.data(), ldx.size() * sizeof(LvlX), hipMemcpyHostToDevice));
+        const size_t pairs = (size_t)(n + 1) * c->rs;
+        const size_t ents = pairs * IL_CAP;
+        HIPCHK(cp, hipMalloc(&c->d_il, ents * sizeof(uint2)));
+        HIPCHK(cp, hipMalloc(&c->d_ilm, ents * sizeof(uint2)));
+        std::vector<int16_t> dummy((size_t)n + 64, (int16_t)INTERN_INF);
+        HIPCHK(cp, hipMalloc(&c->d_dummy, dummy.size() * sizeof(int16_t)));
+        HIPCHK(cp, hipMemcpy(c->d_dummy, dummy.data(), dummy.size() * sizeof(int16_t), hipMemcpyHostToDevice));
+        HIPCHK(cp, hipMalloc(&c->d_ilseg, pairs * IL_SEG * sizeof(uint32_t)));
+        HIPCHK(cp, hipMalloc(&c->d_ilmseg, pairs * IL_SEG * sizeof(uint32_t)));
+        HIPCHK(cp, hipMemset(c->d_ilseg, 0, pairs * IL_SEG * sizeof(uint32_t)));
+        HIPCHK(cp, hipMemset(c->d_ilmseg, 0, pairs * IL_SEG * sizeof(uint32_t)));
+    }
     HIPCHK(cp, hipMalloc(&c->d2i, A2_N * plane * sizeof(int)));
     HIPCHK(cp, hipMalloc(&c->d_vt, plane));
     if (c->total4 > 0 && hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
@@ -1538,6 +1573,16 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.d4 = c->d4;
     T.lb = c->d_lb;
     T.ld = c->d_ld;
+    T.d4x = c->d4x;
+    T.pmx = c->pmx;
+    T.nx = c->nx;
+    T.npm = c->npm;
+    T.ldx = c->d_ldx;
+    T.il = c->d_il;
+    T.ilm = c->d_ilm;
+    T.dummy = c->d_dummy;
+    T.ilseg = c->d_ilseg;
+    T.ilmseg = c->d_ilmseg;
     T.err = c->d_err;
     *out = c.release();
     return CCJ_OK;
@@ -1572,6 +1617,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     HIPCHK(c, hipEventRecord(c->ev_start, st));
     HIPCHK(c, (hipError_t)ccjk_init2d(&c->T, st));
     HIPCHK(c, (hipError_t)ccjk_precompute_ie(&c->T, st));
+    HIPCHK(c, (hipError_t)ccjk_build_il(&c->T, st));
     HIPCHK(c, hipEventRecord(c->ev_pre, st));
     // P(sigma) only needs PK levels <= sigma-3: reduce it on a side stream three levels ahead
     HIPCHK(c, hipEventRecord(c->lev_done[n], st));  // "init done" for the side stream
@@ -1589,6 +1635,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
         HIPCHK(c, hipEventRecord(c->tev[4 * s + 1], st));
         if (s < c->nlev) {
             HIPCHK(c, hipEventRecord(c->tev[4 * s + 2], st));
+            HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, st));
             HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, st));
             HIPCHK(c, hipEventRecord(c->tev[4 * s + 3], st));
             HIPCHK(c, hipEventRecord(c->lev_done[s], st));
@@ -1890,6 +1937,14 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_lv);
     hipFree(c->d_lb);
     hipFree(c->d_ld);
+    hipFree(c->d4x);
+    hipFree(c->pmx);
+    hipFree(c->d_ldx);
+    hipFree(c->d_il);
+    hipFree(c->d_ilm);
+    hipFree(c->d_dummy);
+    hipFree(c->d_ilseg);
+    hipFree(c->d_ilmseg);
     hipFree(c->d_key);
     hipFree(c->d2i);
     hipFree(c->d_vt);

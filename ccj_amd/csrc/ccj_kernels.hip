@@ -391,6 +391,238 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
 }
 
 // ------------------------------------------------------------------------------------------
+// Interior-loop candidate lists (once per problem, after k_precompute_ie).
+// For pair (p, q = p+w):
+//   il  — loops closed by (p,q) around an inner pair (d,dp) = (p+1+u1, q-1-u2), the window of
+//         get_PLiloop / get_PRiloop (pseudo_loop.cc:694-700, 729-735): u1 <= min(w,30)-2,
+//         u2 <= min(w-u1-6, 28);
+//   ilm — loops closed by an outer pair (d,dp) = (p-1-u1, q+1+u2) around (p,q), the window of
+//         get_PMiloop (pseudo_loop.cc:762-768) without its cell-dependent bounds (u1 <= a-2,
+//         u2 <= b-2 are checked per lane by k_iloop).
+// Only candidates whose other pair can pair are kept (the reference skips the rest: can_pair),
+// in order of dt = 2+u1+u2 (the source level distance), u1 ascending; seg[dt] is the first entry
+// of dt.  One wave per pair: lane = u1, ballot compaction.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_build_il(DevTables T) {
+    const int n = T.n, rs = T.rs;
+    const int p = blockIdx.x + 1, w = blockIdx.y, kind = blockIdx.z;
+    const int q = p + w;
+    if (q > n) return;
+    const int lane = threadIdx.x;
+    const size_t pidx = (size_t)w * rs + p;
+    uint32_t *seg = (kind ? T.ilmseg : T.ilseg) + pidx * IL_SEG;
+    uint2 *ent = (kind ? T.ilm : T.il) + pidx * IL_CAP;
+    int cnt = 0;
+    for (int dt = 0; dt < IL_SEG; ++dt) {
+        if (lane == 0) seg[dt] = (uint32_t)cnt;
+        const int u1 = lane, u2 = dt - 2 - lane;
+        bool valid = false;
+        int e = 0;
+        if (dt >= 2 && u1 < IE_U && u2 >= 0 && u2 < IE_U) {
+            if (kind == 0) {
+                const int d = p + 1 + u1, dp = q - 1 - u2;
+                if (u1 <= imin(w, MAXLOOP) - 2 && u2 <= imin(w - u1 - 6, MAXLOOP - 2) && T.pt[(dp - d) * rs + d] > 0) {
+                    valid = true;
+                    e = T.ie[((size_t)(u1 * IE_U + u2) * (n + 1) + w) * rs + p];
+                }
+            } else {
+                const int d = p - 1 - u1, dp = q + 1 + u2;
+                if (d >= 1 && dp <= n && T.pt[(dp - d) * rs + d] > 0) {
+                    valid = true;
+                    e = T.ie[((size_t)(u1 * IE_U + u2) * (n + 1) + (dp - d)) * rs + d];
+                }
+            }
+        }
+        const unsigned long long mask = __ballot(valid);
+        if (valid)
+            ent[cnt + __popcll(mask & ((1ull << lane) - 1))] =
+                make_uint2(((uint32_t)dt << 21) | ((uint32_t)u1 << 16) | (uint32_t)(uint16_t)e, (uint32_t)(2 * u1 * dt));
+        cnt += __popcll(mask);
+    }
+    // null tail: dt 63 addresses T.dummy (32767), energy 32767 -> 65534, never below a clamped result
+    if (lane < IL_B) ent[cnt + lane] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0u);
+}
+
+// ------------------------------------------------------------------------------------------
+// Interior loops of level t (get_PLiloop / get_PRiloop / get_PMiloop, pseudo_loop.cc:682-773).
+// One wave per closing pair and run of cells sharing it, so the pair test, the candidate list and
+// the loop energies are wave-uniform (scalar loads) and only candidates whose inner pair can pair
+// are visited; the partner value comes from the PLx/PRx/PMx copy, contiguous along the lanes.
+//   PL: wave = (a, i, h-chunk), lanes h  — closing pair (i, j)
+//   PR: wave = (a, q, i-chunk), lanes i  — closing pair (k, l), q = i+h-1 = k-a-3
+//   PM: wave = (h, j, a-chunk), lanes a  — pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
+// The minimum (clamped like a store) goes into the cell's PL/PR/PM slot of level t, where
+// k_level4d(t) picks it up.  Needs levels <= t-2 only.
+// ------------------------------------------------------------------------------------------
+// Each list entry's partner address is A[dt] + B[u1] (+ 2*u1*dt for PL/PM) bytes + the lane's
+// offset: A (64-bit, per source level) and B (per u1) are per-wave tables held one value per lane
+// and fetched with readlane, so an entry costs a few scalar ops and one load on a uniform base.
+// IL_B entries are loaded together (one s_load burst), then IL_B partner values, then reduced.
+// Null tail entries (dt 63) hit T.dummy, so the last batch needs no masking (PL/PR: cnt is the
+// whole list; PM stops early and substitutes null entries).
+__device__ __forceinline__ unsigned long long rdl64(unsigned long long v, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ int il_u1(uint32_t x) { return (int)((x >> 16) & 31u); }
+__device__ __forceinline__ int il_dt(uint32_t x) { return (int)(x >> 21); }
+__device__ __forceinline__ int il_e(uint32_t x) { return (int)(int16_t)(x & 0xffffu); }
+
+// min over the wave's candidate list of energy + partner value (PL/PR/PM interior loops)
+template <bool CROSS, bool PMWIN>
+__device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restrict__ ent, int cnt,
+                                       unsigned long long Atab, int Btab, unsigned lofs2, int as, int bs) {
+    int b1 = INF;
+#pragma unroll 1
+    for (int e0 = 0; e0 < cnt; e0 += IL_B) {
+        uint2 E[IL_B];
+        int v[IL_B];
+        const uint2 *ep = ent + e0;
+#pragma unroll
+        for (int u = 0; u < IL_B; ++u) {
+            E[u] = ep[u];
+            // PM stops at dt <= t-2, before the list's null tail: past cnt, substitute a null entry
+            if (PMWIN && e0 + u >= cnt) E[u] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < IL_B; ++u) {
+            const int dt = il_dt(E[u].x), u1 = il_u1(E[u].x);
+            unsigned off = (unsigned)__builtin_amdgcn_readlane(Btab, u1);
+            if (CROSS) off += E[u].y;
+            const char *p = (const char *)(rdl64(Atab, dt) + off);
+#ifdef CCJ_DEBUG_BOUNDS
+            {   // the partner must lie inside its copy (or be the null target)
+                const int16_t *q = (const int16_t *)(p + lofs2);
+                const bool in = (q >= T.d4x && q < T.d4x + T.nx) || (q >= T.pmx && q < T.pmx + T.npm) ||
+                                (q >= T.dummy && q < T.dummy + T.n + 64);
+                if (!in || (dt != 63 && (dt < 2 || dt > 2 * MAXLOOP - 2))) {
+                    if (atomicOr(T.err, 64) == 0)
+                        printf("k_iloop OOB: dt %d u1 %d off %u lofs2 %u p-d4x %lld p-pmx %lld p-dummy %lld\n", dt, u1,
+                               off, lofs2, (long long)(q - T.d4x), (long long)(q - T.pmx), (long long)(q - T.dummy));
+                    v[u] = 0;
+                    continue;
+                }
+            }
+#endif
+            // global address space: a plain pointer rebuilt from an integer would become a flat load
+            v[u] = *(const __attribute__((address_space(1))) int16_t *)(p + lofs2);
+        }
+#pragma unroll
+        for (int u = 0; u < IL_B; ++u) {
+            const int c = il_e(E[u].x) + v[u];
+            if (PMWIN) {
+                const int u1 = il_u1(E[u].x), u2 = il_dt(E[u].x) - 2 - u1;
+                b1 = imin(b1, (u1 <= as - 2 && u2 <= bs - 2) ? c : INF);  // get_PMiloop: d > i, dp < l
+            } else {
+                b1 = imin(b1, c);
+            }
+        }
+    }
+    return b1;
+}
+
+// grid (ceil(n/4), max(t-5, m-2), 3*nz): z / nz = role, z % nz = lane chunk; 4 waves per block
+__global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, int nz) {
+    const int n = T.n, rs = T.rs, m = n - t - 2;
+    const int lane = threadIdx.x & 63;
+    const int X = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int Y = blockIdx.y;
+    const int role = (int)blockIdx.z / nz, zc = (int)blockIdx.z - role * nz;
+    const Lvl16 Lt = T.ld[t];
+    const int tl = t - lane;  // A-table lane L describes source level t-L (dt = L)
+    const bool lvl_ok = lane >= 2 && lane <= 2 * MAXLOOP - 2 && tl >= 0;
+    const long long BIAS = (long long)(n + 64) * (n + 64);  // keeps B >= 0
+    if (role == 0) {
+        // PL: wave = (a, i, h-chunk), lanes h; closing pair (i, j)
+        const int i = X + 1, a = Y + 6;
+        if (i > m || a > t || zc * 64 > m - i || ptype(T, i, i + a) <= 0) return;
+        const int h = zc * 64 + lane;
+        const bool act = h <= m - i;
+        const unsigned lofs2 = 2u * (unsigned)(act ? h : m - i);  // idle lanes re-read a valid cell
+        const size_t pidx = (size_t)a * rs + i;
+        // PLx(t-dt, a-dt, h+dt-1-u1, i+1+u1) = lbx + (a-dt)M + x(m+dt) - x(x-1)/2 + dt-1-u1 + h, x = i+u1
+        //   = [lbx + (a-dt)M + i*m + i*dt + dt-1] + [u1*m - x(x-1)/2 - u1] + u1*dt
+        const int x = i + lane;
+        const int Btab = (int)(2 * ((long long)lane * m - ((long long)x * (x - 1) >> 1) - lane + BIAS));
+        unsigned long long Atab = 0;
+        if (lvl_ok && a >= lane)
+            Atab = (unsigned long long)T.d4x +
+                   2 * (T.ldx[tl].lbx + (long long)(a - lane) * T.ld[tl].M + (long long)i * m + (long long)i * lane + lane - 1 - BIAS);
+        const int B0 = __builtin_amdgcn_readlane(Btab, 0);
+        if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
+        const int b1 = il_scan<true, false>(T, T.il + pidx * IL_CAP, (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1], Atab, Btab, lofs2, 0, 0);
+#ifdef CCJ_DEBUG_BOUNDS
+        if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
+            atomicOr(T.err, 128);
+            return;
+        }
+#endif
+        if (act) T.d4[Lt.lb + (long long)PL * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
+    } else if (role == 1) {
+        // PR: wave = (a, q, i-chunk), lanes i; closing pair (k, l), q = i+h-1 = k-a-3
+        const int q = X, a = Y;
+        const int b = t - a;
+        if (q >= m || b < 6 || zc * 64 > q) return;
+        const int k = q + a + 3, l = k + b;
+        if (ptype(T, k, l) <= 0) return;
+        const int i = zc * 64 + lane + 1;
+        const bool act = i <= q + 1;
+        const unsigned lofs2 = 2u * (unsigned)((act ? i : q + 1) - 1);
+        const int h = q + 1 - i;
+        const size_t pidx = (size_t)b * rs + k;
+        // PRx(t-dt, a, h+1+u1, i) = lbx + C + a*M + qq(qq+1)/2 + i-1, qq = q+1+u1
+        const int qq = q + 1 + lane;
+        const int Btab = qq * (qq + 1);  // bytes
+        unsigned long long Atab = 0;
+        if (lvl_ok) Atab = (unsigned long long)T.d4x + 2 * (T.ldx[tl].lbx + T.ld[tl].C + (long long)a * T.ld[tl].M);
+        const int B0 = __builtin_amdgcn_readlane(Btab, 0);
+        if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
+        const int b1 = il_scan<false, false>(T, T.il + pidx * IL_CAP, (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1], Atab, Btab, lofs2, 0, 0);
+#ifdef CCJ_DEBUG_BOUNDS
+        if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
+            atomicOr(T.err, 128);
+            return;
+        }
+#endif
+        if (act) T.d4[Lt.lb + (long long)PR * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
+    } else {
+        // PM: wave = (h, j, a-chunk), lanes a; pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
+        const int j = X + 1, h = Y + 2;
+        const int g = h + 2, k = j + g;
+        if (j > n || h > m - 1 || k > n) return;
+        const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, j - 1);
+        if (alo + zc * 64 > ahi || ptype(T, j, k) <= 0) return;
+        const int a = alo + zc * 64 + lane;
+        const bool act = a <= ahi;
+        const int as = act ? a : ahi;
+        const unsigned lofs2 = 2u * (unsigned)as;
+        const size_t pidx = (size_t)g * rs + j;
+        // PMx(t-dt, a-1-u1, h+dt, j-1-u1) = pmb + (h+dt)*n*(t+1-dt) + (j-2-u1)(t+1-dt) - 1-u1 + a
+        //   = [pmb + (h+dt)*n*(t+1-dt) + (j-2)(t+1-dt) - 1] + [-u1(t+2)] + u1*dt
+        // Lanes outside the get_PMiloop window read another cell of the same level (h+dt >= 4:
+        // in bounds) and are masked.
+        const int Btab = (int)(2 * (-(long long)lane * (t + 2) + BIAS));
+        unsigned long long Atab = 0;
+        if (lvl_ok)
+            Atab = (unsigned long long)T.pmx +
+                   2 * (T.ldx[tl].pmb + ((long long)(h + lane) * n + (j - 2)) * (tl + 1) - 1 - BIAS);
+        const int B0 = __builtin_amdgcn_readlane(Btab, 0);
+        if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
+        // entries with dt > t-2 fit no cell of this level
+        const int cnt = (int)T.ilmseg[pidx * IL_SEG + imin(t - 1, IL_SEG - 1)];
+        const int b1 = il_scan<true, true>(T, T.ilm + pidx * IL_CAP, cnt, Atab, Btab, lofs2, as, t - as);
+#ifdef CCJ_DEBUG_BOUNDS
+        if (act && (a < 0 || a > t || h < 0 || h >= m || (j - a) < 1 || (j - a) > m - h)) {
+            atomicOr(T.err, 128);
+            return;
+        }
+#endif
+        if (act) T.d4[Lt.lb + (long long)PM * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + (j - a) - 1] = (int16_t)clamp_store(b1);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // 4-D level t: one lane per cell (i,j,k,l); all lanes of a wave share (t, a) so every loop bound
 // is wave-uniform.  pseudo_loop.cc:181-644, 663-808.
 //
@@ -594,108 +826,54 @@ void k_level4d(DevTables T, int t, int wavesPerA) {
     // ---- level t-2 neighbours of PL/PR/PM/PO (stack terms, get_P?mloop, PfromX)
     const Lvl16 L2 = LD[t >= 2 ? t - 2 : 0];
     const int16_t *lp2 = D4 + L2.lb;
-    const int ie_w = (n + 1) * rs;  // stride between (u1,u2) planes of IE
-    // ---- PL (:232-253) with get_PLiloop (:682-703), get_PLmloop (:705-715)
+    // own slots of level t: k_iloop(t) left the interior-loop minima of PL/PR/PM there
+    const Lvl16 Lt = LD[t];
+    const int C = Lt.C;
+    int16_t *dst = T.d4 + Lt.lb + (long long)a * Mt + L0;
+    // ---- PL (:232-253) with get_PLiloop (:682-703, k_iloop), get_PLmloop (:705-715)
     int vPL = INF;
-    if (ptype(T, i, j) > 0) {
+    const bool pl_ok = ptype(T, i, j) > 0;
+    if (pl_ok) {
         int b1 = INF;
         const int Uin = (a - 2) * L2.M + m + 3;  // (i+1, j-1, k, l): lane L0 + h
         if (a > TURN) {
             if (a > TURN + 2) b1 = LDX(lp2, L2, PL, Uin, L0 + uh) + W2E(T.est, i, j);
-            const int mu1 = imin(a, MAXLOOP) - 2;
-#ifdef CCJ_ABLATE_ILOOP
-            if (a < 0)
+#ifndef CCJ_ABLATE_ILOOP
+            if (a >= 6) b1 = imin(b1, (int)dst[PL * C]);
 #endif
-            for (int dt = 2; dt <= a - 4; ++dt) {
-                const Lvl16 L = LD[t - dt];
-                const int16_t *lp = D4 + L.lb + (long long)PL * L.C;
-                const int u1lo = imax(0, dt - 30), u1hi = imin(dt - 2, mu1);
-                int dh = dt - 1 - u1lo;  // candidate (d,dp) = (i+1+u1, j-1-u2), u2 = dt-2-u1
-                int U = (a - dt) * L.M + dh * m + dh * dt - ((dh * (dh - 1)) >> 1) + 1 + u1lo;
-                unsigned ln = L0 + uh * (unsigned)(1 + u1lo);
-                int ieo = (u1lo * IE_U + (dt - 2 - u1lo)) * ie_w + a * rs;
-#pragma unroll 4
-                for (int u1 = u1lo; u1 <= u1hi; ++u1) {
-                    IE_CHECK(u1, dt - 2 - u1, a, i);
-                    CHK(dt, a - dt, dh, 1 + u1);
-                    b1 = imin(b1, (int)T.ie[ieo + i] + (int)lp[(unsigned)U + ln]);
-                    U += dh - m - dt;
-                    --dh;
-                    ln += uh;
-                    ieo += (IE_U - 1) * ie_w;
-                }
-            }
         }
         const int b2 = (a >= 2) ? imin(LDX(lp2, L2, PLmloop10, Uin, L0 + uh), LDX(lp2, L2, PLmloop01, Uin, L0 + uh)) + apbp2 : INF;
         const int b3 = (a >= TURN + 1) ? LDX(lp2, L2, PfromL, Uin, L0 + uh) : INF;
         vPL = imin(imin(b1, b2), b3);
     }
-    // ---- PR (:255-275) with get_PRiloop (:717-738), get_PRmloop (:740-750)
+    // ---- PR (:255-275) with get_PRiloop (:717-738, k_iloop), get_PRmloop (:740-750)
     int vPR = INF;
-    if (ptype(T, k, l) > 0) {
+    const bool pr_ok = ptype(T, k, l) > 0;
+    if (pr_ok) {
         int b1 = INF;
         const int Uin = a * L2.M + m + 2;  // (i, j, k+1, l-1): lane L0 + h
         if (b > TURN) {
             if (b > TURN + 2) b1 = LDX(lp2, L2, PR, Uin, L0 + uh) + W2E(T.est, k, l);
-            const int mu1 = imin(b, MAXLOOP) - 2;
-#ifdef CCJ_ABLATE_ILOOP
-            if (b < 0)
+#ifndef CCJ_ABLATE_ILOOP
+            if (b >= 6) b1 = imin(b1, (int)dst[PR * C]);
 #endif
-            for (int dt = 2; dt <= b - 4; ++dt) {
-                const Lvl16 L = LD[t - dt];
-                const int16_t *lp = D4 + L.lb + (long long)PR * L.C;
-                const int u1lo = imax(0, dt - 30), u1hi = imin(dt - 2, mu1);
-                int dh = 1 + u1lo;  // candidate (d,dp) = (k+1+u1, l-1-u2)
-                int U = a * L.M + dh * m + dh * dt - ((dh * (dh - 1)) >> 1);
-                unsigned ln = L0 + uh * (unsigned)(dt - 1 - u1lo);
-                int ieo = (u1lo * IE_U + (dt - 2 - u1lo)) * ie_w + b * rs;
-#pragma unroll 4
-                for (int u1 = u1lo; u1 <= u1hi; ++u1) {
-                    IE_CHECK(u1, dt - 2 - u1, b, k);
-                    CHK(dt, a, dh, 0);
-                    b1 = imin(b1, (int)T.ie[ieo + k] + (int)lp[(unsigned)U + ln]);
-                    U += m + dt - dh;
-                    ++dh;
-                    ln -= uh;
-                    ieo += (IE_U - 1) * ie_w;
-                }
-            }
         }
         const int b2 = (b >= 2) ? imin(LDX(lp2, L2, PRmloop10, Uin, L0 + uh), LDX(lp2, L2, PRmloop01, Uin, L0 + uh)) + apbp2 : INF;
         const int b3 = (b >= TURN + 1) ? LDX(lp2, L2, PfromR, Uin, L0 + uh) : INF;
         vPR = imin(imin(b1, b2), b3);
     }
-    // ---- PM (:277-300) with get_PMiloop (:752-773), get_PMmloop (:775-785)
+    // ---- PM (:277-300) with get_PMiloop (:752-773, k_iloop), get_PMmloop (:775-785)
     int vPM = INF;
-    if (ptype(T, j, k) > 0) {
+    const bool pm_ok = ptype(T, j, k) > 0;
+    if (pm_ok) {
         int b1 = INF;
         const bool inner = (a >= 1 && b >= 1);
         const int Uin = (a - 1) * L2.M + 2 * m + 3;  // (i, j-1, k+1, l): lane L0
         if (g > TURN) {
             if (inner) b1 = LDX(lp2, L2, PM, Uin, L0) + W2E(T.est, j - 1, k + 1);
-            const int mu1 = imin(a - 2, MAXLOOP - 2);
-            const int mu2 = imin(b - 2, MAXLOOP - 2);
-#ifdef CCJ_ABLATE_ILOOP
-            if (a < 0)
+#ifndef CCJ_ABLATE_ILOOP
+            if (a >= 2 && b >= 2) b1 = imin(b1, (int)dst[PM * C]);
 #endif
-            if (mu1 >= 0 && mu2 >= 0)
-                for (int dt = 2; dt <= 2 + mu1 + mu2; ++dt) {
-                    const Lvl16 L = LD[t - dt];
-                    const int16_t *lp = D4 + L.lb + (long long)PM * L.C;
-                    const int u1lo = imax(0, dt - 2 - mu2), u1hi = imin(dt - 2, mu1);
-                    // candidate (d,dp) = (j-1-u1, k+1+u2): PM(i,d,dp,l) = (t-dt, a-1-u1, h+dt, i), lane L0
-                    int U = (a - 1 - u1lo) * L.M + dt * m + dt * dt - ((dt * (dt - 1)) >> 1);
-                    const int lpm = (g + dt) * rs + j - 1;  // IE outer span g+dt, start j-1-u1
-                    int ieo = (u1lo * IE_U + (dt - 2 - u1lo)) * ie_w - u1lo;
-#pragma unroll 4
-                    for (int u1 = u1lo; u1 <= u1hi; ++u1) {
-                        IE_CHECK(u1, dt - 2 - u1, g + dt, j - 1 - u1);
-                        CHK(dt, a - 1 - u1, dt, 0);
-                        b1 = imin(b1, (int)T.ie[ieo + lpm] + (int)lp[(unsigned)U + L0]);
-                        U -= L.M;
-                        ieo += (IE_U - 1) * ie_w - 1;
-                    }
-                }
         }
         const int b2 = inner ? imin(LDX(lp2, L2, PMmloop10, Uin, L0), LDX(lp2, L2, PMmloop01, Uin, L0)) + apbp2 : INF;
         const int b3 = inner ? LDX(lp2, L2, PfromM, Uin, L0) : INF;
@@ -725,9 +903,6 @@ void k_level4d(DevTables T, int t, int wavesPerA) {
     const int vPK = imin(imin(pK1, pK2), imin(imin(sPL, sPM), imin(sPR, sPO)) + PB);  // :181-202
 
     // ---- stores: one coalesced int16 per matrix
-    const Lvl16 Lt = LD[t];
-    const int C = Lt.C;
-    int16_t *dst = T.d4 + Lt.lb + (long long)a * Mt + L0;
 #ifdef CCJ_DEBUG_BOUNDS
     if (i < 1 || i > m - h || h >= m) { atomicOr(T.err, 32); return; }
 #endif
@@ -753,6 +928,14 @@ void k_level4d(DevTables T, int t, int wavesPerA) {
     dst[POmloop00 * C] = (int16_t)clamp_store(vPOm00);
     dst[POmloop01 * C] = (int16_t)clamp_store(vPOm01);
     dst[POmloop10 * C] = (int16_t)clamp_store(vPOm10);
+    // interior-loop copies, only where a later k_iloop can read them (its pair can pair)
+    const LvlX X = T.ldx[t];
+    if (pl_ok) T.d4x[X.lbx + (long long)a * Mt + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = (int16_t)sPL;
+    if (pr_ok) {
+        const int q = i + h - 1;
+        T.d4x[X.lbx + C + (long long)a * Mt + ((q * (q + 1)) >> 1) + i - 1] = (int16_t)sPR;
+    }
+    if (pm_ok) T.pmx[X.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = (int16_t)sPM;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -787,6 +970,26 @@ extern "C" int ccjk_pterm(const DevTables *T, int sigma, void *stream) {
     const int nddc = (sigma - 2 + PT_WAVES - 1) / PT_WAVES;
     dim3 grid(nddc * ngroups, sigma - 2);
     hipLaunchKernelGGL(k_pterm, grid, dim3(64 * PT_WAVES), 0, (hipStream_t)stream, *T, sigma, ngroups);
+    return (int)hipGetLastError();
+}
+
+extern "C" int ccjk_build_il(const DevTables *T, void *stream) {
+    const int n = T->n;
+    if (n < 1) return 0;
+    hipLaunchKernelGGL(k_build_il, dim3(n, n + 1, 2), dim3(64), 0, (hipStream_t)stream, *T);
+    return (int)hipGetLastError();
+}
+
+extern "C" int ccjk_iloop(const DevTables *T, int t, void *stream) {
+#ifdef CCJ_ABLATE_ILOOP
+    return 0;
+#endif
+    const int n = T->n, m = n - t - 2;
+    if (m <= 0 || t < 4) return 0;
+    const int nz = imax((m + 63) / 64, (t + 64) / 64);
+    const int ny = imax(t - 5, m - 2);
+    if (ny <= 0) return 0;
+    hipLaunchKernelGGL(k_iloop, dim3((n + 3) / 4, ny, 3 * nz), dim3(256), 0, (hipStream_t)stream, *T, t, nz);
     return (int)hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
 """Sum rocprofv3 --pmc counter_collection CSVs over one kernel's dispatches, per fold.
 
-usage: python tools/pmc_summary.py FOLDS CSV [CSV ...]
+usage: python tools/pmc_summary.py FOLDS CSV [CSV ...] [KERNEL]
 level_profile.py runs FOLDS=2 folds; every counter is summed over all dispatches of the matched
 kernel (default k_level4d) and divided by FOLDS.  Also prints the average dispatch duration.
 """
@@ -12,6 +12,8 @@ from collections import defaultdict
 def main(argv):
     folds = float(argv[1])
     kern = "k_level4d"
+    if argv and not argv[-1].endswith(".csv"):
+        kern = argv.pop()
     tot = defaultdict(float)
     dur = {}
     for path in argv[2:]:
