@@ -93,11 +93,12 @@ def main():
         wf.ccj()
     barrier()
     t0 = time.perf_counter()
-    level_ms = diag_ms = fill_ms = 0.0
+    level_ms = diag_ms = fill_ms = il_ms = 0.0
     for _ in range(a.steps):
         wf.ccj()
         tm = wf.timing()
         level_ms += tm["level4d_ms"]
+        il_ms += tm["iloop_ms"]
         diag_ms += tm["diag2d_ms"]
         fill_ms += tm["fill_ms"]
     elapsed = time.perf_counter() - t0
@@ -113,9 +114,15 @@ def main():
     lib().ccj_work_model.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
     lib().ccj_work_model(wf._h, wm)
     bytes4d = wm[0]
+    ws = (ctypes.c_double * 2)()
+    lib().ccj_work_split.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+    lib().ccj_work_split(wf._h, ws)
+    bytes_il, bytes_lv = ws[0], ws[1]
     nlaunch = max(a.n - 2, 1)
     avg_launch_s = (level_ms / a.steps) / 1e3 / nlaunch
-    achieved = (bytes4d / nlaunch) / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    achieved = (bytes_lv / nlaunch) / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    il_launch_s = (il_ms / a.steps) / 1e3 / max(a.n - 6, 1)
+    il_achieved = (bytes_il / max(a.n - 6, 1)) / il_launch_s / 1e9 if il_launch_s > 0 else 0.0
     structure, energy = wf.structure, wf.energy
     wf.close()
 
@@ -146,11 +153,15 @@ def main():
         "mfe": energy,
         "structure": structure,
         "breakdown_ms": {"fill_device": fill_ms / a.steps, "level4d_kernels": level_ms / a.steps,
-                         "diag2d_kernels": diag_ms / a.steps},
+                         "iloop_kernels": il_ms / a.steps, "diag2d_kernels": diag_ms / a.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "k_level4d", "launches_per_fold": nlaunch,
-                     "avg_launch_us": avg_launch_s * 1e6, "algorithmic_bytes_per_fold": bytes4d},
+                     "avg_launch_us": avg_launch_s * 1e6, "algorithmic_bytes_per_fold": bytes_lv},
+        "roofline_iloop": {"bound": "hbm", "achieved": il_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": il_achieved / HBM_PEAK_GBS, "kernel": "k_iloop",
+                           "launches_per_fold": max(a.n - 6, 1), "avg_launch_us": il_launch_s * 1e6,
+                           "algorithmic_bytes_per_fold": bytes_il},
     }
     if world == 1 and not a.no_cpu_baseline:
         cb = cpu_baseline(a.cpu_sample_n)

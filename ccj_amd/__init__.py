@@ -111,6 +111,8 @@ def lib() -> ctypes.CDLL:
     L.ccj_num_cells.restype = ctypes.c_uint64
     L.ccj_host_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
     L.ccj_host_timing.restype = ip
+    L.ccj_iloop_ms.argtypes = [vp]
+    L.ccj_iloop_ms.restype = ctypes.c_double
     _lib = L
     return L
 
@@ -232,7 +234,8 @@ class W_final:
         lib().ccj_last_timing(self._h, ctypes.byref(f), k)
         hst = (ctypes.c_double * 3)()
         lib().ccj_host_timing(self._h, hst)
-        return {"fill_ms": f.value, "level4d_ms": k[0], "diag2d_ms": k[1], "precompute_ms": k[2],
+        return {"fill_ms": f.value, "level4d_ms": k[0], "iloop_ms": lib().ccj_iloop_ms(self._h), "diag2d_ms": k[1],
+                "precompute_ms": k[2],
                 "host_mirror_wait_ms": hst[0], "W_ms": hst[1], "backtrack_ms": hst[2]}
 
     def close(self):

@@ -112,11 +112,12 @@ struct ccj_ctx {
     unsigned long long *d_key = nullptr;  // P_P argmin result
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
     int8_t *d_vt = nullptr;
-    hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr;
+    hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr, st_il = nullptr, st_d = nullptr;
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
-    std::vector<double> lev_ms_v, diag_ms_v;
+    std::vector<double> lev_ms_v, diag_ms_v, il_ms_v;
+    std::vector<hipEvent_t> il_done, dg_done;  // k_iloop(t) / k_diag2d(sigma) finished
     std::vector<hipEvent_t> lev_done;
-    std::vector<hipEvent_t> tev;  // timing events: 2 per level kernel + 2 per diag kernel
+    std::vector<hipEvent_t> tev;  // timing events: 2 per k_level4d, k_iloop and k_diag2d launch
     hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_pre = nullptr;
     DevTables T{};
 
@@ -128,7 +129,7 @@ struct ccj_ctx {
     bool filled = false, mirrored = false;
     std::vector<int> W;
 
-    double fill_ms = 0, level_ms = 0, diag_ms = 0, pre_ms = 0;
+    double fill_ms = 0, level_ms = 0, diag_ms = 0, pre_ms = 0, il_ms = 0;
     double sync_ms = 0, w_ms = 0, bt_ms = 0;  // host side of the last fold
     std::string err;
 
@@ -1424,6 +1425,12 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_p, hipStreamNonBlocking));
+    HIPCHK(cp, hipStreamCreateWithFlags(&c->st_il, hipStreamNonBlocking));
+    HIPCHK(cp, hipStreamCreateWithFlags(&c->st_d, hipStreamNonBlocking));
+    c->il_done.resize(n + 1);
+    for (auto &e : c->il_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->dg_done.resize(n + 1);
+    for (auto &e : c->dg_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(cp, hipEventCreate(&c->ev_start));
     HIPCHK(cp, hipEventCreate(&c->ev_end));
     HIPCHK(cp, hipEventCreate(&c->ev_pre));
@@ -1431,7 +1438,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     for (auto &e : c->lev_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->p_done.resize(n + 1);
     for (auto &e : c->p_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    c->tev.resize(4 * (size_t)n + 4);
+    c->tev.resize(6 * (size_t)n + 6);
     for (auto &e : c->tev) HIPCHK(cp, hipEventCreate(&e));
 
     const size_t plane = (size_t)(n + 1) * c->rs;
@@ -1619,25 +1626,34 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     HIPCHK(c, (hipError_t)ccjk_precompute_ie(&c->T, st));
     HIPCHK(c, (hipError_t)ccjk_build_il(&c->T, st));
     HIPCHK(c, hipEventRecord(c->ev_pre, st));
-    // P(sigma) only needs PK levels <= sigma-3: reduce it on a side stream three levels ahead
-    HIPCHK(c, hipEventRecord(c->lev_done[n], st));  // "init done" for the side stream
-    auto launch_p = [&](int sig) -> int {
-        if (sig < 3 || sig >= n) return CCJ_OK;
-        HIPCHK(c, hipStreamWaitEvent(c->st_p, sig - 3 < c->nlev ? c->lev_done[sig - 3] : c->lev_done[n], 0));
-        HIPCHK(c, (hipError_t)ccjk_pterm(&c->T, sig, c->st_p));
-        HIPCHK(c, hipEventRecord(c->p_done[sig], c->st_p));
-        return CCJ_OK;
-    };
+    // Four streams:
+    //   st_d : k_diag2d(s)  needs P(s) (p_done) and spans < s (stream order)
+    //   st_il: k_iloop(t)   needs 4-D levels <= t-2 (lev_done[t-2])
+    //   st   : k_level4d(t) needs level t-1 (stream order), k_iloop(t), k_diag2d(t-1)
+    //   st_p : k_pterm(s)   needs PK levels <= s-3 (lev_done[s-3])
+    // so k_diag2d(t) and k_iloop(t+1) overlap k_level4d(t).  Every event is recorded (enqueued)
+    // before a stream waits on it.
+    HIPCHK(c, hipStreamWaitEvent(c->st_d, c->ev_pre, 0));
+    HIPCHK(c, hipStreamWaitEvent(c->st_il, c->ev_pre, 0));
+    HIPCHK(c, hipStreamWaitEvent(c->st_p, c->ev_pre, 0));
     for (int s = 0; s < n; ++s) {
-        if (s >= 3) HIPCHK(c, hipStreamWaitEvent(st, c->p_done[s], 0));
-        HIPCHK(c, hipEventRecord(c->tev[4 * s + 0], st));
-        HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, s, st));
-        HIPCHK(c, hipEventRecord(c->tev[4 * s + 1], st));
+        hipEvent_t *ev = &c->tev[6 * (size_t)s];
+        if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_d, c->p_done[s], 0));
+        HIPCHK(c, hipEventRecord(ev[0], c->st_d));
+        HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, s, c->st_d));
+        HIPCHK(c, hipEventRecord(ev[1], c->st_d));
+        HIPCHK(c, hipEventRecord(c->dg_done[s], c->st_d));
         if (s < c->nlev) {
-            HIPCHK(c, hipEventRecord(c->tev[4 * s + 2], st));
-            HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, st));
+            if (s >= 2) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 2], 0));
+            HIPCHK(c, hipEventRecord(ev[2], c->st_il));
+            HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->st_il));
+            HIPCHK(c, hipEventRecord(ev[3], c->st_il));
+            HIPCHK(c, hipEventRecord(c->il_done[s], c->st_il));
+            HIPCHK(c, hipStreamWaitEvent(st, c->il_done[s], 0));
+            if (s >= 1) HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s - 1], 0));
+            HIPCHK(c, hipEventRecord(ev[4], st));
             HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, st));
-            HIPCHK(c, hipEventRecord(c->tev[4 * s + 3], st));
+            HIPCHK(c, hipEventRecord(ev[5], st));
             HIPCHK(c, hipEventRecord(c->lev_done[s], st));
             if (c->overlap && c->h4) {
                 // stream the finished level to the pinned host mirror while later levels run
@@ -1646,12 +1662,24 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
                 HIPCHK(c, hipMemcpyAsync(c->h4 + c->lv_off[s], c->d4 + c->lv_off[s], bytes, hipMemcpyDeviceToHost,
                                          c->st_copy));
             }
+            // P(s+3) only needs PK levels <= s
+            if (s + 3 < n) {
+                HIPCHK(c, hipStreamWaitEvent(c->st_p, c->lev_done[s], 0));
+                HIPCHK(c, (hipError_t)ccjk_pterm(&c->T, s + 3, c->st_p));
+                HIPCHK(c, hipEventRecord(c->p_done[s + 3], c->st_p));
+            }
+        } else if (s + 3 < n && s + 3 >= 3) {
+            HIPCHK(c, (hipError_t)ccjk_pterm(&c->T, s + 3, c->st_p));
+            HIPCHK(c, hipEventRecord(c->p_done[s + 3], c->st_p));
         }
-        if (int rc = launch_p(s + 3)) return rc;
     }
+    // join: the fill ends when the last level and the last span are done
+    HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[n - 1], 0));
     HIPCHK(c, hipEventRecord(c->ev_end, st));
     HIPCHK(c, hipStreamSynchronize(st));
     HIPCHK(c, hipStreamSynchronize(c->st_p));
+    HIPCHK(c, hipStreamSynchronize(c->st_il));
+    HIPCHK(c, hipStreamSynchronize(c->st_d));
     int herr = 0;
     HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (herr & 1) return set_err(c, CCJ_E_PARAMS, "e_intP table value outside int16 range (flags %d)", herr);
@@ -1661,21 +1689,27 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     c->fill_ms = ms;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev_start, c->ev_pre));
     c->pre_ms = ms;
-    double lsum = 0, dsum = 0;
+    double lsum = 0, dsum = 0, isum = 0;
     c->lev_ms_v.assign(n, 0.0);
     c->diag_ms_v.assign(n, 0.0);
+    c->il_ms_v.assign(n, 0.0);
     for (int s = 0; s < n; ++s) {
-        HIPCHK(c, hipEventElapsedTime(&ms, c->tev[4 * s + 0], c->tev[4 * s + 1]));
+        const hipEvent_t *ev = &c->tev[6 * (size_t)s];
+        HIPCHK(c, hipEventElapsedTime(&ms, ev[0], ev[1]));
         dsum += ms;
         c->diag_ms_v[s] = ms;
         if (s < c->nlev) {
-            HIPCHK(c, hipEventElapsedTime(&ms, c->tev[4 * s + 2], c->tev[4 * s + 3]));
+            HIPCHK(c, hipEventElapsedTime(&ms, ev[2], ev[3]));
+            isum += ms;
+            c->il_ms_v[s] = ms;
+            HIPCHK(c, hipEventElapsedTime(&ms, ev[4], ev[5]));
             lsum += ms;
             c->lev_ms_v[s] = ms;
         }
     }
     c->level_ms = lsum;
     c->diag_ms = dsum;
+    c->il_ms = isum;
     c->filled = true;
     (void)plane;
     return CCJ_OK;
@@ -1836,7 +1870,7 @@ static int work_model(int n, const short *S, const int (*pairt)[8], double *out)
                     cnt += can(p + u1 + 1, q - u2 - 1);
             cntW[(size_t)w * (n + 2) + p] = cnt;
         }
-    double reads = 0, cells = 0;
+    double reads = 0, cells = 0, ilreads = 0;
     std::vector<int> cum(IE_U * IE_U);
     for (int j = 1; j <= n; ++j)
         for (int g = 2; j + g <= n; ++g) {
@@ -1856,14 +1890,24 @@ static int work_model(int n, const short *S, const int (*pairt)[8], double *out)
                 const int i = j - a;
                 const bool pl = pr(i, j) > 0 && a > TURN;
                 const double rl = pl ? (double)((a > TURN + 2) + cntW[(size_t)a * (n + 2) + i]) : 0.0;
+                const double il_l = pl ? (double)cntW[(size_t)a * (n + 2) + i] : 0.0;
                 for (int b = 0; k + b <= n; ++b) {
                     const int l = k + b;
                     double r = 14.0 * a + 16.0 * b + rl;
-                    if (b > TURN && pr(k, l) > 0) r += (b > TURN + 2) + cntW[(size_t)b * (n + 2) + k];
+                    double il = il_l;
+                    if (b > TURN && pr(k, l) > 0) {
+                        r += (b > TURN + 2) + cntW[(size_t)b * (n + 2) + k];
+                        il += cntW[(size_t)b * (n + 2) + k];
+                    }
                     if (pm_ok) {
                         r += (a >= 1 && b >= 1);
-                        if (a >= 2 && b >= 2) r += cum[std::min(a - 2, IE_U - 1) * IE_U + std::min(b - 2, IE_U - 1)];
+                        if (a >= 2 && b >= 2) {
+                            const int cm = cum[std::min(a - 2, IE_U - 1) * IE_U + std::min(b - 2, IE_U - 1)];
+                            r += cm;
+                            il += cm;
+                        }
                     }
+                    ilreads += il;
                     if (a >= 1 && b >= 1 && l - i > TURN && pr(i, l) > 0) r += 1;
                     reads += r;
                 }
@@ -1876,12 +1920,25 @@ static int work_model(int n, const short *S, const int (*pairt)[8], double *out)
     out[1] = 4.0 * pterms;                 // bytes, P terms of the 2-D kernels
     out[2] = reads;                        // R4 (4-D part)
     out[3] = cells;
+    out[4] = ilreads;                      // interior-loop candidate reads (k_iloop)
     return CCJ_OK;
 }
 
 extern "C" int ccj_work_model(const ccj_ctx *c, double *out) {
     if (!c || !out) return CCJ_E_ARG;
-    return work_model(c->n, c->S.data(), c->pair, out);
+    double w[5];
+    const int rc = work_model(c->n, c->S.data(), c->pair, w);
+    for (int x = 0; x < 4; ++x) out[x] = w[x];
+    return rc;
+}
+
+extern "C" int ccj_work_split(const ccj_ctx *c, double *out2) {
+    if (!c || !out2) return CCJ_E_ARG;
+    double w[5];
+    const int rc = work_model(c->n, c->S.data(), c->pair, w);
+    out2[0] = 2.0 * w[4];                    // k_iloop: candidate reads
+    out2[1] = w[0] - out2[0];                // k_level4d: everything else (incl. 44 B of stores per cell)
+    return rc;
 }
 
 extern "C" int ccj_work_model_seq(const char *seq, int noGU, double *out) {
@@ -1893,7 +1950,10 @@ extern "C" int ccj_work_model_seq(const char *seq, int noGU, double *out) {
     if (noGU) pairt[3][4] = pairt[4][3] = 0;
     std::vector<short> S(n + 2, 0);
     for (int i = 1; i <= n; ++i) S[i] = (short)encode_base(seq[i - 1]);
-    return work_model(n, S.data(), pairt, out);
+    double w[5];
+    const int rc = work_model(n, S.data(), pairt, w);
+    for (int x = 0; x < 4; ++x) out[x] = w[x];
+    return rc;
 }
 
 extern "C" int ccj_host_timing(const ccj_ctx *c, double *out3) {
@@ -1913,6 +1973,14 @@ extern "C" int ccj_level_times(const ccj_ctx *c, double *level_ms, double *diag_
     return CCJ_OK;
 }
 
+extern "C" int ccj_iloop_times(const ccj_ctx *c, double *iloop_ms, int cap) {
+    if (!c || !iloop_ms) return CCJ_E_ARG;
+    for (int t = 0; t < cap && t < (int)c->il_ms_v.size(); ++t) iloop_ms[t] = c->il_ms_v[t];
+    return CCJ_OK;
+}
+
+extern "C" double ccj_iloop_ms(const ccj_ctx *c) { return c ? c->il_ms : 0.0; }
+
 extern "C" int ccj_n(const ccj_ctx *c) { return c ? c->n : 0; }
 extern "C" const char *ccj_last_error(const ccj_ctx *c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
@@ -1922,6 +1990,8 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->st) hipStreamSynchronize(c->st);
     if (c->st_copy) hipStreamSynchronize(c->st_copy);
     if (c->st_p) hipStreamSynchronize(c->st_p);
+    if (c->st_il) hipStreamSynchronize(c->st_il);
+    if (c->st_d) hipStreamSynchronize(c->st_d);
     hipFree(c->d4);
     hipFree(c->d_ie);
     hipFree(c->d_est);
@@ -1952,6 +2022,10 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     for (auto e : c->lev_done) hipEventDestroy(e);
     for (auto e : c->p_done) hipEventDestroy(e);
     if (c->st_p) hipStreamDestroy(c->st_p);
+    if (c->st_il) hipStreamDestroy(c->st_il);
+    if (c->st_d) hipStreamDestroy(c->st_d);
+    for (auto e : c->il_done) hipEventDestroy(e);
+    for (auto e : c->dg_done) hipEventDestroy(e);
     for (auto e : c->tev) hipEventDestroy(e);
     if (c->ev_start) hipEventDestroy(c->ev_start);
     if (c->ev_end) hipEventDestroy(c->ev_end);

@@ -9,6 +9,7 @@
 // values and the P?mloop00 seeds see the initial 32767.
 // All arithmetic is int32 min-plus; storage is int16 with the reference clamp at 32767.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include "ccj_engine.h"
 #include "ccj_energy.h"
 
@@ -638,19 +639,17 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, int nz) {
 // recurrence that reads it (11a + 13b loads per cell instead of 14a + 16b).  The interior-loop
 // windows are walked by source level dt (outer) so the level descriptor is loaded once per dt.
 // ------------------------------------------------------------------------------------------
-#ifndef CCJ_LIN_UNROLL
-#define CCJ_LIN_UNROLL 2
-#endif
-#define CCJ_PRAGMA(x) _Pragma(#x)
-#define CCJ_UNROLL(n) CCJ_PRAGMA(unroll n)
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(512)
 #ifdef CCJ_WAVES_EU
 __attribute__((amdgpu_waves_per_eu(CCJ_WAVES_EU, CCJ_WAVES_EU)))
 #endif
-void k_level4d(DevTables T, int t, int wavesPerA) {
+void k_level4d(DevTables T, int t, int wavesPerA, int split) {
 #ifdef CCJ_DEBUG_BOUNDS
     g_dbg_err = T.err;
 #endif
+    // split > 1 (late, narrow levels): the split waves of one 64-cell chunk share the a/b loops
+    // (step s = part + 1, part + 1 + split, ...) and min-reduce their partial results through LDS.
+    extern __shared__ int red[];  // [chunk][part-1][22][64], split > 1 only
     const int n = T.n, rs = T.rs;
     int bid = blockIdx.x;
 #ifdef CCJ_XCD_MAP
@@ -659,15 +658,22 @@ void k_level4d(DevTables T, int t, int wavesPerA) {
         bid = x * per + imin(x, rem) + q;
     }
 #endif
-    const int gw = __builtin_amdgcn_readfirstlane((int)((bid * blockDim.x + threadIdx.x) >> 6));
+    const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int part = wib % split;
+    const int cpb = (int)(blockDim.x >> 6) / split;  // chunks per block
+    const int gw = __builtin_amdgcn_readfirstlane(bid * cpb + wib / split);
     const int lane = threadIdx.x & 63;
-    const int a = __builtin_amdgcn_readfirstlane(gw / wavesPerA);
-    if (a > t) return;
-    const int chunk = gw - a * wavesPerA;
+    const int a_raw = __builtin_amdgcn_readfirstlane(gw / wavesPerA);
+    if (split == 1 && a_raw > t) return;
+    const bool wave_ok = a_raw <= t;  // grid tail (split > 1 keeps the wave for the barrier)
+    const int a = wave_ok ? a_raw : t;
+    const int chunk = wave_ok ? gw - a * wavesPerA : 0;
     const int m = n - t - 2;
     const int Mt = (m * (m + 1)) >> 1;
-    const int c = chunk * 64 + lane;
-    if (c >= Mt) return;
+    const int c_raw = chunk * 64 + lane;
+    if (split == 1 && c_raw >= Mt) return;
+    const bool lane_ok = wave_ok && c_raw < Mt;
+    const int c = imin(c_raw, Mt - 1);  // idle lanes shadow the last cell (valid reads, no store)
     // row h: largest h with G(h) = h*m - h(h-1)/2 <= c
     const float tm = 2.0f * m + 1.0f;
     int h = (int)((tm - sqrtf(tm * tm - 8.0f * (float)c)) * 0.5f);
@@ -698,111 +704,186 @@ void k_level4d(DevTables T, int t, int wavesPerA) {
 #define CHK(dt, ap_, dh, di)
 #endif
 
+    // The a- and b-loops are software-pipelined: the loads of step s+split are issued before the
+    // values of step s are consumed, so every wave keeps two steps of loads in flight.  The terms
+    // with d strictly inside the gap (s < a, s < b) are masked on the last step by adding INF;
+    // their loads still hit valid cells.
     // ---- fused a-loop: split point d inside [i, j] ----
     int pLm00 = INTERN_INF + bp, pLm01 = INF, pLm10 = INF, pMm00 = INTERN_INF + bp, pMm10 = INF;
     int pOm00 = INTERN_INF + bp, pOm10 = INF;
     int fL1 = INF, fL2 = INF, fM = INF, fO1 = INF, pK1 = INF;
-    {
-        unsigned lhs = L0;  // L0 + h*s
-        int sjm = 0;        // s*m + s(s+1)/2
-#ifdef CCJ_ABLATE_LINEAR
-        if (a < 0)
+    struct AV { int wb_i, wbp_i, wp_i, wb_j, wbp_j, wp_j, Lm00i, Mm00i, Om00i, fLi, fOi, Lm00j, Mm00j, Lm10j, fLj, fMpj, Kj; };
+    auto load_a = [&](int s) {
+        AV v;
+        const int r2 = (s - 1) * rs, jl = j - s + 1;
+        v.wb_i = WB[r2 + i]; v.wbp_i = WBPr[r2 + i]; v.wp_i = WP[r2 + i];      // (i, i+s-1)
+        v.wb_j = WB[r2 + jl]; v.wbp_j = WBPr[r2 + jl]; v.wp_j = WP[r2 + jl];   // (j-s+1, j)
+        CHK(s, a - s, 0, s);
+        CHK(s, a - s, s, 0);
+#ifdef CCJ_ABLATE_LOCAL
+        const Lvl16 L = LD[t - 1];  // timing only: every step re-reads one level (cache-resident)
+        s = 1;
+#else
+        const Lvl16 L = LD[t - s];
 #endif
-        CCJ_UNROLL(CCJ_LIN_UNROLL)
-        for (int s = 1; s <= a; ++s) {
-            lhs += uh;
-            sjm += m + s;
-            const int r2 = (s - 1) * rs;
-            const int wb_i = WB[r2 + i], wbp_i = WBPr[r2 + i], wp_i = WP[r2 + i];   // (i, i+s-1)
-            const int jl = j - s + 1;
-            const int wb_j = WB[r2 + jl], wbp_j = WBPr[r2 + jl], wp_j = WP[r2 + jl]; // (j-s+1, j)
-            CHK(s, a - s, 0, s);
-            CHK(s, a - s, s, 0);
-            const Lvl16 L = LD[t - s];
-            const int16_t *lp = D4 + L.lb;
-            const int Ui = (a - s) * L.M + s;    // X(d,j,k,l), d = i+s: lane L0 + h*s
-            const int Uj = (a - s) * L.M + sjm;  // X(i,d,k,l), d = j-s: lane L0
-            const int xLm00i = LDX(lp, L, PLmloop00, Ui, lhs);
-            const int xMm00i = LDX(lp, L, PMmloop00, Ui, lhs);
-            const int xOm00i = LDX(lp, L, POmloop00, Ui, lhs);
-            const int xLm00j = LDX(lp, L, PLmloop00, Uj, L0);
-            const int xMm00j = LDX(lp, L, PMmloop00, Uj, L0);
-            pLm00 = imin(pLm00, imin(wb_i + xLm00i, xLm00j + wb_j));   // :449-458
-            pLm01 = imin(pLm01, xLm00j + wbp_j);                        // :468-471
-            pLm10 = imin(pLm10, wbp_i + xLm00i);                        // :481-483
-            pMm00 = imin(pMm00, xMm00j + wb_j);                         // :548-551
-            pMm10 = imin(pMm10, wbp_i + xMm00i);                        // :581-584
-            pOm00 = imin(pOm00, wb_i + xOm00i);                         // :599-602
-            pOm10 = imin(pOm10, wbp_i + xOm00i);                        // :632-635
-            if (s < a) {
-                const int xfLi = LDX(lp, L, PfromL, Ui, lhs);
-                const int xfOi = LDX(lp, L, PfromO, Ui, lhs);
-                const int xLm10j = LDX(lp, L, PLmloop10, Uj, L0);
-                const int xfLj = LDX(lp, L, PfromL, Uj, L0);
-                const int xfMpj = LDX(lp, L, PfromMprime, Uj, L0);
-                const int xKj = LDX(lp, L, PK, Uj, L0);
-                fL1 = imin(fL1, xfLi + wp_i);        // PfromL(d,j,k,l) + WP(i,d-1)  :357-359
-                fO1 = imin(fO1, xfOi + wp_i);        // PfromO(d,j,k,l) + WP(i,d-1)  :425-427
-                pLm10 = imin(pLm10, xLm10j + wb_j);  // PLmloop10(i,d,k,l) + WB(d+1,j) :484-486
-                fL2 = imin(fL2, xfLj + wp_j);        // PfromL(i,d,k,l) + WP(d+1,j)  :360-361
-                fM = imin(fM, xfMpj + wp_j);         // PfromMprime(i,d,k,l) + WP(d+1,j) :399-401
-                pK1 = imin(pK1, xKj + wp_j);         // PK(i,d,k,l) + WP(d+1,j)      :184-187
-            }
+        const int16_t *lp = D4 + L.lb;
+        const int Ui = (a - s) * L.M + s;                          // X(d,j,k,l), d = i+s: lane L0 + h*s
+        const int Uj = (a - s) * L.M + s * m + ((s * (s + 1)) >> 1);  // X(i,d,k,l), d = j-s: lane L0
+        const unsigned lh = L0 + uh * (unsigned)s;
+#ifdef CCJ_ABLATE_WIDE
+        {   // timing only: one 16-byte load per shift (an AoS record), values meaningless
+            const uint4 wi = *(const uint4 *)((unsigned long long)(lp + (unsigned)Ui + lh * 8u) & ~15ull);
+            const uint4 wj = *(const uint4 *)((unsigned long long)(lp + (unsigned)Uj + L0 * 8u) & ~15ull);
+            v.Lm00i = (int16_t)wi.x; v.Mm00i = (int16_t)(wi.x >> 16); v.Om00i = (int16_t)wi.y; v.fLi = (int16_t)(wi.y >> 16);
+            v.fOi = (int16_t)wi.z; v.Lm00j = (int16_t)wj.x; v.Mm00j = (int16_t)(wj.x >> 16); v.Lm10j = (int16_t)wj.y;
+            v.fLj = (int16_t)(wj.y >> 16); v.fMpj = (int16_t)wj.z; v.Kj = (int16_t)(wj.z >> 16);
+        }
+#else
+        v.Lm00i = LDX(lp, L, PLmloop00, Ui, lh);
+        v.Mm00i = LDX(lp, L, PMmloop00, Ui, lh);
+        v.Om00i = LDX(lp, L, POmloop00, Ui, lh);
+        v.fLi = LDX(lp, L, PfromL, Ui, lh);
+        v.fOi = LDX(lp, L, PfromO, Ui, lh);
+        v.Lm00j = LDX(lp, L, PLmloop00, Uj, L0);
+        v.Mm00j = LDX(lp, L, PMmloop00, Uj, L0);
+        v.Lm10j = LDX(lp, L, PLmloop10, Uj, L0);
+        v.fLj = LDX(lp, L, PfromL, Uj, L0);
+        v.fMpj = LDX(lp, L, PfromMprime, Uj, L0);
+        v.Kj = LDX(lp, L, PK, Uj, L0);
+#endif
+        return v;
+    };
+    auto step_a = [&](const AV &v, int mask) {
+        pLm00 = imin(pLm00, imin(v.wb_i + v.Lm00i, v.Lm00j + v.wb_j));  // :449-458
+        pLm01 = imin(pLm01, v.Lm00j + v.wbp_j);                         // :468-471
+        pLm10 = imin(pLm10, v.wbp_i + v.Lm00i);                         // :481-483
+        pMm00 = imin(pMm00, v.Mm00j + v.wb_j);                          // :548-551
+        pMm10 = imin(pMm10, v.wbp_i + v.Mm00i);                         // :581-584
+        pOm00 = imin(pOm00, v.wb_i + v.Om00i);                          // :599-602
+        pOm10 = imin(pOm10, v.wbp_i + v.Om00i);                         // :632-635
+        fL1 = imin(fL1, v.fLi + v.wp_i + mask);         // PfromL(d,j,k,l) + WP(i,d-1)      :357-359
+        fO1 = imin(fO1, v.fOi + v.wp_i + mask);         // PfromO(d,j,k,l) + WP(i,d-1)      :425-427
+        pLm10 = imin(pLm10, v.Lm10j + v.wb_j + mask);   // PLmloop10(i,d,k,l) + WB(d+1,j)   :484-486
+        fL2 = imin(fL2, v.fLj + v.wp_j + mask);         // PfromL(i,d,k,l) + WP(d+1,j)      :360-361
+        fM = imin(fM, v.fMpj + v.wp_j + mask);          // PfromMprime(i,d,k,l) + WP(d+1,j) :399-401
+        pK1 = imin(pK1, v.Kj + v.wp_j + mask);          // PK(i,d,k,l) + WP(d+1,j)          :184-187
+    };
+#ifdef CCJ_ABLATE_LINEAR
+    if (a < 0)
+#endif
+    if (1 + part <= a) {
+        int s = 1 + part;
+        AV cur = load_a(s);
+        for (;;) {
+            const int sn = s + split;
+            const AV nxt = load_a(imin(sn, a));  // the last one re-reads step a (discarded)
+            step_a(cur, s < a ? 0 : INF);
+            if (sn > a) break;
+            cur = nxt;
+            s = sn;
         }
     }
     // ---- fused b-loop: split point d inside [k, l] ----
     int pRm00 = INTERN_INF + bp, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
     int fR1 = INF, fR2 = INF, fMp = INF, fO2 = INF, pK2 = INF;
-    {
-        unsigned lhs = L0;
-        int sjm = 0;
-#ifdef CCJ_ABLATE_LINEAR
-        if (b < 0)
+    struct BV { int wb_k, wbp_k, wp_k, wb_l, wbp_l, wp_l, Rm00k, Mm00k, fRk, PLk, PRk, Kk, Rm00l, Mm00l, Om00l, Mm10l, Om10l, fRl, fOl; };
+    auto load_b = [&](int s) {
+        BV v;
+        const int r2 = (s - 1) * rs, ll = l - s + 1;
+        v.wb_k = WB[r2 + k]; v.wbp_k = WBPr[r2 + k]; v.wp_k = WP[r2 + k];      // (k, k+s-1)
+        v.wb_l = WB[r2 + ll]; v.wbp_l = WBPr[r2 + ll]; v.wp_l = WP[r2 + ll];   // (l-s+1, l)
+        CHK(s, a, s, 0);
+        CHK(s, a, 0, 0);
+#ifdef CCJ_ABLATE_LOCAL
+        const Lvl16 L = LD[t - 1];  // timing only: every step re-reads one level (cache-resident)
+        s = 1;
+#else
+        const Lvl16 L = LD[t - s];
 #endif
-        CCJ_UNROLL(CCJ_LIN_UNROLL)
-        for (int s = 1; s <= b; ++s) {
-            lhs += uh;
-            sjm += m + s;
-            const int r2 = (s - 1) * rs;
-            const int wb_k = WB[r2 + k], wbp_k = WBPr[r2 + k], wp_k = WP[r2 + k];   // (k, k+s-1)
-            const int ll = l - s + 1;
-            const int wb_l = WB[r2 + ll], wbp_l = WBPr[r2 + ll], wp_l = WP[r2 + ll]; // (l-s+1, l)
-            CHK(s, a, s, 0);
-            CHK(s, a, 0, 0);
-            const Lvl16 L = LD[t - s];
-            const int16_t *lp = D4 + L.lb;
-            const int Uk = a * L.M + sjm;  // X(i,j,d,l), d = k+s: lane L0
-            const int Ul = a * L.M;        // X(i,j,k,d), d = l-s: lane L0 + h*s
-            const int xRm00k = LDX(lp, L, PRmloop00, Uk, L0);
-            const int xMm00k = LDX(lp, L, PMmloop00, Uk, L0);
-            const int xRm00l = LDX(lp, L, PRmloop00, Ul, lhs);
-            const int xMm00l = LDX(lp, L, PMmloop00, Ul, lhs);
-            const int xOm00l = LDX(lp, L, POmloop00, Ul, lhs);
-            pRm00 = imin(pRm00, imin(wb_k + xRm00k, xRm00l + wb_l));   // :499-508
-            pRm10 = imin(pRm10, wbp_k + xRm00k);                        // :534-537
-            pRm01 = imin(pRm01, xRm00l + wbp_l);                        // :520-523
-            pMm00 = imin(pMm00, xMm00k + wb_k);                         // :552-555
-            pMm01 = imin(pMm01, xMm00l + wbp_l);                        // :567-570
-            pOm00 = imin(pOm00, xOm00l + wb_l);                         // :603-606
-            pOm01 = imin(pOm01, xOm00l + wbp_l);                        // :618-621
-            if (s < b) {
-                const int xfRk = LDX(lp, L, PfromR, Uk, L0);
-                const int xPLk = LDX(lp, L, PL, Uk, L0);
-                const int xPRk = LDX(lp, L, PR, Uk, L0);
-                const int xKk = LDX(lp, L, PK, Uk, L0);
-                const int xMm10l = LDX(lp, L, PMmloop10, Ul, lhs);
-                const int xOm10l = LDX(lp, L, POmloop10, Ul, lhs);
-                const int xfRl = LDX(lp, L, PfromR, Ul, lhs);
-                const int xfOl = LDX(lp, L, PfromO, Ul, lhs);
-                fR1 = imin(fR1, xfRk + wp_k);                     // PfromR(i,j,d,l) + WP(k,d-1)  :379-381
-                fMp = imin(fMp, imin(xPLk, xPRk) + PB + wp_k);    // PfromM'' (:663-679) + WP(k,d-1) :412-414
-                pK2 = imin(pK2, xKk + wp_k);                      // PK(i,j,d,l) + WP(k,d-1)      :189-192
-                pMm10 = imin(pMm10, xMm10l + wb_l);               // PMmloop10(i,j,k,d) + WB(d+1,l) :585-588
-                pOm10 = imin(pOm10, xOm10l + wb_l);               // POmloop10(i,j,k,d) + WB(d+1,l) :636-639
-                fR2 = imin(fR2, xfRl + wp_l);                     // PfromR(i,j,k,d) + WP(d+1,l)  :382-383
-                fO2 = imin(fO2, xfOl + wp_l);                     // PfromO(i,j,k,d) + WP(d+1,l)  :429-431
-            }
+        const int16_t *lp = D4 + L.lb;
+        const int Uk = a * L.M + s * m + ((s * (s + 1)) >> 1);  // X(i,j,d,l), d = k+s: lane L0
+        const int Ul = a * L.M;                                 // X(i,j,k,d), d = l-s: lane L0 + h*s
+        const unsigned lh = L0 + uh * (unsigned)s;
+#ifdef CCJ_ABLATE_WIDE
+        {
+            const uint4 k1 = *(const uint4 *)((unsigned long long)(lp + (unsigned)Uk + L0 * 8u) & ~15ull);
+            const uint4 k2 = *(const uint4 *)((unsigned long long)(lp + (unsigned)Uk + L.C + L0 * 8u) & ~15ull);
+            const uint4 l1 = *(const uint4 *)((unsigned long long)(lp + (unsigned)Ul + lh * 8u) & ~15ull);
+            const uint4 l2 = *(const uint4 *)((unsigned long long)(lp + (unsigned)Ul + L.C + lh * 8u) & ~15ull);
+            v.Rm00k = (int16_t)k1.x; v.Mm00k = (int16_t)(k1.x >> 16); v.fRk = (int16_t)k2.x; v.PLk = (int16_t)k2.y;
+            v.PRk = (int16_t)(k2.y >> 16); v.Kk = (int16_t)k1.w; v.Rm00l = (int16_t)l2.x; v.Mm00l = (int16_t)l1.x;
+            v.Om00l = (int16_t)(l1.x >> 16); v.Mm10l = (int16_t)l2.y; v.Om10l = (int16_t)(l2.y >> 16);
+            v.fRl = (int16_t)l2.z; v.fOl = (int16_t)l1.y;
         }
+#else
+        v.Rm00k = LDX(lp, L, PRmloop00, Uk, L0);
+        v.Mm00k = LDX(lp, L, PMmloop00, Uk, L0);
+        v.fRk = LDX(lp, L, PfromR, Uk, L0);
+        v.PLk = LDX(lp, L, PL, Uk, L0);
+        v.PRk = LDX(lp, L, PR, Uk, L0);
+        v.Kk = LDX(lp, L, PK, Uk, L0);
+        v.Rm00l = LDX(lp, L, PRmloop00, Ul, lh);
+        v.Mm00l = LDX(lp, L, PMmloop00, Ul, lh);
+        v.Om00l = LDX(lp, L, POmloop00, Ul, lh);
+        v.Mm10l = LDX(lp, L, PMmloop10, Ul, lh);
+        v.Om10l = LDX(lp, L, POmloop10, Ul, lh);
+        v.fRl = LDX(lp, L, PfromR, Ul, lh);
+        v.fOl = LDX(lp, L, PfromO, Ul, lh);
+#endif
+        return v;
+    };
+    auto step_b = [&](const BV &v, int mask) {
+        pRm00 = imin(pRm00, imin(v.wb_k + v.Rm00k, v.Rm00l + v.wb_l));  // :499-508
+        pRm10 = imin(pRm10, v.wbp_k + v.Rm00k);                         // :534-537
+        pRm01 = imin(pRm01, v.Rm00l + v.wbp_l);                         // :520-523
+        pMm00 = imin(pMm00, v.Mm00k + v.wb_k);                          // :552-555
+        pMm01 = imin(pMm01, v.Mm00l + v.wbp_l);                         // :567-570
+        pOm00 = imin(pOm00, v.Om00l + v.wb_l);                          // :603-606
+        pOm01 = imin(pOm01, v.Om00l + v.wbp_l);                         // :618-621
+        fR1 = imin(fR1, v.fRk + v.wp_k + mask);                    // PfromR(i,j,d,l) + WP(k,d-1)     :379-381
+        fMp = imin(fMp, imin(v.PLk, v.PRk) + PB + v.wp_k + mask);  // PfromM'' (:663-679) + WP(k,d-1) :412-414
+        pK2 = imin(pK2, v.Kk + v.wp_k + mask);                     // PK(i,j,d,l) + WP(k,d-1)         :189-192
+        pMm10 = imin(pMm10, v.Mm10l + v.wb_l + mask);              // PMmloop10(i,j,k,d) + WB(d+1,l)  :585-588
+        pOm10 = imin(pOm10, v.Om10l + v.wb_l + mask);              // POmloop10(i,j,k,d) + WB(d+1,l)  :636-639
+        fR2 = imin(fR2, v.fRl + v.wp_l + mask);                    // PfromR(i,j,k,d) + WP(d+1,l)     :382-383
+        fO2 = imin(fO2, v.fOl + v.wp_l + mask);                    // PfromO(i,j,k,d) + WP(d+1,l)     :429-431
+    };
+#ifdef CCJ_ABLATE_LINEAR
+    if (b < 0)
+#endif
+    if (1 + part <= b) {
+        int s = 1 + part;
+        BV cur = load_b(s);
+        for (;;) {
+            const int sn = s + split;
+            const BV nxt = load_b(imin(sn, b));
+            step_b(cur, s < b ? 0 : INF);
+            if (sn > b) break;
+            cur = nxt;
+            s = sn;
+        }
+    }
+    if (split > 1) {
+        // min-reduce the split waves' partial a/b-loop results; part 0 finishes the cell
+        int acc[22] = {pLm00, pLm01, pLm10, pMm00, pMm10, pOm00, pOm10, fL1, fL2, fM, fO1, pK1,
+                       pRm00, pRm01, pRm10, pMm01, pOm01, fR1, fR2, fMp, fO2, pK2};
+        const int cl = wib / split;
+        int *slot = red + ((cl * (split - 1) + (part - 1)) * 22) * 64 + lane;
+        if (part > 0)
+#pragma unroll
+            for (int x = 0; x < 22; ++x) slot[x * 64] = acc[x];
+        __syncthreads();
+        if (part > 0) return;
+        for (int p = 1; p < split; ++p) {
+            const int *src = red + ((cl * (split - 1) + (p - 1)) * 22) * 64 + lane;
+#pragma unroll
+            for (int x = 0; x < 22; ++x) acc[x] = imin(acc[x], src[x * 64]);
+        }
+        pLm00 = acc[0]; pLm01 = acc[1]; pLm10 = acc[2]; pMm00 = acc[3]; pMm10 = acc[4]; pOm00 = acc[5];
+        pOm10 = acc[6]; fL1 = acc[7]; fL2 = acc[8]; fM = acc[9]; fO1 = acc[10]; pK1 = acc[11];
+        pRm00 = acc[12]; pRm01 = acc[13]; pRm10 = acc[14]; pMm01 = acc[15]; pOm01 = acc[16]; fR1 = acc[17];
+        fR2 = acc[18]; fMp = acc[19]; fO2 = acc[20]; pK2 = acc[21];
+        if (!lane_ok) return;
     }
     // ---- single-step seeds (:519, :533, :566, :580), level t-1
     int vPRm01 = pRm01, vPRm10 = pRm10, vPMm01 = pMm01, vPMm10 = pMm10;
@@ -999,7 +1080,17 @@ extern "C" int ccjk_level4d(const DevTables *T, int t, void *stream) {
     const int Mt = m * (m + 1) / 2;
     const int wavesPerA = (Mt + 63) / 64;
     const long waves = (long)(t + 1) * wavesPerA;
-    const long blocks = (waves + 3) / 4;
-    hipLaunchKernelGGL(k_level4d, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *T, t, wavesPerA);
+    // narrow levels: split each chunk's a/b loops over up to 8 waves so ~target waves run at once
+    static const long target = [] {
+        const char *e = getenv("CCJ_SPLIT_TARGET");
+        return e ? atol(e) : 6144L;
+    }();
+    int split = 1;
+    while (split < 8 && waves * split * 2 <= target) split *= 2;
+    const int threads = split <= 4 ? 256 : 64 * split;
+    const int cpb = threads / 64 / split;
+    const long blocks = (waves + cpb - 1) / cpb;
+    const size_t shmem = split > 1 ? (size_t)cpb * (split - 1) * 22 * 64 * sizeof(int) : 0;
+    hipLaunchKernelGGL(k_level4d, dim3((unsigned)blocks), dim3(threads), shmem, (hipStream_t)stream, *T, t, wavesPerA, split);
     return (int)hipGetLastError();
 }

@@ -95,18 +95,25 @@ int  ccj_getW(const ccj_ctx *ctx, int j);
 /* FNV-1a 64 hashes in canonical order: 22 4-D matrices, 8 2-D (ccj_mat2), W. out[31]. */
 int  ccj_hashes(const ccj_ctx *ctx, uint64_t *out);
 
-/* Timing of the last ccj_fill_device (ms, HIP events on the fill stream) and of its dominant
- * kernel family: kernel_ms[0] = 4-D level kernels, [1] = 2-D diagonal kernels, [2] = precompute. */
+/* Timing of the last ccj_fill_device (ms, HIP events on the streams the kernels run on) and of
+ * its kernel families: kernel_ms[0] = k_level4d, [1] = k_diag2d, [2] = precompute. */
 int  ccj_last_timing(const ccj_ctx *ctx, double *fill_ms, double *kernel_ms3);
+/* Sum of the k_iloop (interior-loop pass) times of the last fill (ms). */
+double ccj_iloop_ms(const ccj_ctx *ctx);
 /* Host side of the last fold (ms): out3[0] = wait for the host mirror (D2H tail), [1] = W, [2] = backtrack. */
 int  ccj_host_timing(const ccj_ctx *ctx, double *out3);
-/* Per-level kernel times of the last fill (ms): level_ms[t] (4-D level t), diag_ms[s] (2-D span s). */
+/* Per-level kernel times of the last fill (ms): level_ms[t] (k_level4d, level t), diag_ms[s]
+ * (k_diag2d, span s); ccj_iloop_times: iloop_ms[t] (k_iloop, level t). */
 int  ccj_level_times(const ccj_ctx *ctx, double *level_ms, double *diag_ms, int cap);
+int  ccj_iloop_times(const ccj_ctx *ctx, double *iloop_ms, int cap);
 
 /* Algorithmic work model of this sequence:
  * out[0] = bytes moved by the 4-D level kernels (2 B per int16 operand read + 44 B of writes per cell),
  * out[1] = bytes of the P terms in the 2-D kernels, out[2] = R4 (4-D operand reads), out[3] = cells. */
 int  ccj_work_model(const ccj_ctx *ctx, double *out4);
+/* Split of out[0] by kernel: out2[0] = bytes of k_iloop (interior-loop candidate reads),
+ * out2[1] = bytes of k_level4d (split-point, stack and t-2 reads + 44 B of stores per cell). */
+int  ccj_work_split(const ccj_ctx *ctx, double *out2);
 /* Same model for a bare sequence (no GPU, no context). */
 int  ccj_work_model_seq(const char *seq, int noGU, double *out4);
 

@@ -19,8 +19,11 @@ L.ccj_level_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), 
 lv = (ctypes.c_double * n)()
 dg = (ctypes.c_double * n)()
 L.ccj_level_times(wf._h, lv, dg, n)
+il = (ctypes.c_double * n)()
+L.ccj_iloop_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+L.ccj_iloop_times(wf._h, il, n)
 tm = wf.timing()
 print(json.dumps(tm))
 for t in range(0, n, max(1, n // 25)):
-    print(f"t={t:4d} level4d {lv[t]*1e3:9.1f} us   diag2d {dg[t]*1e3:8.1f} us")
-print("sum level", sum(lv), "sum diag", sum(dg))
+    print(f"t={t:4d} level4d {lv[t]*1e3:9.1f} us   iloop {il[t]*1e3:8.1f} us   diag2d {dg[t]*1e3:8.1f} us")
+print("sum level", sum(lv), "sum iloop", sum(il), "sum diag", sum(dg))
