@@ -88,6 +88,7 @@ struct DevTables {
     // .y = 2*u1*dt (the address cross term); IL_B null entries (dt 63) follow the last one
     uint2 *il, *ilm;               // il: pair (p,p+w) closes the loop (PL, PR); ilm: pair encloses (PM)
     int16_t *dummy;                // n+64 values 32767: target of the null entries
+    const uint32_t *items;         // k_iloop work items (role << 30 | f1 << 20 | f2 << 10 | chunk)
     uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
     int *err;                      // device error word
 };
@@ -104,7 +105,7 @@ extern "C" {
 int ccjk_init2d(const ccj::DevTables *T, void *stream);
 int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
 int ccjk_build_il(const ccj::DevTables *T, void *stream);
-int ccjk_iloop(const ccj::DevTables *T, int t, void *stream);
+int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, void *stream);
 int ccjk_diag2d(const ccj::DevTables *T, int sigma, void *stream);
 int ccjk_level4d(const ccj::DevTables *T, int t, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);

@@ -108,6 +108,8 @@ struct ccj_ctx {
     LvlX *d_ldx = nullptr;
     uint2 *d_il = nullptr, *d_ilm = nullptr;
     int16_t *d_dummy = nullptr;
+    uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
+    std::vector<long long> it_off;        // first item of level t (size n+1)
     uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
     unsigned long long *d_key = nullptr;  // P_P argmin result
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
@@ -1531,6 +1533,66 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         for (int y = 0; y < 8; ++y) pair8[x * 8 + y] = (int8_t)c->pair[x][y];
     }
     HIPCHK(cp, hipMemcpy(c->d_pt, pt.data(), plane, hipMemcpyHostToDevice));
+    // ---- k_iloop work items (one per wave): the closing pairs that can pair, per level, heaviest
+    // first.  item = role << 30 | f1 << 20 | f2 << 10 | chunk
+    {
+        const int rs = c->rs;
+        auto ptp = [&](int p, int q) { return (int)pt[(size_t)(q - p) * rs + p]; };
+        // candidate-list lengths (as k_build_il builds them), used to order the waves
+        std::vector<int> cl((size_t)(n + 1) * rs, 0), cm((size_t)(n + 1) * rs, 0);
+        for (int w = 0; w < n; ++w)
+            for (int p = 1; p + w <= n; ++p) {
+                const int q = p + w;
+                int x = 0, y = 0;
+                for (int u1 = 0; u1 < IE_U; ++u1)
+                    for (int u2 = 0; u2 < IE_U; ++u2) {
+                        if (u1 <= std::min(w, MAXLOOP) - 2 && u2 <= std::min(w - u1 - 6, MAXLOOP - 2) &&
+                            ptp(p + 1 + u1, q - 1 - u2) > 0)
+                            ++x;
+                        const int d = p - 1 - u1, dp = q + 1 + u2;
+                        if (d >= 1 && dp <= n && ptp(d, dp) > 0) ++y;
+                    }
+                cl[(size_t)w * rs + p] = x;
+                cm[(size_t)w * rs + p] = y;
+            }
+        if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
+        std::vector<uint32_t> items;
+        std::vector<std::pair<int, uint32_t>> lvl;
+        c->it_off.assign(n + 1, 0);
+        for (int t = 0; t < n; ++t) {
+            c->it_off[t] = (long long)items.size();
+            const int m = n - t - 2;
+            lvl.clear();
+            if (t < c->nlev && t >= 4) {
+                for (int a = 6; a <= t; ++a)  // PL: (a, i, h-chunk)
+                    for (int i = 1; i <= m; ++i)
+                        if (ptp(i, i + a) > 0)
+                            for (int hc = 0; hc * 64 <= m - i; ++hc)
+                                lvl.push_back({cl[(size_t)a * rs + i], (0u << 30) | ((uint32_t)a << 20) | ((uint32_t)i << 10) | (uint32_t)hc});
+                for (int a = 0; a <= t - 6; ++a)  // PR: (a, q, i-chunk), closing pair (q+a+3, q+t+3)
+                    for (int q = 0; q < m; ++q) {
+                        const int k = q + a + 3, b = t - a;
+                        if (ptp(k, k + b) > 0)
+                            for (int ic = 0; ic * 64 <= q; ++ic)
+                                lvl.push_back({cl[(size_t)b * rs + k], (1u << 30) | ((uint32_t)a << 20) | ((uint32_t)q << 10) | (uint32_t)ic});
+                    }
+                for (int h = 2; h <= m - 1; ++h)  // PM: (h, j, a-chunk)
+                    for (int j = 1; j + h + 2 <= n; ++j) {
+                        const int k = j + h + 2;
+                        const int alo = std::max(2, t - (n - k)), ahi = std::min(t - 2, j - 1);
+                        if (alo > ahi || ptp(j, k) <= 0) continue;
+                        for (int ac = 0; alo + ac * 64 <= ahi; ++ac)
+                            lvl.push_back({cm[(size_t)(h + 2) * rs + j], (2u << 30) | ((uint32_t)h << 20) | ((uint32_t)j << 10) | (uint32_t)ac});
+                    }
+                std::stable_sort(lvl.begin(), lvl.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
+                for (auto &e : lvl) items.push_back(e.second);
+            }
+        }
+        c->it_off[n] = (long long)items.size();
+        HIPCHK(cp, hipMalloc(&c->d_items, std::max<size_t>(items.size(), 1) * sizeof(uint32_t)));
+        if (!items.empty())
+            HIPCHK(cp, hipMemcpy(c->d_items, items.data(), items.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     HIPCHK(cp, hipMemcpy(c->d_hp, hp.data(), plane * sizeof(int), hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_est, est.data(), plane * sizeof(int16_t), hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_pair, pair8, 64, hipMemcpyHostToDevice));
@@ -1588,6 +1650,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.il = c->d_il;
     T.ilm = c->d_ilm;
     T.dummy = c->d_dummy;
+    T.items = c->d_items;
     T.ilseg = c->d_ilseg;
     T.ilmseg = c->d_ilmseg;
     T.err = c->d_err;
@@ -1646,7 +1709,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
         if (s < c->nlev) {
             if (s >= 2) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 2], 0));
             HIPCHK(c, hipEventRecord(ev[2], c->st_il));
-            HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->st_il));
+            HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[s], (int)(c->it_off[s + 1] - c->it_off[s]), c->st_il));
             HIPCHK(c, hipEventRecord(ev[3], c->st_il));
             HIPCHK(c, hipEventRecord(c->il_done[s], c->st_il));
             HIPCHK(c, hipStreamWaitEvent(st, c->il_done[s], 0));
@@ -2013,6 +2076,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_il);
     hipFree(c->d_ilm);
     hipFree(c->d_dummy);
+    hipFree(c->d_items);
     hipFree(c->d_ilseg);
     hipFree(c->d_ilmseg);
     hipFree(c->d_key);

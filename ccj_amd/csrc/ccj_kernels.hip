@@ -523,21 +523,22 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
     return b1;
 }
 
-// grid (ceil(n/4), max(t-5, m-2), 3*nz): z / nz = role, z % nz = lane chunk; 4 waves per block
-__global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, int nz) {
+// one wave per work item (host-built list for level t: closing pairs that can pair, heaviest first)
+__global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long first, int nitems) {
     const int n = T.n, rs = T.rs, m = n - t - 2;
     const int lane = threadIdx.x & 63;
-    const int X = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int Y = blockIdx.y;
-    const int role = (int)blockIdx.z / nz, zc = (int)blockIdx.z - role * nz;
+    const int w = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (w >= nitems) return;
+    const uint32_t it = T.items[first + w];
+    const int role = (int)(it >> 30), f1 = (int)((it >> 20) & 1023u), f2 = (int)((it >> 10) & 1023u);
+    const int zc = (int)(it & 1023u);
     const Lvl16 Lt = T.ld[t];
     const int tl = t - lane;  // A-table lane L describes source level t-L (dt = L)
     const bool lvl_ok = lane >= 2 && lane <= 2 * MAXLOOP - 2 && tl >= 0;
     const long long BIAS = (long long)(n + 64) * (n + 64);  // keeps B >= 0
     if (role == 0) {
         // PL: wave = (a, i, h-chunk), lanes h; closing pair (i, j)
-        const int i = X + 1, a = Y + 6;
-        if (i > m || a > t || zc * 64 > m - i || ptype(T, i, i + a) <= 0) return;
+        const int a = f1, i = f2;
         const int h = zc * 64 + lane;
         const bool act = h <= m - i;
         const unsigned lofs2 = 2u * (unsigned)(act ? h : m - i);  // idle lanes re-read a valid cell
@@ -562,11 +563,9 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, int nz) {
         if (act) T.d4[Lt.lb + (long long)PL * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
     } else if (role == 1) {
         // PR: wave = (a, q, i-chunk), lanes i; closing pair (k, l), q = i+h-1 = k-a-3
-        const int q = X, a = Y;
+        const int a = f1, q = f2;
         const int b = t - a;
-        if (q >= m || b < 6 || zc * 64 > q) return;
-        const int k = q + a + 3, l = k + b;
-        if (ptype(T, k, l) <= 0) return;
+        const int k = q + a + 3;
         const int i = zc * 64 + lane + 1;
         const bool act = i <= q + 1;
         const unsigned lofs2 = 2u * (unsigned)((act ? i : q + 1) - 1);
@@ -589,11 +588,9 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, int nz) {
         if (act) T.d4[Lt.lb + (long long)PR * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
     } else {
         // PM: wave = (h, j, a-chunk), lanes a; pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
-        const int j = X + 1, h = Y + 2;
+        const int h = f1, j = f2;
         const int g = h + 2, k = j + g;
-        if (j > n || h > m - 1 || k > n) return;
         const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, j - 1);
-        if (alo + zc * 64 > ahi || ptype(T, j, k) <= 0) return;
         const int a = alo + zc * 64 + lane;
         const bool act = a <= ahi;
         const int as = act ? a : ahi;
@@ -1061,16 +1058,12 @@ extern "C" int ccjk_build_il(const DevTables *T, void *stream) {
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_iloop(const DevTables *T, int t, void *stream) {
+extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int nitems, void *stream) {
 #ifdef CCJ_ABLATE_ILOOP
     return 0;
 #endif
-    const int n = T->n, m = n - t - 2;
-    if (m <= 0 || t < 4) return 0;
-    const int nz = imax((m + 63) / 64, (t + 64) / 64);
-    const int ny = imax(t - 5, m - 2);
-    if (ny <= 0) return 0;
-    hipLaunchKernelGGL(k_iloop, dim3((n + 3) / 4, ny, 3 * nz), dim3(256), 0, (hipStream_t)stream, *T, t, nz);
+    if (nitems <= 0) return 0;
+    hipLaunchKernelGGL(k_iloop, dim3((unsigned)((nitems + 3) / 4)), dim3(256), 0, (hipStream_t)stream, *T, t, first_item, nitems);
     return (int)hipGetLastError();
 }
 
