@@ -68,7 +68,7 @@ def main():
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--params", default="Turner04")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-n", type=int, default=100)
+    ap.add_argument("--cpu-sample-n", type=int, default=110)
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -125,6 +125,15 @@ def main():
     il_achieved = (bytes_il / max(a.n - 6, 1)) / il_launch_s / 1e9 if il_launch_s > 0 else 0.0
     structure, energy = wf.structure, wf.energy
     wf.close()
+    # HBM traffic per k_level4d launch, measured with rocprofv3 PMC passes (tools/gpu_profile.sh ->
+    # tools/make_profiles.py); null when no profile of this configuration is committed
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tp) and a.n == 200 and a.seed == 5 and a.params == "Turner04":
+        with open(tp) as f:
+            tk = json.load(f)["kernels"].get("k_level4d")
+        if tk:
+            traffic = tk["hbm_bytes_per_launch"]
 
     if rank != 0:
         if dist is not None:
@@ -155,7 +164,8 @@ def main():
         "breakdown_ms": {"fill_device": fill_ms / a.steps, "level4d_kernels": level_ms / a.steps,
                          "iloop_kernels": il_ms / a.steps, "diag2d_kernels": diag_ms / a.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "algorithmic_bytes_per_launch": bytes_lv / nlaunch,
                      "kernel": "k_level4d", "launches_per_fold": nlaunch,
                      "avg_launch_us": avg_launch_s * 1e6, "algorithmic_bytes_per_fold": bytes_lv},
         "roofline_iloop": {"bound": "hbm", "achieved": il_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
