@@ -18,7 +18,7 @@ from typing import Optional
 
 __all__ = [
     "W_final", "ccj", "load_params", "param_path", "CCJError", "BacktrackExit", "lib", "MAT4", "MAT2",
-    "num_cells",
+    "num_cells", "comm_unique_id", "shard_range", "level_layout",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -71,7 +71,10 @@ class _Problem(ctypes.Structure):
 
 
 class _Options(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int), ("overlap_d2h", ctypes.c_int)]
+    _fields_ = [("device", ctypes.c_int), ("overlap_d2h", ctypes.c_int), ("shard_world", ctypes.c_int),
+                ("shard_rank", ctypes.c_int), ("shard_simulate", ctypes.c_int)]
+
+COMM_ID_BYTES = 128
 
 
 _lib = None
@@ -113,6 +116,14 @@ def lib() -> ctypes.CDLL:
     L.ccj_host_timing.restype = ip
     L.ccj_iloop_ms.argtypes = [vp]
     L.ccj_iloop_ms.restype = ctypes.c_double
+    L.ccj_comm_unique_id.argtypes = [cp]
+    L.ccj_comm_unique_id.restype = ip
+    L.ccj_comm_init.argtypes = [vp, cp]
+    L.ccj_comm_init.restype = ip
+    L.ccj_shard_range.argtypes = [ip, ip, ip, ip, ctypes.POINTER(ip), ctypes.POINTER(ip)]
+    L.ccj_shard_range.restype = ip
+    L.ccj_level_layout.argtypes = [ip, ip, ip, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ip)]
+    L.ccj_level_layout.restype = ip
     _lib = L
     return L
 
@@ -157,7 +168,11 @@ class W_final:
     """
 
     def __init__(self, seq: str, dangle: int = 2, params: str | bytes = "DirksPierce09",
-                 noGU: bool = False, device: int = 0, overlap_d2h: bool = True):
+                 noGU: bool = False, device: int = 0, overlap_d2h: bool = True, shard_world: int = 1,
+                 shard_rank: int = 0, shard_simulate: bool = False, comm_id: Optional[bytes] = None):
+        """shard_world > 1: band-shard this one sequence over shard_world processes (one per GPU),
+        exchanging each level over RCCL; every rank passes the same comm_id (from comm_unique_id()
+        on one rank).  shard_simulate runs all shards in this process without an exchange."""
         self.seq = seq
         self.n = len(seq)
         self.dangle = dangle
@@ -167,12 +182,16 @@ class W_final:
         L = lib()
         prob = _Problem(ctypes.cast(self._seq_buf, ctypes.c_char_p), dangle, 1 if noGU else 0,
                         ctypes.cast(self._blob_buf, ctypes.c_void_p), None)
-        opts = _Options(device, 1 if overlap_d2h else 0)
+        opts = _Options(device, 1 if overlap_d2h else 0, shard_world, shard_rank, 1 if shard_simulate else 0)
         h = ctypes.c_void_p()
         rc = L.ccj_create(ctypes.byref(prob), ctypes.byref(opts), ctypes.byref(h))
         if rc != CCJ_OK:
             raise CCJError(rc, L.ccj_last_error(None).decode())
         self._h = h
+        if shard_world > 1 and not shard_simulate:
+            if comm_id is None or len(comm_id) != COMM_ID_BYTES:
+                raise CCJError(CCJ_E_ARG, "sharded context needs the 128-byte comm_id of rank 0")
+            self._check(L.ccj_comm_init(h, comm_id))
         self.structure: Optional[str] = None
         self.energy: Optional[float] = None
         self.stdout_msgs = ""
@@ -248,6 +267,33 @@ class W_final:
             self.close()
         except Exception:
             pass
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id for a sharded fold (broadcast it to every rank)."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    rc = lib().ccj_comm_unique_id(buf)
+    if rc != CCJ_OK:
+        raise CCJError(rc, "ncclGetUniqueId failed")
+    return buf.raw
+
+
+def shard_range(n: int, t: int, world: int, rank: int):
+    """a-blocks [lo, end) of 4-D level t that rank computes in a band-sharded fold (no GPU needed)."""
+    lo, end = ctypes.c_int(), ctypes.c_int()
+    rc = lib().ccj_shard_range(n, t, world, rank, ctypes.byref(lo), ctypes.byref(end))
+    if rc != CCJ_OK:
+        raise CCJError(rc, "bad shard arguments")
+    return lo.value, end.value
+
+
+def level_layout(n: int, t: int, world: int):
+    """(C_t, M_t): per-matrix element stride of level t (padded to world equal chunks), a-block size."""
+    C, M = ctypes.c_longlong(), ctypes.c_int()
+    rc = lib().ccj_level_layout(n, t, world, ctypes.byref(C), ctypes.byref(M))
+    if rc != CCJ_OK:
+        raise CCJError(rc, "bad layout arguments")
+    return C.value, M.value
 
 
 def ccj(seq: str, dangle: int = 2, params: str | bytes = "DirksPierce09", noGU: bool = False,

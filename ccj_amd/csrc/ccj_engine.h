@@ -105,9 +105,10 @@ extern "C" {
 int ccjk_init2d(const ccj::DevTables *T, void *stream);
 int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
 int ccjk_build_il(const ccj::DevTables *T, void *stream);
-int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, void *stream);
+int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, int a_lo, int a_end, void *stream);
 int ccjk_diag2d(const ccj::DevTables *T, int sigma, void *stream);
-int ccjk_level4d(const ccj::DevTables *T, int t, void *stream);
+int ccjk_level4d(const ccj::DevTables *T, int t, int a_lo, int a_end, int copies, void *stream);
+int ccjk_copies(const ccj::DevTables *T, int t, int a_lo, int a_end, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
 int ccjk_pp_argmin(const ccj::DevTables *T, int i, int l, int target, unsigned long long *d_out, void *stream);
 }

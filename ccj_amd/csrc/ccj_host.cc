@@ -10,6 +10,7 @@
 //   pseudo_loop::backtrack                reference src/pseudo_loop.cc:861-2820
 //   W_final::fill_structure               reference src/W_final.cc:764-819
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -86,6 +87,8 @@ struct ccj_ctx {
     int rs = 0;
     int device = 0;
     bool overlap = true;
+    int world = 1, rank = 0, simulate = 0;  // band sharding
+    ncclComm_t comm = nullptr;
 
     // layout
     std::vector<LevelDesc> lv_host;     // device pointers
@@ -109,7 +112,7 @@ struct ccj_ctx {
     uint2 *d_il = nullptr, *d_ilm = nullptr;
     int16_t *d_dummy = nullptr;
     uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
-    std::vector<long long> it_off;        // first item of level t (size n+1)
+    std::vector<long long> it_off;        // first item of (level t, shard r) at t*world + r
     uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
     unsigned long long *d_key = nullptr;  // P_P argmin result
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
@@ -1370,6 +1373,10 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     c->noGU = prob->noGU ? 1 : 0;
     c->device = opts ? opts->device : 0;
     c->overlap = opts ? (opts->overlap_d2h != 0) : true;
+    c->world = (opts && opts->shard_world > 1) ? opts->shard_world : 1;
+    c->rank = (opts && c->world > 1) ? opts->shard_rank : 0;
+    c->simulate = (opts && c->world > 1) ? (opts->shard_simulate != 0) : 0;
+    if (c->rank < 0 || c->rank >= c->world) return CCJ_E_ARG;
     memcpy(&c->prm, prob->params, sizeof(ccj_energy_params));
     if (c->prm.magic != CCJ_PARAMS_MAGIC || c->prm.size_bytes != sizeof(ccj_energy_params))
         return CCJ_E_ARG;
@@ -1411,8 +1418,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         const int m = n - t - 2;
         LevelDesc L{nullptr, 0, 0, m > 0 ? m : 0, 0};
         if (m > 0) {
-            L.M = m * (m + 1) / 2;
-            L.C = (t + 1) * L.M;
+            long long C = 0;
+            ccj_level_layout(n, t, c->world, &C, &L.M);
+            L.C = (int)C;  // padded to world equal a-chunks when sharded
             c->nlev = t + 1;
         }
         c->lv_off[t] = off;
@@ -1420,7 +1428,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         off += (int64_t)NMAT4 * L.C;
     }
     c->total4 = off;
-    if ((uint64_t)off != (uint64_t)NMAT4 * ccj_num_cells(n)) return set_err(c.get(), CCJ_E_ARG, "layout size mismatch");
+    if (c->world == 1 && (uint64_t)off != (uint64_t)NMAT4 * ccj_num_cells(n))
+        return set_err(c.get(), CCJ_E_ARG, "layout size mismatch");
 
     ccj_ctx *cp = c.get();
     HIPCHK(cp, hipSetDevice(c->device));
@@ -1558,18 +1567,23 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
         std::vector<uint32_t> items;
         std::vector<std::pair<int, uint32_t>> lvl;
-        c->it_off.assign(n + 1, 0);
-        for (int t = 0; t < n; ++t) {
-            c->it_off[t] = (long long)items.size();
+        const int G = c->world;
+        c->it_off.assign((size_t)n * G + 1, 0);
+        for (int tr = 0; tr < n * G; ++tr) {
+            const int t = tr / G, r = tr % G;
+            c->it_off[tr] = (long long)items.size();
             const int m = n - t - 2;
             lvl.clear();
-            if (t < c->nlev && t >= 4) {
-                for (int a = 6; a <= t; ++a)  // PL: (a, i, h-chunk)
+            int a_lo = 0, a_end = 0;
+            ccj_shard_range(n, t, G, r, &a_lo, &a_end);
+            const bool mine = c->simulate || r == c->rank;
+            if (mine && t < c->nlev && t >= 4) {
+                for (int a = std::max(6, a_lo); a < a_end; ++a)  // PL: (a, i, h-chunk)
                     for (int i = 1; i <= m; ++i)
                         if (ptp(i, i + a) > 0)
                             for (int hc = 0; hc * 64 <= m - i; ++hc)
                                 lvl.push_back({cl[(size_t)a * rs + i], (0u << 30) | ((uint32_t)a << 20) | ((uint32_t)i << 10) | (uint32_t)hc});
-                for (int a = 0; a <= t - 6; ++a)  // PR: (a, q, i-chunk), closing pair (q+a+3, q+t+3)
+                for (int a = a_lo; a <= std::min(t - 6, a_end - 1); ++a)  // PR: (a, q, i-chunk), closing pair (q+a+3, q+t+3)
                     for (int q = 0; q < m; ++q) {
                         const int k = q + a + 3, b = t - a;
                         if (ptp(k, k + b) > 0)
@@ -1579,7 +1593,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
                 for (int h = 2; h <= m - 1; ++h)  // PM: (h, j, a-chunk)
                     for (int j = 1; j + h + 2 <= n; ++j) {
                         const int k = j + h + 2;
-                        const int alo = std::max(2, t - (n - k)), ahi = std::min(t - 2, j - 1);
+                        const int alo = std::max({2, t - (n - k), a_lo}), ahi = std::min({t - 2, j - 1, a_end - 1});
                         if (alo > ahi || ptp(j, k) <= 0) continue;
                         for (int ac = 0; alo + ac * 64 <= ahi; ++ac)
                             lvl.push_back({cm[(size_t)(h + 2) * rs + j], (2u << 30) | ((uint32_t)h << 20) | ((uint32_t)j << 10) | (uint32_t)ac});
@@ -1588,7 +1602,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
                 for (auto &e : lvl) items.push_back(e.second);
             }
         }
-        c->it_off[n] = (long long)items.size();
+        c->it_off[(size_t)n * G] = (long long)items.size();
         HIPCHK(cp, hipMalloc(&c->d_items, std::max<size_t>(items.size(), 1) * sizeof(uint32_t)));
         if (!items.empty())
             HIPCHK(cp, hipMemcpy(c->d_items, items.data(), items.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1709,13 +1723,43 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
         if (s < c->nlev) {
             if (s >= 2) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 2], 0));
             HIPCHK(c, hipEventRecord(ev[2], c->st_il));
-            HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[s], (int)(c->it_off[s + 1] - c->it_off[s]), c->st_il));
+            const int G = c->world;
+            for (int r = 0; r < G; ++r) {
+                if (!c->simulate && r != c->rank) continue;
+                int lo = 0, hi = 0;
+                ccj_shard_range(n, s, G, r, &lo, &hi);
+                const size_t tr = (size_t)s * G + r;
+                HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[tr], (int)(c->it_off[tr + 1] - c->it_off[tr]), lo, hi,
+                                                 c->st_il));
+            }
             HIPCHK(c, hipEventRecord(ev[3], c->st_il));
             HIPCHK(c, hipEventRecord(c->il_done[s], c->st_il));
             HIPCHK(c, hipStreamWaitEvent(st, c->il_done[s], 0));
             if (s >= 1) HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s - 1], 0));
             HIPCHK(c, hipEventRecord(ev[4], st));
-            HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, st));
+            for (int r = 0; r < G; ++r) {
+                if (!c->simulate && r != c->rank) continue;
+                int lo = 0, hi = 0;
+                ccj_shard_range(n, s, G, r, &lo, &hi);
+                HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, lo, hi, G == 1 ? 1 : 0, st));
+            }
+            if (G > 1) {
+                if (!c->simulate) {
+                    // in-place all-gather of the level: per matrix, rank r owns chunk r of C_t
+                    if (!c->comm) return set_err(c, CCJ_E_STATE, "sharded context without ccj_comm_init");
+                    const LevelDesc &L = c->lv_host[s];
+                    const size_t chunk = (size_t)L.C / G;
+                    if (ncclGroupStart() != ncclSuccess) return set_err(c, CCJ_E_HIP, "ncclGroupStart failed");
+                    for (int x = 0; x < NMAT4; ++x) {
+                        int16_t *base = c->d4 + c->lv_off[s] + (size_t)x * L.C;
+                        if (ncclAllGather(base + chunk * c->rank, base, chunk * sizeof(int16_t), ncclInt8, c->comm, st) !=
+                            ncclSuccess)
+                            return set_err(c, CCJ_E_HIP, "ncclAllGather failed at level %d", s);
+                    }
+                    if (ncclGroupEnd() != ncclSuccess) return set_err(c, CCJ_E_HIP, "ncclGroupEnd failed");
+                }
+                HIPCHK(c, (hipError_t)ccjk_copies(&c->T, s, 0, s + 1, st));
+            }
             HIPCHK(c, hipEventRecord(ev[5], st));
             HIPCHK(c, hipEventRecord(c->lev_done[s], st));
             if (c->overlap && c->h4) {
@@ -2044,6 +2088,46 @@ extern "C" int ccj_iloop_times(const ccj_ctx *c, double *iloop_ms, int cap) {
 
 extern "C" double ccj_iloop_ms(const ccj_ctx *c) { return c ? c->il_ms : 0.0; }
 
+extern "C" int ccj_shard_range(int n, int t, int world, int rank, int *a_lo, int *a_end) {
+    if (!a_lo || !a_end || world < 1 || rank < 0 || rank >= world || t < 0) return CCJ_E_ARG;
+    (void)n;
+    const int B = (t + 1 + world - 1) / world;  // a-blocks per shard (the last one may be short)
+    *a_lo = std::min(rank * B, t + 1);
+    *a_end = std::min((rank + 1) * B, t + 1);
+    return CCJ_OK;
+}
+
+extern "C" int ccj_level_layout(int n, int t, int world, long long *C, int *M) {
+    if (!C || !M || world < 1 || t < 0) return CCJ_E_ARG;
+    const int m = n - t - 2;
+    *M = m > 0 ? m * (m + 1) / 2 : 0;
+    const long long B = world == 1 ? t + 1 : (long long)((t + 1 + world - 1) / world) * world;
+    *C = B * *M;
+    return CCJ_OK;
+}
+
+extern "C" int ccj_comm_unique_id(char *id_out) {
+    if (!id_out) return CCJ_E_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return CCJ_E_HIP;
+    static_assert(sizeof(id) == CCJ_COMM_ID_BYTES, "RCCL unique id size");
+    memcpy(id_out, &id, sizeof id);
+    return CCJ_OK;
+}
+
+extern "C" int ccj_comm_init(ccj_ctx *c, const char *id_in) {
+    if (!c || !id_in) return CCJ_E_ARG;
+    if (c->world == 1 || c->simulate) return CCJ_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    ncclUniqueId id;
+    memcpy(&id, id_in, sizeof id);
+    if (c->comm) ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&c->comm, c->world, id, c->rank);
+    if (r != ncclSuccess) return set_err(c, CCJ_E_HIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    return CCJ_OK;
+}
+
 extern "C" int ccj_n(const ccj_ctx *c) { return c ? c->n : 0; }
 extern "C" const char *ccj_last_error(const ccj_ctx *c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
@@ -2086,6 +2170,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     for (auto e : c->lev_done) hipEventDestroy(e);
     for (auto e : c->p_done) hipEventDestroy(e);
     if (c->st_p) hipStreamDestroy(c->st_p);
+    if (c->comm) ncclCommDestroy(c->comm);
     if (c->st_il) hipStreamDestroy(c->st_il);
     if (c->st_d) hipStreamDestroy(c->st_d);
     for (auto e : c->il_done) hipEventDestroy(e);

@@ -524,7 +524,7 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
 }
 
 // one wave per work item (host-built list for level t: closing pairs that can pair, heaviest first)
-__global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long first, int nitems) {
+__global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long first, int nitems, int a_lo, int a_end) {
     const int n = T.n, rs = T.rs, m = n - t - 2;
     const int lane = threadIdx.x & 63;
     const int w = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -590,7 +590,7 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         // PM: wave = (h, j, a-chunk), lanes a; pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
         const int h = f1, j = f2;
         const int g = h + 2, k = j + g;
-        const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, j - 1);
+        const int alo = imax(imax(2, t - (n - k)), a_lo), ahi = imin(imin(t - 2, j - 1), a_end - 1);
         const int a = alo + zc * 64 + lane;
         const bool act = a <= ahi;
         const int as = act ? a : ahi;
@@ -640,7 +640,7 @@ __global__ __launch_bounds__(512)
 #ifdef CCJ_WAVES_EU
 __attribute__((amdgpu_waves_per_eu(CCJ_WAVES_EU, CCJ_WAVES_EU)))
 #endif
-void k_level4d(DevTables T, int t, int wavesPerA, int split) {
+void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end, int copies) {
 #ifdef CCJ_DEBUG_BOUNDS
     g_dbg_err = T.err;
 #endif
@@ -660,11 +660,13 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split) {
     const int cpb = (int)(blockDim.x >> 6) / split;  // chunks per block
     const int gw = __builtin_amdgcn_readfirstlane(bid * cpb + wib / split);
     const int lane = threadIdx.x & 63;
-    const int a_raw = __builtin_amdgcn_readfirstlane(gw / wavesPerA);
-    if (split == 1 && a_raw > t) return;
-    const bool wave_ok = a_raw <= t;  // grid tail (split > 1 keeps the wave for the barrier)
-    const int a = wave_ok ? a_raw : t;
-    const int chunk = wave_ok ? gw - a * wavesPerA : 0;
+    // this launch computes the a-blocks [a_lo, a_end) of level t (a band shard, §7)
+    const int a_rel = __builtin_amdgcn_readfirstlane(gw / wavesPerA);
+    const int a_raw = a_lo + a_rel;
+    if (split == 1 && a_raw >= a_end) return;
+    const bool wave_ok = a_raw < a_end;  // grid tail (split > 1 keeps the wave for the barrier)
+    const int a = wave_ok ? a_raw : a_end - 1;
+    const int chunk = wave_ok ? gw - a_rel * wavesPerA : 0;
     const int m = n - t - 2;
     const int Mt = (m * (m + 1)) >> 1;
     const int c_raw = chunk * 64 + lane;
@@ -1006,7 +1008,9 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split) {
     dst[POmloop00 * C] = (int16_t)clamp_store(vPOm00);
     dst[POmloop01 * C] = (int16_t)clamp_store(vPOm01);
     dst[POmloop10 * C] = (int16_t)clamp_store(vPOm10);
-    // interior-loop copies, only where a later k_iloop can read them (its pair can pair)
+    // interior-loop copies, only where a later k_iloop can read them (its pair can pair); sharded
+    // fills write them after the level's all-gather instead (k_copies)
+    if (!copies) return;
     const LvlX X = T.ldx[t];
     if (pl_ok) T.d4x[X.lbx + (long long)a * Mt + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = (int16_t)sPL;
     if (pr_ok) {
@@ -1058,21 +1062,62 @@ extern "C" int ccjk_build_il(const DevTables *T, void *stream) {
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int nitems, void *stream) {
+extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int nitems, int a_lo, int a_end,
+                          void *stream) {
 #ifdef CCJ_ABLATE_ILOOP
     return 0;
 #endif
     if (nitems <= 0) return 0;
-    hipLaunchKernelGGL(k_iloop, dim3((unsigned)((nitems + 3) / 4)), dim3(256), 0, (hipStream_t)stream, *T, t, first_item, nitems);
+    hipLaunchKernelGGL(k_iloop, dim3((unsigned)((nitems + 3) / 4)), dim3(256), 0, (hipStream_t)stream, *T, t, first_item,
+                       nitems, a_lo, a_end);
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_level4d(const DevTables *T, int t, void *stream) {
+// ------------------------------------------------------------------------------------------
+// Interior-loop copies of level t for the a-blocks [a_lo, a_end) (sharded fills: after the
+// all-gather the other ranks' cells of level t are present in the main layout but not in the
+// copies).  One lane per cell, main-layout order.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_copies(DevTables T, int t, int a_lo, int a_end) {
+    const int n = T.n, m = n - t - 2, Mt = (m * (m + 1)) >> 1;
+    const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int a = a_lo + (int)(gc / Mt);
+    if (a >= a_end) return;
+    const int c = (int)(gc - (long long)(a - a_lo) * Mt);
+    const float tm = 2.0f * m + 1.0f;
+    int h = (int)((tm - sqrtf(tm * tm - 8.0f * (float)c)) * 0.5f);
+    h = imax(0, imin(h, m - 1));
+    while (h > 0 && h * m - ((h * (h - 1)) >> 1) > c) --h;
+    while (h + 1 < m && (h + 1) * m - (((h + 1) * h) >> 1) <= c) ++h;
+    const int Gh = h * m - ((h * (h - 1)) >> 1);
+    const int i = c - Gh + 1, b = t - a;
+    const int j = i + a, k = j + h + 2, l = k + b;
+    const Lvl16 Lt = T.ld[t];
+    const LvlX X = T.ldx[t];
+    const int16_t *src = T.d4 + Lt.lb + (long long)a * Mt + Gh + i - 1;
+    if (ptype(T, i, j) > 0) T.d4x[X.lbx + (long long)a * Mt + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = src[PL * (long long)Lt.C];
+    if (ptype(T, k, l) > 0) {
+        const int q = i + h - 1;
+        T.d4x[X.lbx + Lt.C + (long long)a * Mt + ((q * (q + 1)) >> 1) + i - 1] = src[PR * (long long)Lt.C];
+    }
+    if (ptype(T, j, k) > 0) T.pmx[X.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = src[PM * (long long)Lt.C];
+}
+
+extern "C" int ccjk_copies(const DevTables *T, int t, int a_lo, int a_end, void *stream) {
+    const int m = T->n - t - 2;
+    if (m <= 0 || a_end <= a_lo) return 0;
+    const long long cells = (long long)(a_end - a_lo) * (m * (m + 1) / 2);
+    hipLaunchKernelGGL(k_copies, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, a_lo, a_end);
+    return (int)hipGetLastError();
+}
+
+extern "C" int ccjk_level4d(const DevTables *T, int t, int a_lo, int a_end, int copies, void *stream) {
     const int m = T->n - t - 2;
     if (m <= 0) return 0;
     const int Mt = m * (m + 1) / 2;
     const int wavesPerA = (Mt + 63) / 64;
-    const long waves = (long)(t + 1) * wavesPerA;
+    if (a_end <= a_lo) return 0;
+    const long waves = (long)(a_end - a_lo) * wavesPerA;
     // narrow levels: split each chunk's a/b loops over up to 8 waves so ~target waves run at once
     static const long target = [] {
         const char *e = getenv("CCJ_SPLIT_TARGET");
@@ -1084,6 +1129,6 @@ extern "C" int ccjk_level4d(const DevTables *T, int t, void *stream) {
     const int cpb = threads / 64 / split;
     const long blocks = (waves + cpb - 1) / cpb;
     const size_t shmem = split > 1 ? (size_t)cpb * (split - 1) * 22 * 64 * sizeof(int) : 0;
-    hipLaunchKernelGGL(k_level4d, dim3((unsigned)blocks), dim3(threads), shmem, (hipStream_t)stream, *T, t, wavesPerA, split);
+    hipLaunchKernelGGL(k_level4d, dim3((unsigned)blocks), dim3(threads), shmem, (hipStream_t)stream, *T, t, wavesPerA, split, a_lo, a_end, copies);
     return (int)hipGetLastError();
 }

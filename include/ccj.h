@@ -63,7 +63,13 @@ typedef struct ccj_ctx ccj_ctx;
 /* Engine options for ccj_create.  device = HIP device ordinal. */
 typedef struct ccj_options {
     int device;
-    int overlap_d2h;   /* 1: stream finished levels to the host mirror while later levels compute */
+    int overlap_d2h;     /* 1: stream finished levels to the host mirror while later levels compute */
+    /* Band sharding of one sequence over shard_world processes (one per GPU):
+     * this process computes the a-blocks ccj_shard_range() gives it and the levels are all-gathered
+     * over RCCL (ccj_comm_init before the first fill).  0 or 1 = unsharded. */
+    int shard_world;
+    int shard_rank;
+    int shard_simulate;  /* 1: run every shard's launches in this one context, no exchange (tests) */
 } ccj_options;
 
 /* Create a context for one sequence: copies the problem, allocates device + pinned host
@@ -106,6 +112,17 @@ int  ccj_host_timing(const ccj_ctx *ctx, double *out3);
  * (k_diag2d, span s); ccj_iloop_times: iloop_ms[t] (k_iloop, level t). */
 int  ccj_level_times(const ccj_ctx *ctx, double *level_ms, double *diag_ms, int cap);
 int  ccj_iloop_times(const ccj_ctx *ctx, double *iloop_ms, int cap);
+
+/* ---- band sharding (one sequence over several GPUs) ---- */
+#define CCJ_COMM_ID_BYTES 128
+/* A fresh RCCL unique id (call on one rank, broadcast the bytes to the others). */
+int  ccj_comm_unique_id(char *id_out);
+/* Join the sharded context to the RCCL communicator of shard_world ranks. */
+int  ccj_comm_init(ccj_ctx *ctx, const char *id);
+/* The a-blocks [*a_lo, *a_end) of level t that rank computes (host helper, no GPU). */
+int  ccj_shard_range(int n, int t, int world, int rank, int *a_lo, int *a_end);
+/* Per-matrix element stride C_t (padded to world equal chunks) and a-block size M_t of level t. */
+int  ccj_level_layout(int n, int t, int world, long long *C, int *M);
 
 /* Algorithmic work model of this sequence:
  * out[0] = bytes moved by the 4-D level kernels (2 B per int16 operand read + 44 B of writes per cell),
