@@ -120,7 +120,7 @@ int main(int argc, char *argv[]) {
         return EXIT_FAILURE;
     }
     ccj_problem prob{seq.c_str(), dangles, noGU, reinterpret_cast<const ccj_energy_params *>(blob.data()), nullptr};
-    ccj_options o{device, 1};
+    ccj_options o{device, 0, 0, 0, 0, 0};  // fill + traceback on the GPU
     ccj_ctx *ctx = nullptr;
     int rc = ccj_create(&prob, &o, &ctx);
     if (rc != CCJ_OK) {

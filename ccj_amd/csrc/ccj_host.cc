@@ -28,6 +28,7 @@
 #include "ccj.h"
 #include "ccj_energy.h"
 #include "ccj_engine.h"
+#include "ccj_backtrack.h"
 
 using namespace ccj;
 
@@ -36,27 +37,6 @@ namespace {
 const int BP_PAIR[8][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 5, 0, 0, 5}, {0, 0, 0, 1, 0, 0, 0, 0},
                            {0, 0, 2, 0, 3, 0, 0, 0}, {0, 6, 0, 4, 0, 0, 0, 6}, {0, 0, 0, 0, 0, 0, 2, 0},
                            {0, 0, 0, 0, 0, 1, 0, 0}, {0, 6, 0, 0, 5, 0, 0, 0}};
-
-// backtrack interval types, reference constants.hh:21-73
-constexpr char T_NONE = 'N', T_HAIRP = 'H', T_INTER = 'I', T_MULTI = 'M';
-constexpr char M_WM = 'B', M_WMv = 'v', M_WMp = 'p', FREE = 'W', LOOP = 'V';
-constexpr char P_P = 'P', P_PK = 'k', P_PL = 'l', P_PR = 'r', P_PM = 'm', P_PO = 'o';
-constexpr char P_PfromL = 'f', P_PfromR = 'g', P_PfromM = 'h', P_PfromMprime = '[', P_PfromMdoubleprime = ']',
-               P_PfromO = 'i';
-constexpr char P_PLiloop = 'j', P_PLiloop5 = 'b', P_PLmloop = 'c', P_PLmloop10 = 'e', P_PLmloop01 = 'n',
-               P_PLmloop00 = 'a';
-constexpr char P_PRiloop = 'q', P_PRiloop5 = 's', P_PRmloop = 't', P_PRmloop10 = 'u', P_PRmloop01 = '&',
-               P_PRmloop00 = '9';
-constexpr char P_PMiloop = 'w', P_PMiloop5 = 'x', P_PMmloop = 'y', P_PMmloop10 = '0', P_PMmloop01 = '1',
-               P_PMmloop00 = '8';
-constexpr char P_POiloop = 'z', P_POiloop5 = '5', P_POmloop = '+', P_POmloop10 = '-', P_POmloop01 = '=',
-               P_POmloop00 = '_';
-constexpr char P_WB = '*', P_WBP = '^', P_WP = '#', P_WPP = '@';
-
-struct Interval {  // reference h_struct.hh:65-92 (seq_interval)
-    int i, j, k, l;
-    char type;
-};
 
 struct BacktrackExit {  // reference exit(...) inside the backtrack
     int code;
@@ -88,6 +68,7 @@ struct ccj_ctx {
     int device = 0;
     bool overlap = true;
     int world = 1, rank = 0, simulate = 0;  // band sharding
+    bool host_tb = false;                   // W + traceback on the host over the mirror (else on the GPU)
     ncclComm_t comm = nullptr;
 
     // layout
@@ -116,6 +97,11 @@ struct ccj_ctx {
     uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
     unsigned long long *d_key = nullptr;  // P_P argmin result
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
+    unsigned long long *d_pk = nullptr;  // P with its first split (k_pterm), [w][p]
+    int *d_W = nullptr, *d_fpair = nullptr;  // device traceback outputs
+    int8_t *d_ftype = nullptr;
+    BtOut *d_btout = nullptr;
+    std::vector<unsigned long long> h_pk;
     int8_t *d_vt = nullptr;
     hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr, st_il = nullptr, st_d = nullptr;
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
@@ -136,6 +122,7 @@ struct ccj_ctx {
 
     double fill_ms = 0, level_ms = 0, diag_ms = 0, pre_ms = 0, il_ms = 0;
     double sync_ms = 0, w_ms = 0, bt_ms = 0;  // host side of the last fold
+    int bt_steps = 0;
     std::string err;
 
     // ---- host accessors (reference getter semantics) ----
@@ -594,21 +581,15 @@ struct Backtracker {
                 const int i = cur.i, l = cur.j;
                 if (i >= l) die("border case: This should not have happened!, P_P");
                 int best_d = 0, best_j = 0, best_k = 0;
-                // The O(sigma^3) argmin runs on the GPU, which still holds PK: first (j,d,k) in the
-                // reference's loop order whose sum equals the minimum P(i,l).
+                // first (j,d,k) in the reference's loop order whose sum equals the minimum P(i,l):
+                // k_pterm keeps it next to the minimum (Pk)
                 const int target = H.Pg(i, l);
                 if (l - i >= 3 && target < INF / 2) {
-                    unsigned long long key = ~0ull;
-                    const int sigma = l - i;
-                    hipError_t e = hipMemcpyAsync(c->d_key, &key, sizeof key, hipMemcpyHostToDevice, c->st);
-                    if (e == hipSuccess) e = (hipError_t)ccjk_pp_argmin(&c->T, i, l, target, c->d_key, c->st);
-                    if (e == hipSuccess) e = hipMemcpyAsync(&key, c->d_key, sizeof key, hipMemcpyDeviceToHost, c->st);
-                    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
-                    if (e != hipSuccess) throw BacktrackExit{2, std::string("CCJ: HIP error in P_P argmin: ") + hipGetErrorString(e) + "\n"};
-                    if (key == ~0ull) throw BacktrackExit{2, "CCJ: P_P argmin found no split matching P(i,l)\n"};
-                    best_j = i + (int)(key / ((unsigned long long)sigma * sigma));
-                    best_d = i + (int)((key / sigma) % sigma);
-                    best_k = i + (int)(key % sigma);
+                    const unsigned long long key = c->h_pk[c->a2(i, l)];
+                    const unsigned sig = (unsigned)(l - i), kk = (unsigned)(key & 0xffffffffull);
+                    best_j = i + (int)(kk / (sig * sig));
+                    best_d = i + (int)((kk / sig) % sig);
+                    best_k = i + (int)(kk % sig);
                 }
                 push4(i, best_k, best_j, best_d + 1, P_PK);
                 push4(best_j + 1, l, best_d, best_k + 1, P_PK);
@@ -1376,6 +1357,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     c->world = (opts && opts->shard_world > 1) ? opts->shard_world : 1;
     c->rank = (opts && c->world > 1) ? opts->shard_rank : 0;
     c->simulate = (opts && c->world > 1) ? (opts->shard_simulate != 0) : 0;
+    c->host_tb = opts ? (opts->host_traceback != 0) : false;
     if (c->rank < 0 || c->rank >= c->world) return CCJ_E_ARG;
     memcpy(&c->prm, prob->params, sizeof(ccj_energy_params));
     if (c->prm.magic != CCJ_PARAMS_MAGIC || c->prm.size_bytes != sizeof(ccj_energy_params))
@@ -1501,6 +1483,11 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         HIPCHK(cp, hipMemset(c->d_ilmseg, 0, pairs * IL_SEG * sizeof(uint32_t)));
     }
     HIPCHK(cp, hipMalloc(&c->d2i, A2_N * plane * sizeof(int)));
+    HIPCHK(cp, hipMalloc(&c->d_pk, plane * sizeof(unsigned long long)));
+    HIPCHK(cp, hipMalloc(&c->d_W, (n + 1) * sizeof(int)));
+    HIPCHK(cp, hipMalloc(&c->d_fpair, (n + 1) * sizeof(int)));
+    HIPCHK(cp, hipMalloc(&c->d_ftype, (n + 1)));
+    HIPCHK(cp, hipMalloc(&c->d_btout, sizeof(BtOut)));
     HIPCHK(cp, hipMalloc(&c->d_vt, plane));
     if (c->total4 > 0 && hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
         return set_err(cp, CCJ_E_OOM, "pinned host allocation of %.2f GB failed", c->total4 * 2e-9);
@@ -1647,6 +1634,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.WMv = c->d2i + A2_WMV * plane;
     T.WMp = c->d2i + A2_WMP * plane;
     T.P = c->d2i + A2_P * plane;
+    T.Pk = c->d_pk;
     T.WBP = c->d2i + A2_WBP * plane;
     T.WPP = c->d2i + A2_WPP * plane;
     T.WB = c->d2i + A2_WB * plane;
@@ -1839,6 +1827,8 @@ extern "C" int ccj_sync_host(ccj_ctx *c) {
     }
     HIPCHK(c, hipMemcpy(c->h2i.data(), c->d2i, A2_N * plane * sizeof(int), hipMemcpyDeviceToHost));
     HIPCHK(c, hipMemcpy(c->hvt.data(), c->d_vt, plane, hipMemcpyDeviceToHost));
+    c->h_pk.resize(plane);
+    HIPCHK(c, hipMemcpy(c->h_pk.data(), c->d_pk, plane * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     c->mirrored = true;
     return CCJ_OK;
 }
@@ -1846,48 +1836,109 @@ extern "C" int ccj_sync_host(ccj_ctx *c) {
 extern "C" int ccj_fill(ccj_ctx *c) {
     int rc = ccj_fill_device(c);
     if (rc) return rc;
-    return ccj_sync_host(c);
+    // the device traceback needs no host mirror; getters make it on demand (ccj_sync_host)
+    return c->host_tb ? ccj_sync_host(c) : CCJ_OK;
 }
+
+namespace {
+int ensure_mirror(const ccj_ctx *cc) {
+    ccj_ctx *c = const_cast<ccj_ctx *>(cc);
+    return c->mirrored ? CCJ_OK : ccj_sync_host(c);
+}
+
+// W + traceback on the GPU (ccj_backtrack.hip); brackets on the host
+int device_result(ccj_ctx *c, std::string &structure, std::string &out) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int n = c->n;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, (hipError_t)ccjk_compute_W(&c->T, c->d_W, c->st));
+    const int cap = std::min(4 * n + 64, 3000);
+    HIPCHK(c, (hipError_t)ccjk_backtrack(&c->T, c->d_W, c->d_fpair, c->d_ftype, c->d_btout, cap, c->st));
+    BtOut bo{};
+    std::vector<int> fp(n + 1);
+    std::vector<int8_t> ft(n + 1);
+    c->W.assign(n + 1, 0);
+    HIPCHK(c, hipMemcpyAsync(c->W.data(), c->d_W, (n + 1) * sizeof(int), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(fp.data(), c->d_fpair, (n + 1) * sizeof(int), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(ft.data(), c->d_ftype, n + 1, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(&bo, c->d_btout, sizeof bo, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    c->w_ms = 0;
+    c->bt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->bt_steps = bo.steps;
+    for (int x = 0; x < bo.n_snbh; ++x) out += "Should not be here!\n";
+    switch (bo.status) {
+        case BT_OK: break;
+        case BT_DIE:
+            c->err = std::string(bt_prefix(bo.prefix)) + "This should not have happened!, " + bt_case_name(bo.node) + "\n";
+            return CCJ_E_BACKTRACK;
+        case BT_INTER: {
+            char buf[160];
+            snprintf(buf, sizeof buf, "NOT GOOD RESTR INTER, i=%d, j=%d, best_ip=%d, best_jp=%d\n", bo.args[0], bo.args[1],
+                     bo.args[2], bo.args[3]);
+            c->err = buf;
+            return CCJ_E_INTER_EXIT;
+        }
+        case BT_ASSERT:
+            c->err = "CCJ: matrices.hh:167: Assertion `!(i<=0 || l> n_)' failed.\n";
+            return CCJ_E_BACKTRACK;
+        default:
+            return set_err(c, CCJ_E_HIP, "device traceback stack overflow (capacity %d)", cap);
+    }
+    HostView H(c);
+    Backtracker B(H, c);
+    for (int x = 1; x <= n; ++x) {
+        B.f[x].pair = fp[x];
+        B.f[x].type = (char)ft[x];
+    }
+    B.fill_structure();
+    structure = B.structure;
+    return CCJ_OK;
+}
+}  // namespace
 
 extern "C" int ccj_result(ccj_ctx *c, char *structure, double *energy_kcal, char *msgs, int msgs_cap) {
     if (!c) return CCJ_E_ARG;
-    if (!c->mirrored) return set_err(c, CCJ_E_STATE, "ccj_result before ccj_fill");
-    const auto t0 = std::chrono::steady_clock::now();
-    compute_W(c);
-    const auto t1 = std::chrono::steady_clock::now();
-    c->w_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    HostView H(c);
-    Backtracker B(H, c);
+    if (!c->filled) return set_err(c, CCJ_E_STATE, "ccj_result before ccj_fill");
+    std::string st, out;
     int rc = CCJ_OK;
-    struct Rec {
-        ccj_ctx *c;
-        std::chrono::steady_clock::time_point t1;
-        ~Rec() { c->bt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count(); }
-    } rec{c, t1};
-    try {
-        B.run();
-        B.fill_structure();
-    } catch (const BacktrackExit &e) {
-        c->err = e.stderr_msg;
-        rc = e.code == 0 ? CCJ_E_INTER_EXIT : e.code == 2 ? CCJ_E_HIP : CCJ_E_BACKTRACK;
-        if (e.code == 134 || e.code == 139) rc = CCJ_E_BACKTRACK;
+    if (!c->host_tb) {
+        rc = device_result(c, st, out);
+    } else {
+        if (int e = ensure_mirror(c)) return e;
+        const auto t0 = std::chrono::steady_clock::now();
+        compute_W(c);
+        const auto t1 = std::chrono::steady_clock::now();
+        c->w_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        HostView H(c);
+        Backtracker B(H, c);
+        try {
+            B.run();
+            B.fill_structure();
+        } catch (const BacktrackExit &e) {
+            c->err = e.stderr_msg;
+            rc = e.code == 0 ? CCJ_E_INTER_EXIT : e.code == 2 ? CCJ_E_HIP : CCJ_E_BACKTRACK;
+        }
+        c->bt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        st = B.structure;
+        out = B.out;
     }
     if (msgs && msgs_cap > 0) {
-        const size_t nb = std::min((size_t)msgs_cap - 1, B.out.size());
-        memcpy(msgs, B.out.data(), nb);
+        const size_t nb = std::min((size_t)msgs_cap - 1, out.size());
+        memcpy(msgs, out.data(), nb);
         msgs[nb] = 0;
     }
     if (rc != CCJ_OK) return rc;
     if (energy_kcal) *energy_kcal = c->W[c->n] / 100.0;
     if (structure) {
-        memcpy(structure, B.structure.data() + 1, c->n);
+        memcpy(structure, st.data() + 1, c->n);
         structure[c->n] = 0;
     }
     return CCJ_OK;
 }
 
 extern "C" int ccj_get4(const ccj_ctx *c, int mat, int i, int j, int k, int l) {
-    if (!c || !c->mirrored || mat < 0 || mat >= NMAT4) return INF;
+    if (!c || !c->filled || ensure_mirror(c) || mat < 0 || mat >= NMAT4) return INF;
     if (!(i <= j && j < k - 1 && k <= l)) return INF;
     if (i < 1 || l > c->n) return INF;
     const int t = (j - i) + (l - k);
@@ -1895,7 +1946,7 @@ extern "C" int ccj_get4(const ccj_ctx *c, int mat, int i, int j, int k, int l) {
 }
 
 extern "C" int ccj_get2(const ccj_ctx *c, int mat, int i, int j) {
-    if (!c || !c->mirrored || i < 1 || j > c->n || i > j) return INF;
+    if (!c || !c->filled || ensure_mirror(c) || i < 1 || j > c->n || i > j) return INF;
     switch (mat) {
         case CCJ_M2_P: return c->raw2(A2_P, i, j);
         case CCJ_M2_WBP: return c->raw2(A2_WBP, i, j);
@@ -1915,7 +1966,7 @@ extern "C" int ccj_getW(const ccj_ctx *c, int j) {
 }
 
 extern "C" int ccj_hashes(const ccj_ctx *c, uint64_t *out) {
-    if (!c || !c->mirrored || !out) return CCJ_E_STATE;
+    if (!c || !c->filled || !out || ensure_mirror(c)) return CCJ_E_STATE;
     const int n = c->n;
     const uint64_t H0 = 1469598103934665603ull;
     for (int m = 0; m < NMAT4; ++m) {
@@ -2165,6 +2216,11 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_ilmseg);
     hipFree(c->d_key);
     hipFree(c->d2i);
+    hipFree(c->d_pk);
+    hipFree(c->d_W);
+    hipFree(c->d_fpair);
+    hipFree(c->d_ftype);
+    hipFree(c->d_btout);
     hipFree(c->d_vt);
     if (c->h4) hipHostFree(c->h4);
     for (auto e : c->lev_done) hipEventDestroy(e);

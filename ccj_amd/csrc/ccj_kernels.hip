@@ -148,6 +148,7 @@ __global__ void k_init2d(DevTables T, int total) {
         T.Vt[x] = 'N';
         T.WM[x] = T.WMv[x] = T.WMp[x] = INF + 1;
         T.P[x] = T.WBP[x] = T.WPP[x] = INF + 1;
+        T.Pk[x] = ~0ull;
         T.WB[x] = 0;
         T.WP[x] = 0;
     }
@@ -254,7 +255,11 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
     }
 
     // ---- P(i,l) was reduced into T.P by k_pterm(sigma) (ordered before this kernel by an event)
-    if (tid == 0) sh_p = T.P[cell];
+    if (tid == 0) {  // value half of k_pterm's (value, first split) minimum; never set -> INF+1
+        const unsigned long long pk = T.Pk[cell];
+        sh_p = pk == ~0ull ? INF + 1 : (int)((unsigned)(pk >> 32) - 0x80000000u);
+        T.P[cell] = sh_p;
+    }
     __syncthreads();
     const int v_il = sh_v, p_il = sh_p;
 
@@ -353,7 +358,7 @@ extern "C" int ccjk_pp_argmin(const DevTables *T, int i, int l, int target, unsi
 constexpr int PT_WAVES = 4;  // waves per k_pterm workgroup = consecutive do values sharing jo
 
 __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngroups) {
-    __shared__ int red[PT_WAVES][64];
+    __shared__ unsigned long long red[PT_WAVES][64];
     const int n = T.n;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -364,7 +369,8 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
     if (dd0 > sigma - 2) return;  // whole workgroup
     const int dd = dd0 + w;
     const int i = grp * 64 + lane + 1;
-    int best = INF + 1;
+    // (value, key) of the first minimum in the reference's loop order, key = (jo*sigma + do)*sigma + ko
+    unsigned long long best = ~0ull;
     if (dd <= sigma - 2 && i + sigma <= n) {
         // PK(i, j, d+1, k): level jo+(ko-dd-1), a = jo, h = dd-jo-1, interval start i
         // PK(j+1, d, k+1, l): level (dd-jo-1)+(sigma-ko-1), a = dd-jo-1, h = ko-dd-1, start i+jo+1
@@ -372,6 +378,8 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
         const int g1 = (h1 * (h1 - 1)) >> 1;
         const int16_t *__restrict__ D4 = T.d4;
         const Lvl16 *__restrict__ LD = T.ld;
+        const unsigned kbase = ((unsigned)jo * (unsigned)sigma + (unsigned)dd) * (unsigned)sigma;
+        int bv = INF + 1, bk = 0;
 #pragma unroll 4
         for (int ko = dd + 1; ko < sigma; ++ko) {
             const int h2 = ko - dd - 1;
@@ -380,14 +388,19 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
             const int o1 = PK * L1.C + a1 * L1.M + h1 * (n - t1 - 2) - g1 - 1;
             const int o2 = PK * L2.C + a2 * L2.M + h2 * (n - t2 - 2) - ((h2 * (h2 - 1)) >> 1) + jo;
             const int v = (int)(D4 + L1.lb + o1)[i] + (int)(D4 + L2.lb + o2)[i];
-            best = imin(best, v);
+            if (v < bv) {  // strict: keeps the first ko of the minimum
+                bv = v;
+                bk = ko;
+            }
         }
+        if (bv <= INF) best = ((unsigned long long)((unsigned)bv + 0x80000000u) << 32) | (kbase + (unsigned)bk);
     }
     red[w][lane] = best;
     __syncthreads();
     if (w == 0 && i + sigma <= n) {
-        int v = imin(imin(red[0][lane], red[1][lane]), imin(red[2][lane], red[3][lane]));
-        if (v <= INF) atomicMin(T.P + sigma * T.rs + i, v);
+        unsigned long long v = red[0][lane];
+        for (int x = 1; x < PT_WAVES; ++x) v = red[x][lane] < v ? red[x][lane] : v;
+        if (v != ~0ull) atomicMin(T.Pk + sigma * T.rs + i, v);
     }
 }
 

@@ -70,6 +70,9 @@ typedef struct ccj_options {
     int shard_world;
     int shard_rank;
     int shard_simulate;  /* 1: run every shard's launches in this one context, no exchange (tests) */
+    /* 0 (default): W and the traceback run on the GPU (no host copy of the 4-D matrices; getters
+     * copy them on first use).  1: on the host over the mirror (the reference restatement). */
+    int host_traceback;
 } ccj_options;
 
 /* Create a context for one sequence: copies the problem, allocates device + pinned host

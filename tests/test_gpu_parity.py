@@ -107,3 +107,51 @@ def test_determinism_and_mirror_modes():
     finally:
         a.close()
         b.close()
+
+
+def _result(wf):
+    from ccj_amd import BacktrackExit
+    try:
+        e = wf.result()
+        return ("ok", e, wf.structure, wf.stdout_msgs)
+    except BacktrackExit as ex:
+        return ("exit", ex.exit_code, ex.msg, ex.stdout)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_device_traceback_equals_host_traceback(seed):
+    """The GPU traceback (ccj_backtrack.hip, wave-parallel first-minimum scans) and the host
+    restatement over the mirror give the same MFE, brackets, stdout lines and exits."""
+    r = random.Random(7000 + seed)
+    n = r.choice([24, 40, 64, 90, 130])
+    seq = _rseq(9000 + seed, n, r.choice(["ACGU", "GGCCAU", "GCAU"]))
+    params = r.choice(["Turner04", "DirksPierce09", "DirksPierce03", "CaoChen09", "Matthews04"])
+    d, g = r.choice([0, 1, 2]), r.random() < 0.25
+    dev = _wf(seq, params, d, g)
+    host = _wf(seq, params, d, g, host_traceback=True, overlap_d2h=True)
+    try:
+        dev.fill()
+        host.fill()
+        assert _result(dev) == _result(host)
+        assert [dev.W(j) for j in range(n + 1)] == [host.W(j) for j in range(n + 1)]
+    finally:
+        dev.close()
+        host.close()
+
+
+@pytest.mark.parametrize("case", [c for c in E2E if len(c["seq"]) >= 30][:20],
+                         ids=lambda c: f"n{len(c['seq'])}-{c['params']}-d{c['dangles']}-g{c['noGU']}")
+def test_host_traceback_matches_reference(case):
+    """The host restatement (mirror path) against the reference's CLI output, so both traceback
+    implementations stay pinned."""
+    wf = _wf(case["seq"], case["params"], case["dangles"], case["noGU"], host_traceback=True)
+    try:
+        wf.fill()
+        res = _result(wf)
+        last = case["stdout"].splitlines()[-1] if case["stdout"] else ""
+        if res[0] == "ok":
+            assert f"{res[2]} ({res[1]:g})" == last
+        else:
+            assert res[1] == case["rc"] and res[2] == case["stderr"]
+    finally:
+        wf.close()
