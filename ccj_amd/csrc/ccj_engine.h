@@ -111,5 +111,4 @@ int ccjk_diag2d(const ccj::DevTables *T, int sigma, void *stream);
 int ccjk_level4d(const ccj::DevTables *T, int t, int a_lo, int a_end, int copies, void *stream);
 int ccjk_copies(const ccj::DevTables *T, int t, int a_lo, int a_end, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
-int ccjk_pp_argmin(const ccj::DevTables *T, int i, int l, int target, unsigned long long *d_out, void *stream);
 }

@@ -95,7 +95,6 @@ struct ccj_ctx {
     uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
     std::vector<long long> it_off;        // first item of (level t, shard r) at t*world + r
     uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
-    unsigned long long *d_key = nullptr;  // P_P argmin result
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
     unsigned long long *d_pk = nullptr;  // P with its first split (k_pterm), [w][p]
     int *d_W = nullptr, *d_fpair = nullptr;  // device traceback outputs
@@ -1452,7 +1451,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipMalloc(&c->d_lv, c->lv_host.size() * sizeof(LevelDesc)));
     HIPCHK(cp, hipMalloc(&c->d_lb, c->lv_off.size() * sizeof(long long)));
     HIPCHK(cp, hipMalloc(&c->d_ld, c->lv_off.size() * sizeof(Lvl16)));
-    HIPCHK(cp, hipMalloc(&c->d_key, sizeof(unsigned long long)));
     {
         // interior-loop copies (ccj_engine.h): PLx+PRx mirror the level sizes, PMx is padded per (h, j)
         std::vector<LvlX> ldx(c->lv_off.size(), LvlX{0, 0});
@@ -1489,7 +1487,10 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipMalloc(&c->d_ftype, (n + 1)));
     HIPCHK(cp, hipMalloc(&c->d_btout, sizeof(BtOut)));
     HIPCHK(cp, hipMalloc(&c->d_vt, plane));
-    if (c->total4 > 0 && hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
+    // the pinned host mirror is only needed by the host traceback and the getters: allocate it up
+    // front when the fill streams into it, else on first use (ccj_sync_host)
+    if (c->overlap && c->total4 > 0 &&
+        hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
         return set_err(cp, CCJ_E_OOM, "pinned host allocation of %.2f GB failed", c->total4 * 2e-9);
     c->h2i.assign(A2_N * plane, 0);
     c->hvt.assign(plane, 0);
@@ -1820,9 +1821,11 @@ extern "C" int ccj_sync_host(ccj_ctx *c) {
     } rec{c, t0};
     HIPCHK(c, hipSetDevice(c->device));
     const size_t plane = (size_t)(c->n + 1) * c->rs;
-    if (c->overlap) {
+    if (c->overlap && c->h4) {
         HIPCHK(c, hipStreamSynchronize(c->st_copy));
-    } else if (c->h4) {
+    } else if (c->total4 > 0) {
+        if (!c->h4 && hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
+            return set_err(c, CCJ_E_OOM, "pinned host allocation of %.2f GB failed", c->total4 * 2e-9);
         HIPCHK(c, hipMemcpy(c->h4, c->d4, (size_t)c->total4 * sizeof(int16_t), hipMemcpyDeviceToHost));
     }
     HIPCHK(c, hipMemcpy(c->h2i.data(), c->d2i, A2_N * plane * sizeof(int), hipMemcpyDeviceToHost));
@@ -2214,7 +2217,6 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_items);
     hipFree(c->d_ilseg);
     hipFree(c->d_ilmseg);
-    hipFree(c->d_key);
     hipFree(c->d2i);
     hipFree(c->d_pk);
     hipFree(c->d_W);

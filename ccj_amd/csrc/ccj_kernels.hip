@@ -321,40 +321,13 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
 // P(i, i+sigma) = min over i<=j<d<k<l of PK(i,j,d+1,k) + PK(j+1,d,k+1,l)   (pseudo_loop.cc:166-179)
 // One wave = (jo = j-i, do = d-i, a group of 64 consecutive intervals i), looping over k: for fixed
 // offsets the two PK cells of neighbouring intervals are neighbours in HBM, so every load is
-// coalesced.  The 4 waves of a workgroup (4 consecutive do) min-reduce in LDS, then one atomicMin
-// per interval into T.P (initialised INF+1 = "never set"; every candidate is <= 65534 < INF/2,
-// A-Q4).  Needs PK levels
+// coalesced.  Each lane keeps its first minimum in the reference's loop order as one 64-bit key,
+// (P + 2^31) << 32 | (j-i, d-i, k-i) split, the 4 waves of a workgroup (4 consecutive do)
+// min-reduce it in LDS, and one 64-bit atomicMin per interval lands in T.Pk (initialised all-ones
+// = "never set"; every candidate is <= 65534 < INF/2, A-Q4).  k_diag2d(sigma) takes P from it and
+// the P_P traceback its split (pseudo_loop.cc:867-896), without a rescan.  Needs PK levels
 // <= sigma-3 only, so it runs on a side stream three levels ahead of k_diag2d(sigma).
 // ------------------------------------------------------------------------------------------
-// Backtrack helper for the P_P case (pseudo_loop.cc:867-896): the first (j,d,k) in the reference
-// loop order (j, then d, then k ascending) whose PK(i,j,d+1,k) + PK(j+1,d,k+1,l) equals P(i,l).
-// Keys are lexicographic in (j,d,k), so an atomicMin over matching keys returns that first one.
-__global__ void k_pp_argmin(DevTables T, int i, int l, int target, unsigned long long *out) {
-    const int sigma = l - i;
-    const int jo = blockIdx.y;
-    const int d_o = jo + 1 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (d_o > sigma - 2) return;
-    const int j = i + jo, d = i + d_o;
-    for (int k = d + 1; k < l; ++k) {
-        const int v = ld4(T, PK, (j - i) + (k - d - 1), j - i, d - 1 - j, i) +
-                      ld4(T, PK, (d - j - 1) + (l - k - 1), d - j - 1, k - 1 - d, j + 1);
-        if (v == target) {
-            const unsigned long long key = ((unsigned long long)jo * (unsigned)sigma + (unsigned)d_o) * (unsigned)sigma +
-                                           (unsigned)(k - i);
-            atomicMin(out, key);
-            return;
-        }
-    }
-}
-
-extern "C" int ccjk_pp_argmin(const DevTables *T, int i, int l, int target, unsigned long long *d_out, void *stream) {
-    const int sigma = l - i;
-    if (sigma < 3) return 0;
-    dim3 grid((sigma + 255) / 256, sigma - 2);
-    hipLaunchKernelGGL(k_pp_argmin, grid, dim3(256), 0, (hipStream_t)stream, *T, i, l, target, d_out);
-    return (int)hipGetLastError();
-}
-
 constexpr int PT_WAVES = 4;  // waves per k_pterm workgroup = consecutive do values sharing jo
 
 __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngroups) {
