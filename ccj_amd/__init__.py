@@ -17,7 +17,7 @@ import os
 from typing import Optional
 
 __all__ = [
-    "W_final", "ccj", "load_params", "param_path", "CCJError", "BacktrackExit", "lib", "MAT4", "MAT2",
+    "W_final", "ccj", "load_params", "load_par", "ParFileError", "param_path", "CCJError", "BacktrackExit", "lib", "MAT4", "MAT2",
     "num_cells", "comm_unique_id", "shard_range", "level_layout",
 ]
 
@@ -36,6 +36,7 @@ MAT2 = ["P", "WBP", "WPP", "V", "Vtype", "WM", "WMv", "WMp"]
 HASH_NAMES = MAT4 + MAT2 + ["W"]
 
 CCJ_OK, CCJ_E_ARG, CCJ_E_OOM, CCJ_E_HIP, CCJ_E_PARAMS, CCJ_E_BACKTRACK, CCJ_E_STATE, CCJ_E_INTER_EXIT = range(8)
+CCJ_E_PARFILE = 8  # include/ccj_parfile.h
 
 # name -> blob file (the reference's params/*.par sets, dumped to our table format)
 PARAM_SETS = {
@@ -124,6 +125,10 @@ def lib() -> ctypes.CDLL:
     L.ccj_shard_range.restype = ip
     L.ccj_level_layout.argtypes = [ip, ip, ip, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ip)]
     L.ccj_level_layout.restype = ip
+    L.ccj_params_load_par.argtypes = [cp, cp, cp, cp, ip]
+    L.ccj_params_load_par.restype = ip
+    L.ccj_params_load_par_string.argtypes = [cp, cp, cp, cp, ip]
+    L.ccj_params_load_par_string.restype = ip
     _lib = L
     return L
 
@@ -137,6 +142,7 @@ def num_cells(n: int) -> int:
 
 
 def param_path(name_or_path: str) -> str:
+    """Bundled blob for a parameter-set name ("Turner04", "rna_Turner04.par", ...) or a .ccjp path."""
     if os.path.exists(name_or_path) and name_or_path.endswith(".ccjp"):
         return name_or_path
     base = os.path.basename(name_or_path)
@@ -148,16 +154,62 @@ def param_path(name_or_path: str) -> str:
     raise CCJError(CCJ_E_ARG, f"unknown parameter set {name_or_path!r}")
 
 
-_PARAM_CACHE: dict = {}
+class ParFileError(CCJError):
+    """A .par file the reference loader rejects: it prints ``log`` on stderr and exits 1."""
+
+    def __init__(self, log: str):
+        super().__init__(CCJ_E_PARFILE, log)
+        self.log = log
 
 
-def load_params(name_or_path: str = "DirksPierce09") -> bytes:
-    """Scaled 37 C energy tables (include/ccj_params.h) for one of the reference parameter sets."""
-    p = param_path(name_or_path)
+def load_par(path: str, base: bytes | None = None, text: bool = False):
+    """Read a ViennaRNA v2.0 parameter file natively (include/ccj_parfile.h).
+
+    ``base`` is the table state the file lands on (default: the reference's compiled-in
+    defaults, ccj_amd/params/default.ccjp).  ``text=True`` treats ``path`` as the file contents
+    (vrna_params_load_from_string).  Returns (applied, blob, log): applied is 1 when the file was
+    parsed, 0 when it could not be opened or was empty (blob == base); log is what the reference
+    prints on stderr.  Raises ParFileError where the reference exits 1.
+    """
+    if base is None:
+        base = _read_blob(os.path.join(PARAM_DIR, "default.ccjp"))
+    L = lib()
+    out = ctypes.create_string_buffer(len(base))
+    cap = 1 << 22
+    log = ctypes.create_string_buffer(cap)
+    fn = L.ccj_params_load_par_string if text else L.ccj_params_load_par
+    rc = fn(path.encode(), bytes(base), out, log, cap)
+    msg = log.value.decode(errors="replace")
+    if rc == CCJ_E_PARFILE:
+        raise ParFileError(msg)
+    if rc < 0:
+        raise CCJError(CCJ_E_ARG, "bad parameter base blob")
+    return rc, out.raw, msg
+
+
+def _read_blob(p: str) -> bytes:
     if p not in _PARAM_CACHE:
         with open(p, "rb") as f:
             _PARAM_CACHE[p] = f.read()
     return _PARAM_CACHE[p]
+
+
+_PARAM_CACHE: dict = {}
+
+
+def load_params(name_or_path: str = "DirksPierce09") -> bytes:
+    """Scaled 37 C energy tables (include/ccj_params.h).
+
+    An existing .par file is read natively over the compiled-in defaults (like the reference's
+    vrna_params_load); an existing .ccjp is used as is; otherwise the name selects one of the
+    bundled sets (Turner04, DirksPierce09, ... — dumps of the reference's own files).
+    """
+    if os.path.isfile(name_or_path) and not name_or_path.endswith(".ccjp"):
+        key = ("par", os.path.abspath(name_or_path), os.path.getmtime(name_or_path))
+        if key not in _PARAM_CACHE:
+            _PARAM_CACHE[key] = load_par(name_or_path)[1]
+        return _PARAM_CACHE[key]
+    return _read_blob(param_path(name_or_path))
 
 
 class W_final:

@@ -1,21 +1,29 @@
 // ccj_cli.cc — the `CCJ` command line on top of libccj_hip.so (drop-in for reference src/CCJ.cc).
 //
-//   CCJ [-i FILE] [-d N] [-P paramfile] [--noConv] [--noGU] [sequence]
+//   CCJ [-h] [-V] [-i FILE] [-d N] [-P paramfile] [--noConv] [--noGU] [sequence]
 //
-// Mirrors reference CCJ.cc:58-115 and ccj.ggo:13-31: sequence from argv[0] or the first stdin
-// line (not read at all when -i is given), toupper, T->U unless --noConv, validation messages on
-// stdout + exit 1, "Not a valid parameter file!" on stderr + exit 1, DNA Mathews 2004 + noGU when
-// a 'T' survives, output "SEQ\nSTRUCT (E)\n" with std::cout's default double formatting, and the
-// reference's backtrack exits (stderr text + exit code).
-// Parameter files: -P takes one of our table blobs (*.ccjp) or the name of a reference parameter
-// file (rna_Turner04.par, ...), resolved to the blob dumped from it (ccj_amd/params/).
-// Without -P the DirksPierce09 tables are used (the reference reads params/rna_DirksPierce09.par
-// relative to the CWD and fails elsewhere).
+// Option handling follows the gengetopt parser the reference is built with (src/ccj.ggo:1-33,
+// src/cmdline.cc:505-640, update_arg cmdline.cc:375-470): the same getopt_long table (so the
+// same prefix matching, permutation and glibc messages with argv[0]), -h / -V print and exit 0
+// as soon as they are seen, a repeated option is "`--x' (`-c') option given more than once",
+// -d goes through strtol(base 0) and rejects trailing characters with "invalid numeric value".
+// Main body follows reference CCJ.cc:58-115: sequence from the first non-option argument or the
+// first stdin line (not read at all when -i is given), toupper, T->U unless --noConv, validation
+// messages on stdout + exit 1, "Not a valid parameter file!" on stderr + exit 1 for a -P path that
+// does not exist, DNA Mathews 2004 + noGU when a 'T' survives, output "SEQ\nSTRUCT (E)\n" with
+// std::cout's default double formatting, and the reference's backtrack exits.
+// Parameter files: -P reads any ViennaRNA v2.0 .par file natively (ccj_parfile.h) on top of the
+// compiled-in defaults, printing the reference loader's warnings/errors; a *.ccjp path is taken as
+// one of our table blobs.  Without -P the reference loads params/rna_DirksPierce09.par relative
+// to the CWD: that file is read when present, otherwise the bundled DirksPierce09 tables are used
+// (the reference would print "Not a valid parameter file!" there).
+// Device: $CCJ_DEVICE (default 0) — the reference has no device option, so none is added.
 #include <getopt.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -25,6 +33,31 @@
 #include <vector>
 
 #include "ccj.h"
+#include "ccj_parfile.h"
+
+static const char kHelp[] =
+    "Usage: CCJ [options] [sequence]\n"
+    "Pseudoknotted minimum free energy folding of RNAs\n"
+    "\n"
+    "Read RNA sequence from stdin or cmdline; predict minimum\n"
+    "free energy and optimum structure\n"
+    "\n"
+    "  -h, --help               Print help and exit\n"
+    "  -V, --version            Print version and exit\n"
+    "  -i, --input-file=STRING  Give a path to an input file containing the sequence\n"
+    "                             (and input structure if known)\n"
+    "  -d, --dangles=INT        Specify the dangle model to be used (base is 2)\n"
+    "                             (default=`2')\n"
+    "  -P, --paramFile=STRING   Read energy parameters from paramfile, instead of\n"
+    "                             using the default parameter set.\n"
+    "      --noConv             Do not convert DNA into RNA. This will use the\n"
+    "                             Matthews 2004 parameters for DNA  (default=off)\n"
+    "      --noGU               Turn off G-U and U-G (and G-T and T-G) base pairing\n"
+    "                             (default=off)\n"
+    "\n"
+    "The input sequence is read from standard input, unless it is\n"
+    "given on the command line.\n"
+    "\n";
 
 static bool exists(const std::string &p) {
     struct stat b;
@@ -40,18 +73,6 @@ static std::string exe_dir() {
     return s.substr(0, s.find_last_of('/'));
 }
 
-static std::string blob_for(const std::string &arg) {
-    if (arg.size() > 5 && arg.substr(arg.size() - 5) == ".ccjp") return arg;
-    std::string base = arg.substr(arg.find_last_of('/') + 1);
-    if (base.size() > 4 && base.substr(base.size() - 4) == ".par") base = base.substr(0, base.size() - 4);
-    static const char *map[][2] = {{"rna_Turner04", "Turner04"},           {"rna_DirksPierce09", "DirksPierce09"},
-                                   {"rna_DirksPierce03", "DirksPierce03"}, {"rna_CaoChen06", "CaoChen06"},
-                                   {"rna_CaoChen09", "CaoChen09"},         {"dna_Matthews04", "Matthews04"}};
-    for (auto &m : map)
-        if (base == m[0] || base == m[1]) return exe_dir() + "/../params/" + m[1] + ".ccjp";
-    return "";
-}
-
 static bool read_blob(const std::string &path, std::vector<char> &out) {
     std::ifstream f(path, std::ios::binary);
     if (!f) return false;
@@ -59,39 +80,104 @@ static bool read_blob(const std::string &path, std::vector<char> &out) {
     return out.size() == sizeof(ccj_energy_params);
 }
 
-int main(int argc, char *argv[]) {
-    int dangles = 2, noConv = 0, noGU_flag = 0, input_given = 0, device = 0;
-    std::string param_file;
-    static option opts[] = {{"input-file", required_argument, nullptr, 'i'}, {"dangles", required_argument, nullptr, 'd'},
-                            {"paramFile", required_argument, nullptr, 'P'},  {"noConv", no_argument, nullptr, 1},
-                            {"noGU", no_argument, nullptr, 2},               {"device", required_argument, nullptr, 3},
-                            {"help", no_argument, nullptr, 'h'},             {"version", no_argument, nullptr, 'V'},
-                            {nullptr, 0, nullptr, 0}};
-    int ch;
-    while ((ch = getopt_long(argc, argv, "i:d:P:hV", opts, nullptr)) != -1) {
-        switch (ch) {
-            case 'i': input_given = 1; break;
-            case 'd': dangles = atoi(optarg); break;
-            case 'P': param_file = optarg; break;
-            case 1: noConv = 1; break;
-            case 2: noGU_flag = 1; break;
-            case 3: device = atoi(optarg); break;
-            case 'h':
-                std::cout << "Usage: CCJ [options] [sequence]\n  -i, --input-file=STRING\n  -d, --dangles=INT (default=`2')\n"
-                             "  -P, --paramFile=STRING\n      --noConv\n      --noGU\n";
-                return 0;
-            case 'V': std::cout << "CCJ 1.0 (MI355X engine)\n"; return 0;
-            default: return 1;
+static std::string bundled(const char *name) { return exe_dir() + "/../params/" + name + ".ccjp"; }
+
+// vrna_params_load on top of the compiled-in defaults; 0 ok, 1 = reference would exit(1).
+static int load_par_file(const std::string &path, std::vector<char> &blob) {
+    std::vector<char> base;
+    if (!read_blob(bundled("default"), base)) {
+        std::cerr << "CCJ: missing " << bundled("default") << std::endl;
+        return 1;
+    }
+    blob.assign(sizeof(ccj_energy_params), 0);
+    std::vector<char> log(1 << 22);
+    int rc = ccj_params_load_par(path.c_str(), reinterpret_cast<const ccj_energy_params *>(base.data()),
+                                 reinterpret_cast<ccj_energy_params *>(blob.data()), log.data(), (int)log.size());
+    std::cerr << log.data();
+    if (rc == CCJ_E_PARFILE) return 1;
+    return 0;
+}
+
+struct Args {
+    int dangles = 2;
+    bool input_given = false, noConv = false, noGU = false, paramFile_given = false;
+    std::string paramFile;
+    std::vector<std::string> inputs;
+};
+
+// gengetopt's cmdline_parser: 0 ok, 1 failure (message printed), -1 help/version printed.
+static int parse(int argc, char *argv[], Args &a) {
+    static option table[] = {{"help", no_argument, nullptr, 'h'},          {"version", no_argument, nullptr, 'V'},
+                             {"input-file", required_argument, nullptr, 'i'}, {"dangles", required_argument, nullptr, 'd'},
+                             {"paramFile", required_argument, nullptr, 'P'},  {"noConv", no_argument, nullptr, 0},
+                             {"noGU", no_argument, nullptr, 0},               {nullptr, 0, nullptr, 0}};
+    const char *prog = argv[0];
+    int given_i = 0, given_d = 0, given_P = 0, given_conv = 0, given_gu = 0;
+    auto twice = [&](int &g, const char *lng, char sht) {
+        if (g++ == 0) return false;
+        if (sht) fprintf(stderr, "%s: `--%s' (`-%c') option given more than once\n", prog, lng, sht);
+        else fprintf(stderr, "%s: `--%s' option given more than once\n", prog, lng);
+        return true;
+    };
+    opterr = 1;
+    for (;;) {
+        int idx = 0;
+        int c = getopt_long(argc, argv, "hVi:d:P:", table, &idx);
+        if (c == -1) break;
+        switch (c) {
+            case 'h': fputs(kHelp, stdout); return -1;
+            case 'V': fputs("CCJ 1.0\n", stdout); return -1;
+            case 'i':
+                if (twice(given_i, "input-file", 'i')) return 1;
+                a.input_given = true;
+                break;
+            case 'd': {
+                if (twice(given_d, "dangles", 'd')) return 1;
+                char *stop = nullptr;
+                a.dangles = (int)strtol(optarg, &stop, 0);
+                if (!(stop && *stop == '\0')) {
+                    fprintf(stderr, "%s: invalid numeric value: %s\n", prog, optarg);
+                    return 1;
+                }
+                break;
+            }
+            case 'P':
+                if (twice(given_P, "paramFile", 'P')) return 1;
+                a.paramFile_given = true;
+                a.paramFile = optarg;
+                break;
+            case 0:
+                if (!strcmp(table[idx].name, "noConv")) {
+                    if (twice(given_conv, "noConv", 0)) return 1;
+                    a.noConv = true;
+                } else {
+                    if (twice(given_gu, "noGU", 0)) return 1;
+                    a.noGU = true;
+                }
+                break;
+            default: return 1;  // getopt_long already printed the message
         }
     }
+    for (int k = optind; k < argc; ++k) a.inputs.push_back(argv[k]);
+    return 0;
+}
+
+int main(int argc, char *argv[]) {
+    Args a;
+    int pr = parse(argc, argv, a);
+    if (pr < 0) return EXIT_SUCCESS;
+    if (pr > 0) return 1;
+    const char *dev_env = getenv("CCJ_DEVICE");
+    int device = dev_env ? atoi(dev_env) : 0;
+
     std::string seq;
-    if (optind < argc) seq = argv[optind];
-    else if (!input_given) std::getline(std::cin, seq);
+    if (!a.inputs.empty()) seq = a.inputs[0];
+    else if (!a.input_given) std::getline(std::cin, seq);
     std::transform(seq.begin(), seq.end(), seq.begin(), ::toupper);
-    if (!noConv)
+    if (!a.noConv)
         for (char &c : seq)
             if (c == 'T') c = 'U';
-    int noGU = noGU_flag;
+    int noGU = a.noGU;
     if (seq.empty()) {
         std::cout << "sequence is missing" << std::endl;
         return EXIT_FAILURE;
@@ -101,25 +187,37 @@ int main(int argc, char *argv[]) {
             std::cout << "Sequence contains character " << c << " that is not G,C,A,U, or T." << std::endl;
             return EXIT_FAILURE;
         }
-    std::string blob_path;
-    if (!param_file.empty()) {
-        if (!exists(param_file)) {
+    std::vector<char> blob;
+    if (a.paramFile_given) {
+        if (!exists(a.paramFile)) {
             std::cerr << "Not a valid parameter file!" << std::endl;
             return EXIT_FAILURE;
         }
-        blob_path = blob_for(param_file);
+        size_t L = a.paramFile.size();
+        if (L > 5 && a.paramFile.compare(L - 5, 5, ".ccjp") == 0) {
+            if (!read_blob(a.paramFile, blob)) {
+                std::cerr << "Not a valid parameter file!" << std::endl;
+                return EXIT_FAILURE;
+            }
+        } else if (load_par_file(a.paramFile, blob)) {
+            return EXIT_FAILURE;
+        }
     } else if (seq.find('T') != std::string::npos) {
         noGU = 1;
-        blob_path = exe_dir() + "/../params/DNA_Mathews2004.ccjp";
+        read_blob(bundled("DNA_Mathews2004"), blob);
+        // vrna_params_load_DNA_Mathews2004 ends in check_symmetry (io.c:1126); the built-in DNA
+        // set has two asymmetric stack-enthalpy pairs, so the reference always prints this
+        for (int w = 0; w < 4; ++w) std::cerr << "WARNING: stacking enthalpies not symmetric" << std::endl;
+    } else if (exists("params/rna_DirksPierce09.par")) {
+        if (load_par_file("params/rna_DirksPierce09.par", blob)) return EXIT_FAILURE;
     } else {
-        blob_path = exe_dir() + "/../params/DirksPierce09.ccjp";
+        read_blob(bundled("DirksPierce09"), blob);
     }
-    std::vector<char> blob;
-    if (blob_path.empty() || !read_blob(blob_path, blob)) {
-        std::cerr << "Not a valid parameter file!" << std::endl;
-        return EXIT_FAILURE;
+    if (blob.size() != sizeof(ccj_energy_params)) {
+        std::cerr << "CCJ: bundled parameter tables missing next to " << exe_dir() << std::endl;
+        return 2;
     }
-    ccj_problem prob{seq.c_str(), dangles, noGU, reinterpret_cast<const ccj_energy_params *>(blob.data()), nullptr};
+    ccj_problem prob{seq.c_str(), a.dangles, noGU, reinterpret_cast<const ccj_energy_params *>(blob.data()), nullptr};
     ccj_options o{device, 0, 0, 0, 0, 0};  // fill + traceback on the GPU
     ccj_ctx *ctx = nullptr;
     int rc = ccj_create(&prob, &o, &ctx);

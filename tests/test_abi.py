@@ -15,7 +15,7 @@ LIB = os.path.join(ROOT, "ccj_amd", "lib", "libccj_hip.so")
 
 def declared_symbols():
     names = set()
-    for h in ("ccj.h",):
+    for h in ("ccj.h", "ccj_parfile.h"):
         txt = open(os.path.join(ROOT, "include", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         for m in re.finditer(r"\b(ccj_[a-z0-9_]+)\s*\(", txt):
