@@ -64,7 +64,7 @@ struct DV {
             return INF;
         }
         const int t = (j - i) + (l - k), m = n - t - 2, h = k - j - 2, a = j - i;
-        const Lvl16 L = T.ld[t];
+        const LvlDev L = T.ld[t];
         return (int)T.d4[L.lb + (long long)x * L.C + (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) + i - 1];
     }
     __device__ bool can_pair(int i, int j) const { return (j - i > TURN) && pr(i, j) > 0; }  // pseudo_loop.hh:131-135

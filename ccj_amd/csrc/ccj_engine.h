@@ -39,11 +39,22 @@ struct LevelDesc {
     int pad;
 };
 
-struct Lvl16 {      // per-level descriptor read by the level kernel (one s_load_dwordx4)
+struct LvlDev {     // per-level descriptor read by the level kernel (one s_load_dwordx8)
     long long lb;  // element offset of level t in the 4-D storage
+    long long lr;  // record offset of level t in the AoS loop records (3 record types x C)
     int C;         // cells per matrix in level t = (t+1)*M
     int M;         // cells per a-block = m(m+1)/2, m = n-t-2
+    int pad[2];
 };
+
+// AoS loop records: the operands the fused split-point loops of k_level4d read at
+// one neighbour cell, 8 int16 per 16-byte record, so each neighbour costs one dwordx4 load instead
+// of 5-7 int16 loads.  Three record types per level, each indexed like a matrix (a*M + G(h) + i-1):
+//   RA (a-loop, both sides): PLmloop00 PMmloop00 | POmloop00 PfromL | PfromO PLmloop10 | PfromMprime PK
+//   RK (b-loop, k side):     PRmloop00 PMmloop00 | PfromR min(PL,PR) | PK -          | -  -
+//   RL (b-loop, l side):     PRmloop00 PMmloop00 | POmloop00 PMmloop10 | POmloop10 PfromR | PfromO -
+// Values are the stored (clamped) int16 matrix values; unused slots hold 32767.
+enum RecType { RA = 0, RK = 1, RL = 2, NREC = 3 };
 
 struct LvlX {        // per-level bases of the interior-loop copies
     long long lbx;  // element offset of level t in d4x: PLx (C_t elements) then PRx (C_t)
@@ -75,7 +86,9 @@ struct DevTables {
     const LevelDesc *lv;           // per level t
     int16_t *d4;                   // 4-D storage base
     const long long *lb;           // element offset of level t in d4
-    const Lvl16 *ld;               // per-level descriptors
+    const LvlDev *ld;             // per-level descriptors
+    uint4 *rec;                    // AoS loop records, level t at ld[t].lr
+    long long nrec;                // records allocated (debug bounds checks)
     // interior-loop copies of PL / PR / PM, laid out so that the lanes of one k_iloop wave share
     // the loop's closing pair:
     //   PLx(t,a,h,i) = lbx + a*M + G(i-1) + h               (h fastest: fixed (i,j), lanes k)

@@ -86,8 +86,10 @@ struct ccj_ctx {
     ccj_energy_params *d_prm = nullptr;
     LevelDesc *d_lv = nullptr;
     long long *d_lb = nullptr;
-    Lvl16 *d_ld = nullptr;
+    LvlDev *d_ld = nullptr;
     int16_t *d4x = nullptr, *pmx = nullptr;  // interior-loop copies of PL/PR and PM
+    uint4 *d_rec = nullptr;                  // AoS loop records
+    long long nrec = 0;
     long long nx = 0, npm = 0;
     LvlX *d_ldx = nullptr;
     uint2 *d_il = nullptr, *d_ilm = nullptr;
@@ -1437,6 +1439,10 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     const size_t ie_elems = (size_t)IE_U * IE_U * (n + 1) * c->rs;
     if (c->total4 > 0 && hipMalloc(&c->d4, (size_t)c->total4 * sizeof(int16_t)) != hipSuccess)
         return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for 4-D matrices failed", c->total4 * 2e-9);
+    // AoS loop records: NREC 16-byte records per cell (ccj_engine.h)
+    c->nrec = c->total4 / NMAT4 * NREC;
+    if (c->nrec > 0 && hipMalloc(&c->d_rec, (size_t)c->nrec * sizeof(uint4)) != hipSuccess)
+        return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for loop records failed", c->nrec * 16e-9);
     HIPCHK(cp, hipMalloc(&c->d_ie, ie_elems * sizeof(int16_t)));
     HIPCHK(cp, hipMalloc(&c->d_est, plane * sizeof(int16_t)));
     HIPCHK(cp, hipMalloc(&c->d_hp, plane * sizeof(int)));
@@ -1450,7 +1456,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipMalloc(&c->d_prm, sizeof(ccj_energy_params)));
     HIPCHK(cp, hipMalloc(&c->d_lv, c->lv_host.size() * sizeof(LevelDesc)));
     HIPCHK(cp, hipMalloc(&c->d_lb, c->lv_off.size() * sizeof(long long)));
-    HIPCHK(cp, hipMalloc(&c->d_ld, c->lv_off.size() * sizeof(Lvl16)));
+    HIPCHK(cp, hipMalloc(&c->d_ld, c->lv_off.size() * sizeof(LvlDev)));
     {
         // interior-loop copies (ccj_engine.h): PLx+PRx mirror the level sizes, PMx is padded per (h, j)
         std::vector<LvlX> ldx(c->lv_off.size(), LvlX{0, 0});
@@ -1607,9 +1613,13 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     {
         std::vector<long long> lb(c->lv_off.begin(), c->lv_off.end());
         HIPCHK(cp, hipMemcpy(c->d_lb, lb.data(), lb.size() * sizeof(long long), hipMemcpyHostToDevice));
-        std::vector<Lvl16> ld(c->lv_off.size());
-        for (size_t t = 0; t < ld.size(); ++t) ld[t] = Lvl16{c->lv_off[t], c->lv_host[t].C, c->lv_host[t].M};
-        HIPCHK(cp, hipMemcpy(c->d_ld, ld.data(), ld.size() * sizeof(Lvl16), hipMemcpyHostToDevice));
+        std::vector<LvlDev> ld(c->lv_off.size());
+        long long lr = 0;
+        for (size_t t = 0; t < ld.size(); ++t) {
+            ld[t] = LvlDev{c->lv_off[t], lr, c->lv_host[t].C, c->lv_host[t].M, {0, 0}};
+            lr += (long long)NREC * c->lv_host[t].C;
+        }
+        HIPCHK(cp, hipMemcpy(c->d_ld, ld.data(), ld.size() * sizeof(LvlDev), hipMemcpyHostToDevice));
     }
 
     DevTables &T = c->T;
@@ -1646,6 +1656,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.lb = c->d_lb;
     T.ld = c->d_ld;
     T.d4x = c->d4x;
+    T.rec = c->d_rec;
+    T.nrec = c->nrec;
     T.pmx = c->pmx;
     T.nx = c->nx;
     T.npm = c->npm;
@@ -2209,6 +2221,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_lb);
     hipFree(c->d_ld);
     hipFree(c->d4x);
+    hipFree(c->d_rec);
     hipFree(c->pmx);
     hipFree(c->d_ldx);
     hipFree(c->d_il);

@@ -350,14 +350,14 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
         const int a1 = jo, h1 = dd - jo - 1, a2 = dd - jo - 1;
         const int g1 = (h1 * (h1 - 1)) >> 1;
         const int16_t *__restrict__ D4 = T.d4;
-        const Lvl16 *__restrict__ LD = T.ld;
+        const LvlDev *__restrict__ LD = T.ld;
         const unsigned kbase = ((unsigned)jo * (unsigned)sigma + (unsigned)dd) * (unsigned)sigma;
         int bv = INF + 1, bk = 0;
 #pragma unroll 4
         for (int ko = dd + 1; ko < sigma; ++ko) {
             const int h2 = ko - dd - 1;
             const int t1 = a1 + h2, t2 = a2 + (sigma - ko - 1);
-            const Lvl16 L1 = LD[t1], L2 = LD[t2];
+            const LvlDev L1 = LD[t1], L2 = LD[t2];
             const int o1 = PK * L1.C + a1 * L1.M + h1 * (n - t1 - 2) - g1 - 1;
             const int o2 = PK * L2.C + a2 * L2.M + h2 * (n - t2 - 2) - ((h2 * (h2 - 1)) >> 1) + jo;
             const int v = (int)(D4 + L1.lb + o1)[i] + (int)(D4 + L2.lb + o2)[i];
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
     const uint32_t it = T.items[first + w];
     const int role = (int)(it >> 30), f1 = (int)((it >> 20) & 1023u), f2 = (int)((it >> 10) & 1023u);
     const int zc = (int)(it & 1023u);
-    const Lvl16 Lt = T.ld[t];
+    const LvlDev Lt = T.ld[t];
     const int tl = t - lane;  // A-table lane L describes source level t-L (dt = L)
     const bool lvl_ok = lane >= 2 && lane <= 2 * MAXLOOP - 2 && tl >= 0;
     const long long BIAS = (long long)(n + 64) * (n + 64);  // keeps B >= 0
@@ -607,6 +607,22 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
 }
 
 // ------------------------------------------------------------------------------------------
+// AoS loop records (ccj_engine.h RecType): pack / unpack int16 pairs
+__device__ __forceinline__ unsigned pk16(int lo, int hi) { return (unsigned)(uint16_t)lo | ((unsigned)(uint16_t)hi << 16); }
+__device__ __forceinline__ int lo16(unsigned w) { return (int)(int16_t)(w & 0xffffu); }
+__device__ __forceinline__ int hi16(unsigned w) { return (int)w >> 16; }
+
+// the three records of one cell (values as stored, i.e. already clamped)
+__device__ __forceinline__ void write_records(const DevTables &T, long long lr, int C, unsigned cell, int Lm00, int Mm00,
+                                              int Om00, int fL, int fO, int Lm10, int fMp, int K, int Rm00, int fR,
+                                              int PLR, int Mm10, int Om10) {
+    uint4 *rp = T.rec + lr;
+    rp[cell] = make_uint4(pk16(Lm00, Mm00), pk16(Om00, fL), pk16(fO, Lm10), pk16(fMp, K));
+    rp[(unsigned)C + cell] = make_uint4(pk16(Rm00, Mm00), pk16(fR, PLR), pk16(K, INTERN_INF), pk16(INTERN_INF, INTERN_INF));
+    rp[2u * (unsigned)C + cell] = make_uint4(pk16(Rm00, Mm00), pk16(Om00, Mm10), pk16(Om10, fR), pk16(fO, INTERN_INF));
+}
+
+// ------------------------------------------------------------------------------------------
 // 4-D level t: one lane per cell (i,j,k,l); all lanes of a wave share (t, a) so every loop bound
 // is wave-uniform.  pseudo_loop.cc:181-644, 663-808.
 //
@@ -678,15 +694,18 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     const int *__restrict__ WB = T.WB;
     const int *__restrict__ WP = T.WP;
     const int *__restrict__ WBPr = T.WBP;
-    const Lvl16 *__restrict__ LD = T.ld;
+    const LvlDev *__restrict__ LD = T.ld;
     const int16_t *__restrict__ D4 = T.d4;
 #define LDX(lp, L, x, U, ln) ((int)(lp)[(unsigned)((x) * (L).C + (U)) + (ln)])
 #ifdef CCJ_DEBUG_BOUNDS
 #define CHK(dt, ap_, dh, di) \
     if ((dt) < 1 || (dt) > t || (ap_) < 0 || (ap_) > t - (dt) || h + (dh) >= m + (dt) || i + (di) < 1 || \
         i + (di) > m + (dt) - h - (dh)) atomicOr(T.err, 4)
+#define CHKR(idx) \
+    if ((long long)(idx) < 0 || (long long)(idx) >= T.nrec) atomicOr(T.err, 8)
 #else
 #define CHK(dt, ap_, dh, di)
+#define CHKR(idx)
 #endif
 
     // The a- and b-loops are software-pipelined: the loads of step s+split are issued before the
@@ -706,36 +725,23 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
         CHK(s, a - s, 0, s);
         CHK(s, a - s, s, 0);
 #ifdef CCJ_ABLATE_LOCAL
-        const Lvl16 L = LD[t - 1];  // timing only: every step re-reads one level (cache-resident)
+        const LvlDev L = LD[t - 1];  // timing only: every step re-reads one level (cache-resident)
         s = 1;
 #else
-        const Lvl16 L = LD[t - s];
+        const LvlDev L = LD[t - s];
 #endif
-        const int16_t *lp = D4 + L.lb;
         const int Ui = (a - s) * L.M + s;                          // X(d,j,k,l), d = i+s: lane L0 + h*s
         const int Uj = (a - s) * L.M + s * m + ((s * (s + 1)) >> 1);  // X(i,d,k,l), d = j-s: lane L0
         const unsigned lh = L0 + uh * (unsigned)s;
-#ifdef CCJ_ABLATE_WIDE
-        {   // timing only: one 16-byte load per shift (an AoS record), values meaningless
-            const uint4 wi = *(const uint4 *)((unsigned long long)(lp + (unsigned)Ui + lh * 8u) & ~15ull);
-            const uint4 wj = *(const uint4 *)((unsigned long long)(lp + (unsigned)Uj + L0 * 8u) & ~15ull);
-            v.Lm00i = (int16_t)wi.x; v.Mm00i = (int16_t)(wi.x >> 16); v.Om00i = (int16_t)wi.y; v.fLi = (int16_t)(wi.y >> 16);
-            v.fOi = (int16_t)wi.z; v.Lm00j = (int16_t)wj.x; v.Mm00j = (int16_t)(wj.x >> 16); v.Lm10j = (int16_t)wj.y;
-            v.fLj = (int16_t)(wj.y >> 16); v.fMpj = (int16_t)wj.z; v.Kj = (int16_t)(wj.z >> 16);
-        }
-#else
-        v.Lm00i = LDX(lp, L, PLmloop00, Ui, lh);
-        v.Mm00i = LDX(lp, L, PMmloop00, Ui, lh);
-        v.Om00i = LDX(lp, L, POmloop00, Ui, lh);
-        v.fLi = LDX(lp, L, PfromL, Ui, lh);
-        v.fOi = LDX(lp, L, PfromO, Ui, lh);
-        v.Lm00j = LDX(lp, L, PLmloop00, Uj, L0);
-        v.Mm00j = LDX(lp, L, PMmloop00, Uj, L0);
-        v.Lm10j = LDX(lp, L, PLmloop10, Uj, L0);
-        v.fLj = LDX(lp, L, PfromL, Uj, L0);
-        v.fMpj = LDX(lp, L, PfromMprime, Uj, L0);
-        v.Kj = LDX(lp, L, PK, Uj, L0);
-#endif
+        // one RA record per side (ccj_engine.h): x = Lm00|Mm00, y = Om00|fL, z = fO|Lm10, w = fMp|K
+        const uint4 *rp = T.rec + L.lr;
+        CHKR(L.lr + (unsigned)Ui + lh);
+        CHKR(L.lr + (unsigned)Uj + L0);
+        const uint4 wi = rp[(unsigned)Ui + lh];
+        const uint4 wj = rp[(unsigned)Uj + L0];
+        v.Lm00i = lo16(wi.x); v.Mm00i = hi16(wi.x); v.Om00i = lo16(wi.y); v.fLi = hi16(wi.y); v.fOi = lo16(wi.z);
+        v.Lm00j = lo16(wj.x); v.Mm00j = hi16(wj.x); v.fLj = hi16(wj.y); v.Lm10j = hi16(wj.z);
+        v.fMpj = lo16(wj.w); v.Kj = hi16(wj.w);
         return v;
     };
     auto step_a = [&](const AV &v, int mask) {
@@ -771,7 +777,7 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     // ---- fused b-loop: split point d inside [k, l] ----
     int pRm00 = INTERN_INF + bp, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
     int fR1 = INF, fR2 = INF, fMp = INF, fO2 = INF, pK2 = INF;
-    struct BV { int wb_k, wbp_k, wp_k, wb_l, wbp_l, wp_l, Rm00k, Mm00k, fRk, PLk, PRk, Kk, Rm00l, Mm00l, Om00l, Mm10l, Om10l, fRl, fOl; };
+    struct BV { int wb_k, wbp_k, wp_k, wb_l, wbp_l, wp_l, Rm00k, Mm00k, fRk, PLRk, Kk, Rm00l, Mm00l, Om00l, Mm10l, Om10l, fRl, fOl; };
     auto load_b = [&](int s) {
         BV v;
         const int r2 = (s - 1) * rs, ll = l - s + 1;
@@ -780,41 +786,24 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
         CHK(s, a, s, 0);
         CHK(s, a, 0, 0);
 #ifdef CCJ_ABLATE_LOCAL
-        const Lvl16 L = LD[t - 1];  // timing only: every step re-reads one level (cache-resident)
+        const LvlDev L = LD[t - 1];  // timing only: every step re-reads one level (cache-resident)
         s = 1;
 #else
-        const Lvl16 L = LD[t - s];
+        const LvlDev L = LD[t - s];
 #endif
-        const int16_t *lp = D4 + L.lb;
         const int Uk = a * L.M + s * m + ((s * (s + 1)) >> 1);  // X(i,j,d,l), d = k+s: lane L0
         const int Ul = a * L.M;                                 // X(i,j,k,d), d = l-s: lane L0 + h*s
         const unsigned lh = L0 + uh * (unsigned)s;
-#ifdef CCJ_ABLATE_WIDE
-        {
-            const uint4 k1 = *(const uint4 *)((unsigned long long)(lp + (unsigned)Uk + L0 * 8u) & ~15ull);
-            const uint4 k2 = *(const uint4 *)((unsigned long long)(lp + (unsigned)Uk + L.C + L0 * 8u) & ~15ull);
-            const uint4 l1 = *(const uint4 *)((unsigned long long)(lp + (unsigned)Ul + lh * 8u) & ~15ull);
-            const uint4 l2 = *(const uint4 *)((unsigned long long)(lp + (unsigned)Ul + L.C + lh * 8u) & ~15ull);
-            v.Rm00k = (int16_t)k1.x; v.Mm00k = (int16_t)(k1.x >> 16); v.fRk = (int16_t)k2.x; v.PLk = (int16_t)k2.y;
-            v.PRk = (int16_t)(k2.y >> 16); v.Kk = (int16_t)k1.w; v.Rm00l = (int16_t)l2.x; v.Mm00l = (int16_t)l1.x;
-            v.Om00l = (int16_t)(l1.x >> 16); v.Mm10l = (int16_t)l2.y; v.Om10l = (int16_t)(l2.y >> 16);
-            v.fRl = (int16_t)l2.z; v.fOl = (int16_t)l1.y;
-        }
-#else
-        v.Rm00k = LDX(lp, L, PRmloop00, Uk, L0);
-        v.Mm00k = LDX(lp, L, PMmloop00, Uk, L0);
-        v.fRk = LDX(lp, L, PfromR, Uk, L0);
-        v.PLk = LDX(lp, L, PL, Uk, L0);
-        v.PRk = LDX(lp, L, PR, Uk, L0);
-        v.Kk = LDX(lp, L, PK, Uk, L0);
-        v.Rm00l = LDX(lp, L, PRmloop00, Ul, lh);
-        v.Mm00l = LDX(lp, L, PMmloop00, Ul, lh);
-        v.Om00l = LDX(lp, L, POmloop00, Ul, lh);
-        v.Mm10l = LDX(lp, L, PMmloop10, Ul, lh);
-        v.Om10l = LDX(lp, L, POmloop10, Ul, lh);
-        v.fRl = LDX(lp, L, PfromR, Ul, lh);
-        v.fOl = LDX(lp, L, PfromO, Ul, lh);
-#endif
+        // RK at X(i,j,d,l): x = Rm00|Mm00, y = fR|min(PL,PR), z = K|-
+        // RL at X(i,j,k,d): x = Rm00|Mm00, y = Om00|Mm10, z = Om10|fR, w = fO|-
+        const uint4 *rp = T.rec + L.lr;
+        CHKR(L.lr + L.C + (unsigned)Uk + L0);
+        CHKR(L.lr + 2 * L.C + (unsigned)Ul + lh);
+        const uint4 wk = rp[(unsigned)(L.C + Uk) + L0];
+        const uint4 wl = rp[(unsigned)(2 * L.C + Ul) + lh];
+        v.Rm00k = lo16(wk.x); v.Mm00k = hi16(wk.x); v.fRk = lo16(wk.y); v.PLRk = hi16(wk.y); v.Kk = lo16(wk.z);
+        v.Rm00l = lo16(wl.x); v.Mm00l = hi16(wl.x); v.Om00l = lo16(wl.y); v.Mm10l = hi16(wl.y);
+        v.Om10l = lo16(wl.z); v.fRl = hi16(wl.z); v.fOl = lo16(wl.w);
         return v;
     };
     auto step_b = [&](const BV &v, int mask) {
@@ -826,7 +815,7 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
         pOm00 = imin(pOm00, v.Om00l + v.wb_l);                          // :603-606
         pOm01 = imin(pOm01, v.Om00l + v.wbp_l);                         // :618-621
         fR1 = imin(fR1, v.fRk + v.wp_k + mask);                    // PfromR(i,j,d,l) + WP(k,d-1)     :379-381
-        fMp = imin(fMp, imin(v.PLk, v.PRk) + PB + v.wp_k + mask);  // PfromM'' (:663-679) + WP(k,d-1) :412-414
+        fMp = imin(fMp, v.PLRk + PB + v.wp_k + mask);         // PfromM'' (:663-679) + WP(k,d-1) :412-414
         pK2 = imin(pK2, v.Kk + v.wp_k + mask);                     // PK(i,j,d,l) + WP(k,d-1)         :189-192
         pMm10 = imin(pMm10, v.Mm10l + v.wb_l + mask);              // PMmloop10(i,j,k,d) + WB(d+1,l)  :585-588
         pOm10 = imin(pOm10, v.Om10l + v.wb_l + mask);              // POmloop10(i,j,k,d) + WB(d+1,l)  :636-639
@@ -876,7 +865,7 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
         const int16_t *dummy = D4;
         (void)dummy;
         if (t >= 1) {
-            const Lvl16 L = LD[t - 1];
+            const LvlDev L = LD[t - 1];
             const int16_t *lp = D4 + L.lb;
             if (b >= 1) {
                 vPRm01 = imin(vPRm01, LDX(lp, L, PRmloop01, a * L.M, L0 + uh) + cp);          // (i,j,k,l-1)
@@ -890,10 +879,10 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     const int vPOm00 = pOm00, vPOm01 = pOm01, vPOm10 = pOm10;
 
     // ---- level t-2 neighbours of PL/PR/PM/PO (stack terms, get_P?mloop, PfromX)
-    const Lvl16 L2 = LD[t >= 2 ? t - 2 : 0];
+    const LvlDev L2 = LD[t >= 2 ? t - 2 : 0];
     const int16_t *lp2 = D4 + L2.lb;
     // own slots of level t: k_iloop(t) left the interior-loop minima of PL/PR/PM there
-    const Lvl16 Lt = LD[t];
+    const LvlDev Lt = LD[t];
     const int C = Lt.C;
     int16_t *dst = T.d4 + Lt.lb + (long long)a * Mt + L0;
     // ---- PL (:232-253) with get_PLiloop (:682-703, k_iloop), get_PLmloop (:705-715)
@@ -959,6 +948,7 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     }
 #undef LDX
 #undef CHK
+#undef CHKR
     // values as stored (Matrix4D::set clamp / never-set 32767), read back by same-cell terms
     const int sPL = clamp_store(vPL), sPR = clamp_store(vPR), sPM = clamp_store(vPM), sPO = clamp_store(vPO);
     const int vPfromL = imin(imin(fL1, fL2), imin(imin(sPR, sPM), sPO) + PB);   // :354-374
@@ -994,9 +984,13 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     dst[POmloop00 * C] = (int16_t)clamp_store(vPOm00);
     dst[POmloop01 * C] = (int16_t)clamp_store(vPOm01);
     dst[POmloop10 * C] = (int16_t)clamp_store(vPOm10);
-    // interior-loop copies, only where a later k_iloop can read them (its pair can pair); sharded
-    // fills write them after the level's all-gather instead (k_copies)
+    // loop records and interior-loop copies (the copies only where a later k_iloop can read them:
+    // its pair can pair); sharded fills write both after the level's all-gather (k_copies)
     if (!copies) return;
+    write_records(T, Lt.lr, C, (unsigned)(a * Mt) + L0, clamp_store(vPLm00), clamp_store(vPMm00), clamp_store(vPOm00),
+                  clamp_store(vPfromL), clamp_store(vPfromO), clamp_store(vPLm10), clamp_store(vPfromMp),
+                  clamp_store(vPK), clamp_store(vPRm00), clamp_store(vPfromR), imin(sPL, sPR), clamp_store(vPMm10),
+                  clamp_store(vPOm10));
     const LvlX X = T.ldx[t];
     if (pl_ok) T.d4x[X.lbx + (long long)a * Mt + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = (int16_t)sPL;
     if (pr_ok) {
@@ -1078,9 +1072,14 @@ __global__ __launch_bounds__(256) void k_copies(DevTables T, int t, int a_lo, in
     const int Gh = h * m - ((h * (h - 1)) >> 1);
     const int i = c - Gh + 1, b = t - a;
     const int j = i + a, k = j + h + 2, l = k + b;
-    const Lvl16 Lt = T.ld[t];
+    const LvlDev Lt = T.ld[t];
     const LvlX X = T.ldx[t];
     const int16_t *src = T.d4 + Lt.lb + (long long)a * Mt + Gh + i - 1;
+    const long long C = Lt.C;
+    write_records(T, Lt.lr, Lt.C, (unsigned)(a * Mt + Gh + i - 1), src[PLmloop00 * C], src[PMmloop00 * C],
+                  src[POmloop00 * C], src[PfromL * C], src[PfromO * C], src[PLmloop10 * C], src[PfromMprime * C],
+                  src[PK * C], src[PRmloop00 * C], src[PfromR * C], imin(src[PL * C], src[PR * C]),
+                  src[PMmloop10 * C], src[POmloop10 * C]);
     if (ptype(T, i, j) > 0) T.d4x[X.lbx + (long long)a * Mt + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = src[PL * (long long)Lt.C];
     if (ptype(T, k, l) > 0) {
         const int q = i + h - 1;
