@@ -73,7 +73,8 @@ class _Problem(ctypes.Structure):
 
 class _Options(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("overlap_d2h", ctypes.c_int), ("shard_world", ctypes.c_int),
-                ("shard_rank", ctypes.c_int), ("shard_simulate", ctypes.c_int), ("host_traceback", ctypes.c_int)]
+                ("shard_rank", ctypes.c_int), ("shard_simulate", ctypes.c_int), ("host_traceback", ctypes.c_int),
+                ("split_target", ctypes.c_int), ("share_splits", ctypes.c_int)]
 
 COMM_ID_BYTES = 128
 
@@ -222,12 +223,14 @@ class W_final:
     def __init__(self, seq: str, dangle: int = 2, params: str | bytes = "DirksPierce09",
                  noGU: bool = False, device: int = 0, overlap_d2h: bool = False, shard_world: int = 1,
                  shard_rank: int = 0, shard_simulate: bool = False, comm_id: Optional[bytes] = None,
-                 host_traceback: bool = False):
+                 host_traceback: bool = False, split_target: int = 0, share_splits: int = 0):
         """shard_world > 1: band-shard this one sequence over shard_world processes (one per GPU),
         exchanging each level over RCCL; every rank passes the same comm_id (from comm_unique_id()
         on one rank).  shard_simulate runs all shards in this process without an exchange.
         host_traceback: run W and the traceback on the host over a mirror of every matrix (the
-        reference restatement; overlap_d2h streams that mirror during the fill) instead of on the GPU."""
+        reference restatement; overlap_d2h streams that mirror during the fill) instead of on the GPU.
+        split_target / share_splits: level-kernel tuning (include/ccj.h ccj_options; 0 = default,
+        < 0 = never split a level / no split-point sharing)."""
         self.seq = seq
         self.n = len(seq)
         self.dangle = dangle
@@ -238,7 +241,7 @@ class W_final:
         prob = _Problem(ctypes.cast(self._seq_buf, ctypes.c_char_p), dangle, 1 if noGU else 0,
                         ctypes.cast(self._blob_buf, ctypes.c_void_p), None)
         opts = _Options(device, 1 if overlap_d2h else 0, shard_world, shard_rank, 1 if shard_simulate else 0,
-                        1 if host_traceback else 0)
+                        1 if host_traceback else 0, split_target, share_splits)
         h = ctypes.c_void_p()
         rc = L.ccj_create(ctypes.byref(prob), ctypes.byref(opts), ctypes.byref(h))
         if rc != CCJ_OK:

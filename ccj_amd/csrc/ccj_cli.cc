@@ -218,7 +218,7 @@ int main(int argc, char *argv[]) {
         return 2;
     }
     ccj_problem prob{seq.c_str(), a.dangles, noGU, reinterpret_cast<const ccj_energy_params *>(blob.data()), nullptr};
-    ccj_options o{device, 0, 0, 0, 0, 0};  // fill + traceback on the GPU
+    ccj_options o{device, 0, 0, 0, 0, 0, 0, 0};  // fill + traceback on the GPU
     ccj_ctx *ctx = nullptr;
     int rc = ccj_create(&prob, &o, &ctx);
     if (rc != CCJ_OK) {

@@ -56,6 +56,31 @@ struct LvlDev {     // per-level descriptor read by the level kernel (one s_load
 // Values are the stored (clamped) int16 matrix values; unused slots hold 32767.
 enum RecType { RA = 0, RK = 1, RL = 2, NREC = 3 };
 
+// Split-point sharing (k_level4d).  The cells of one gap column — same (j,k,l)
+// for the i-side split, (i,k,l) j-side, (i,j,l) k-side, (i,j,k) l-side — sit on consecutive levels
+// and read the same neighbours over the same split range, shifted by one split point per level.
+// A leader cell (a % SHARE_R == 0 for the a-loop, b % SHARE_R == 0 for the b-loop) scans its whole
+// range once and also reduces it for the next SHARE_R-1 cells of each of its columns; those
+// followers scan only the split points the leader did not see and take the rest from a partial
+// record.  Partial records live in a ring of SHARE_R level slots (the level t' cells' records are
+// written at levels t'-SHARE_R+1 .. t'-1 and read at t'), SHARE_NACC 16-byte records per cell:
+//   AI (i side): PLmloop00 PLmloop10 | PMmloop10 POmloop00 | POmloop10 PfromL | PfromO -
+//   AJ (j side): PLmloop00 PLmloop01 | PMmloop00 PLmloop10 | PfromL PfromMprime | PK -
+//   AK (k side): PRmloop00 PRmloop10 | PMmloop00 PfromR | PfromM'' PK | PfromO(l side) -
+//   AL (l side): PRmloop00 PRmloop01 | PMmloop01 POmloop00 | POmloop01 PMmloop10 | POmloop10 PfromR
+// (AK's 7th slot carries the l side's 9th field; it is written by the l-side leader, the first six
+// by the k-side leader, so the two never write the same bytes.)  Values are min-clamped at 32767
+// like a store (clamp commutes with min).  The leader's W(i-r, .) / W(., j+r) operands come from
+// two transposed copies of WB/WBP/WP (wq: row q, p contiguous; wp: row p, q contiguous), one
+// SHARE_R-wide vector load per array.
+#ifndef CCJ_SHARE_R
+#define CCJ_SHARE_R 3
+#endif
+constexpr int SHARE_R = CCJ_SHARE_R;
+constexpr int SHARE_NACC = 4;
+enum AccRec { AI = 0, AJ = 1, AK = 2, AL = 3 };
+constexpr int WQ_OFF = 4;  // wq column of p is p + WQ_OFF (p >= 1-SHARE_R+1)
+
 struct LvlX {        // per-level bases of the interior-loop copies
     long long lbx;  // element offset of level t in d4x: PLx (C_t elements) then PRx (C_t)
     long long pmb;  // element offset of level t in pmx: m_t * n * (t+1) elements
@@ -105,6 +130,15 @@ struct DevTables {
     const uint32_t *items;         // k_iloop work items (role << 30 | f1 << 20 | f2 << 10 | chunk)
     uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
     int *err;                      // device error word
+    // split-point sharing (above): levels [g_lo, g_hi) share; W copies of row stride ws, one plane
+    // of wpl ints per array (WB, WBP, WP); partial-record ring of SHARE_R slots x SHARE_NACC x accC
+    int split_target;              // k_level4d: narrow levels split loops so ~this many waves run (0: never)
+    int g_lo, g_hi;
+    int ws;
+    long long wpl;
+    int *wq, *wp;
+    uint4 *acc;
+    long long accC;
 };
 
 // element offset of cell (a,h,i) of matrix x inside level t (relative to lv[t].base)
@@ -122,6 +156,8 @@ int ccjk_build_il(const ccj::DevTables *T, void *stream);
 int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, int a_lo, int a_end, void *stream);
 int ccjk_diag2d(const ccj::DevTables *T, int sigma, void *stream);
 int ccjk_level4d(const ccj::DevTables *T, int t, int a_lo, int a_end, int copies, void *stream);
+int ccjk_level_split(int n, int t, int a_lo, int a_end, int split_target);
+int ccjk_level4d_lead(const ccj::DevTables *T, int t, void *stream);
 int ccjk_copies(const ccj::DevTables *T, int t, int a_lo, int a_end, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
 }

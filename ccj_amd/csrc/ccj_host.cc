@@ -69,6 +69,8 @@ struct ccj_ctx {
     bool overlap = true;
     int world = 1, rank = 0, simulate = 0;  // band sharding
     bool host_tb = false;                   // W + traceback on the host over the mirror (else on the GPU)
+    int split_target = 6144;                // k_level4d split heuristic (0: never split)
+    bool share = true;                      // split-point sharing
     ncclComm_t comm = nullptr;
 
     // layout
@@ -89,6 +91,8 @@ struct ccj_ctx {
     LvlDev *d_ld = nullptr;
     int16_t *d4x = nullptr, *pmx = nullptr;  // interior-loop copies of PL/PR and PM
     uint4 *d_rec = nullptr;                  // AoS loop records
+    int *d_wq = nullptr, *d_wp = nullptr;    // transposed WB/WBP/WP copies (split-point sharing)
+    uint4 *d_acc = nullptr;                  // partial-record ring (split-point sharing)
     long long nrec = 0;
     long long nx = 0, npm = 0;
     LvlX *d_ldx = nullptr;
@@ -105,6 +109,8 @@ struct ccj_ctx {
     std::vector<unsigned long long> h_pk;
     int8_t *d_vt = nullptr;
     hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr, st_il = nullptr, st_d = nullptr;
+    hipStream_t st_lead = nullptr;   // k_level4d<true>: split-point-sharing leaders of the level
+    std::vector<hipEvent_t> ld_done;
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<double> lev_ms_v, diag_ms_v, il_ms_v;
     std::vector<hipEvent_t> il_done, dg_done;  // k_iloop(t) / k_diag2d(sigma) finished
@@ -1359,6 +1365,13 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     c->rank = (opts && c->world > 1) ? opts->shard_rank : 0;
     c->simulate = (opts && c->world > 1) ? (opts->shard_simulate != 0) : 0;
     c->host_tb = opts ? (opts->host_traceback != 0) : false;
+    {
+        const char *e = getenv("CCJ_SPLIT_TARGET");
+        c->split_target = e ? atoi(e) : 6144;
+        if (opts && opts->split_target) c->split_target = opts->split_target < 0 ? 0 : opts->split_target;
+        const char *g = getenv("CCJ_SHARE_SPLITS");
+        c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
+    }
     if (c->rank < 0 || c->rank >= c->world) return CCJ_E_ARG;
     memcpy(&c->prm, prob->params, sizeof(ccj_energy_params));
     if (c->prm.magic != CCJ_PARAMS_MAGIC || c->prm.size_bytes != sizeof(ccj_energy_params))
@@ -1421,6 +1434,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_p, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_il, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_d, hipStreamNonBlocking));
+    HIPCHK(cp, hipStreamCreateWithFlags(&c->st_lead, hipStreamNonBlocking));
+    c->ld_done.resize(n + 1);
+    for (auto &e : c->ld_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->il_done.resize(n + 1);
     for (auto &e : c->il_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->dg_done.resize(n + 1);
@@ -1443,6 +1459,29 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     c->nrec = c->total4 / NMAT4 * NREC;
     if (c->nrec > 0 && hipMalloc(&c->d_rec, (size_t)c->nrec * sizeof(uint4)) != hipSuccess)
         return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for loop records failed", c->nrec * 16e-9);
+    // split-point sharing: the level range it covers (every level of it runs unsplit, so each leader
+    // and its followers run one cell per lane), the transposed W copies and the partial-record ring
+    int g_lo = 0, g_hi = 0;
+    long long accC = 0;
+    if (c->share && c->world == 1) {
+        for (int t = 0; t < c->nlev; ++t) {
+            const bool unsplit = ccjk_level_split(n, t, 0, t + 1, c->split_target) == 1;
+            if (unsplit && g_hi == 0) g_lo = t, g_hi = t + 1;
+            else if (unsplit && g_hi == t) g_hi = t + 1;
+        }
+        for (int t = g_lo; t < g_hi; ++t) accC = std::max<long long>(accC, c->lv_host[t].C);
+    }
+    const int ws = n + 8;
+    const long long wpl = (long long)(n + 2) * ws;
+    if (g_hi > g_lo) {
+        HIPCHK(cp, hipMalloc(&c->d_wq, 3 * wpl * sizeof(int)));
+        HIPCHK(cp, hipMalloc(&c->d_wp, 3 * wpl * sizeof(int)));
+        HIPCHK(cp, hipMemset(c->d_wq, 0, 3 * wpl * sizeof(int)));
+        HIPCHK(cp, hipMemset(c->d_wp, 0, 3 * wpl * sizeof(int)));
+        if (hipMalloc(&c->d_acc, (size_t)SHARE_R * SHARE_NACC * accC * sizeof(uint4)) != hipSuccess)
+            return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for split-sharing records failed",
+                           SHARE_R * SHARE_NACC * accC * 16e-9);
+    }
     HIPCHK(cp, hipMalloc(&c->d_ie, ie_elems * sizeof(int16_t)));
     HIPCHK(cp, hipMalloc(&c->d_est, plane * sizeof(int16_t)));
     HIPCHK(cp, hipMalloc(&c->d_hp, plane * sizeof(int)));
@@ -1669,6 +1708,15 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.ilseg = c->d_ilseg;
     T.ilmseg = c->d_ilmseg;
     T.err = c->d_err;
+    T.split_target = c->split_target;
+    T.g_lo = g_lo;
+    T.g_hi = g_hi;
+    T.ws = ws;
+    T.wpl = wpl;
+    T.wq = c->d_wq;
+    T.wp = c->d_wp;
+    T.acc = c->d_acc;
+    T.accC = accC;
     *out = c.release();
     return CCJ_OK;
 }
@@ -1743,6 +1791,17 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
                 int lo = 0, hi = 0;
                 ccj_shard_range(n, s, G, r, &lo, &hi);
                 HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, lo, hi, G == 1 ? 1 : 0, st));
+            }
+            if (s >= c->T.g_lo && s < c->T.g_hi) {
+                // leaders on their own stream, same inputs as the level kernel (level s-1 complete,
+                // k_iloop(s), k_diag2d(s-1)); the level is done when both launches are
+                HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->il_done[s], 0));
+                if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->dg_done[s - 1], 0));
+                if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->lev_done[s - 1], 0));
+                else HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->ev_pre, 0));
+                HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, c->st_lead));
+                HIPCHK(c, hipEventRecord(c->ld_done[s], c->st_lead));
+                HIPCHK(c, hipStreamWaitEvent(st, c->ld_done[s], 0));
             }
             if (G > 1) {
                 if (!c->simulate) {
@@ -2205,6 +2264,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->st_p) hipStreamSynchronize(c->st_p);
     if (c->st_il) hipStreamSynchronize(c->st_il);
     if (c->st_d) hipStreamSynchronize(c->st_d);
+    if (c->st_lead) hipStreamSynchronize(c->st_lead);
     hipFree(c->d4);
     hipFree(c->d_ie);
     hipFree(c->d_est);
@@ -2222,6 +2282,9 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_ld);
     hipFree(c->d4x);
     hipFree(c->d_rec);
+    hipFree(c->d_wq);
+    hipFree(c->d_wp);
+    hipFree(c->d_acc);
     hipFree(c->pmx);
     hipFree(c->d_ldx);
     hipFree(c->d_il);
@@ -2244,6 +2307,8 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->st_il) hipStreamDestroy(c->st_il);
     if (c->st_d) hipStreamDestroy(c->st_d);
+    if (c->st_lead) hipStreamDestroy(c->st_lead);
+    for (auto e : c->ld_done) hipEventDestroy(e);
     for (auto e : c->il_done) hipEventDestroy(e);
     for (auto e : c->dg_done) hipEventDestroy(e);
     for (auto e : c->tev) hipEventDestroy(e);

@@ -289,6 +289,12 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
             int wpp = INF + 1;
             if (m < INF / 2) { wpp = m; T.WPP[cell] = m; }
             T.WP[cell] = imin(pe.PUP * (sigma + 1), wpp);
+            if (T.wq) {  // transposed copies for the split-point-sharing leaders of k_level4d
+                const long long q0 = (long long)l * T.ws + i + WQ_OFF, p0 = (long long)i * T.ws + l;
+                const int wb = imin(pe.cp * (sigma + 1), wbp), wp = imin(pe.PUP * (sigma + 1), wpp);
+                T.wq[q0] = wb; T.wq[T.wpl + q0] = wbp; T.wq[2 * T.wpl + q0] = wp;
+                T.wp[p0] = wb; T.wp[T.wpl + p0] = wbp; T.wp[2 * T.wpl + p0] = wp;
+            }
         }
     }
 
@@ -612,6 +618,24 @@ __device__ __forceinline__ unsigned pk16(int lo, int hi) { return (unsigned)(uin
 __device__ __forceinline__ int lo16(unsigned w) { return (int)(int16_t)(w & 0xffffu); }
 __device__ __forceinline__ int hi16(unsigned w) { return (int)w >> 16; }
 
+// ints per lane a leader's split wave hands to part 0: the follower slices of one side
+constexpr int LEAD_RED = 15 * (SHARE_R - 1);
+
+// split-point sharing (ccj_engine.h): SHARE_R consecutive W values of one transposed-copy row
+typedef int wv_t __attribute__((ext_vector_type(SHARE_R)));
+__device__ __forceinline__ wv_t ldw(const int *p) {
+    wv_t v;
+    __builtin_memcpy(&v, p, sizeof(v));  // 4-byte aligned: one dwordx4 (R = 4) in unaligned-access mode
+    return v;
+}
+// partial record: up to 7 int16 fields (min-clamped like a store), slot 7 = 32767
+__device__ __forceinline__ uint4 pack_acc(const int *f, int nf) {
+    int c[8];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) c[x] = x < nf ? clamp_store(f[x]) : INTERN_INF;
+    return make_uint4(pk16(c[0], c[1]), pk16(c[2], c[3]), pk16(c[4], c[5]), pk16(c[6], c[7]));
+}
+
 // the three records of one cell (values as stored, i.e. already clamped)
 __device__ __forceinline__ void write_records(const DevTables &T, long long lr, int C, unsigned cell, int Lm00, int Mm00,
                                               int Om00, int fL, int fO, int Lm10, int fMp, int K, int Rm00, int fR,
@@ -638,6 +662,7 @@ __device__ __forceinline__ void write_records(const DevTables &T, long long lr, 
 // recurrence that reads it (11a + 13b loads per cell instead of 14a + 16b).  The interior-loop
 // windows are walked by source level dt (outer) so the level descriptor is loaded once per dt.
 // ------------------------------------------------------------------------------------------
+template <bool LEAD>
 __global__ __launch_bounds__(512)
 #ifdef CCJ_WAVES_EU
 __attribute__((amdgpu_waves_per_eu(CCJ_WAVES_EU, CCJ_WAVES_EU)))
@@ -703,15 +728,36 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
         i + (di) > m + (dt) - h - (dh)) atomicOr(T.err, 4)
 #define CHKR(idx) \
     if ((long long)(idx) < 0 || (long long)(idx) >= T.nrec) atomicOr(T.err, 8)
+#define CHKA(idx) \
+    if (!T.acc || (long long)(idx) >= T.accC) atomicOr(T.err, 256)
 #else
 #define CHK(dt, ap_, dh, di)
 #define CHKR(idx)
+#define CHKA(idx)
 #endif
 
     // The a- and b-loops are software-pipelined: the loads of step s+split are issued before the
     // values of step s are consumed, so every wave keeps two steps of loads in flight.  The terms
     // with d strictly inside the gap (s < a, s < b) are masked on the last step by adding INF;
     // their loads still hit valid cells.
+    // ---- split-point sharing roles (ccj_engine.h), wave-uniform: 0 = own full scan, 1 = leader
+    // (full scan, also for the next SHARE_R-1 cells of its columns), 2 = follower (scans only the
+    // split points 1..a%R / 1..b%R, takes the rest from its leader's partial record).  A leader's
+    // W(i-r, .) / W(., j+r) operands have spans up to a+r-1 <= t-1 only if b >= r (a-side) / a >= r
+    // (b-side), so columns with a short other gap keep full scans.
+    const bool grp = t >= T.g_lo && t < T.g_hi;
+    const int ra = a % SHARE_R, rb = b % SHARE_R;
+    const int arole = (grp && b >= SHARE_R - 1) ? (ra == 0 ? 1 : (t - ra >= T.g_lo ? 2 : 0)) : 0;
+    const int brole = (grp && a >= SHARE_R - 1) ? (rb == 0 ? 1 : (t - rb >= T.g_lo ? 2 : 0)) : 0;
+    // On sharing levels every wave with a long scan (a leader, or a full scan on either side) runs
+    // in its own launch (k_level4d<true>: more registers, scans split over several waves, side
+    // stream); the plain kernel keeps the cells that only follow (short scans, full occupancy).
+    if (grp && LEAD != (arole != 2 || brole != 2)) return;
+    const int a_stop = arole == 2 ? ra : a;  // last split step this cell scans itself
+    const int b_stop = brole == 2 ? rb : b;
+    const int ws = T.ws;
+    const long long wpl = T.wpl;
+
     // ---- fused a-loop: split point d inside [i, j] ----
     int pLm00 = INTERN_INF + bp, pLm01 = INF, pLm10 = INF, pMm00 = INTERN_INF + bp, pMm10 = INF;
     int pOm00 = INTERN_INF + bp, pOm10 = INF;
@@ -759,20 +805,171 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
         fM = imin(fM, v.fMpj + v.wp_j + mask);          // PfromMprime(i,d,k,l) + WP(d+1,j) :399-401
         pK1 = imin(pK1, v.Kj + v.wp_j + mask);          // PK(i,d,k,l) + WP(d+1,j)          :184-187
     };
+    // a-leader: one scan of s = 1..a for this cell (r = 0) and its followers r = 1..R-1:
+    //   i side: cell (i-r, j, k, l) (level t+r, block a+r, row h), term X(i+s,j,k,l) + W(i-r, i+s-1)
+    //   j side: cell (i, j+r, k, l) (level t+r, block a+r, row h-r), term X(i,j-s,k,l) + W(j-s+1, j+r)
+    // Both followers mask the same last split point (d = j / d = i) as the leader.
+    auto lead_a = [&]() {
+        int AI_[SHARE_R][7], AJ_[SHARE_R][7];
+#pragma unroll
+        for (int r = 0; r < SHARE_R; ++r)
+#pragma unroll
+            for (int f = 0; f < 7; ++f) AI_[r][f] = AJ_[r][f] = INF;
+        struct LA { uint4 wi, wj; wv_t qb, qbp, qp, pb, pbp, pp; };
+        auto ld = [&](int s) {
+            LA v;
+            const LvlDev L = LD[t - s];
+            const int Ui = (a - s) * L.M + s;
+            const int Uj = (a - s) * L.M + s * m + ((s * (s + 1)) >> 1);
+            const unsigned lh = L0 + uh * (unsigned)s;
+            const uint4 *rp = T.rec + L.lr;
+            CHKR(L.lr + (unsigned)Ui + lh);
+            CHKR(L.lr + (unsigned)Uj + L0);
+            v.wi = rp[(unsigned)Ui + lh];
+            v.wj = rp[(unsigned)Uj + L0];
+#ifdef CCJ_SHARE_WVEC
+            const int *q = T.wq + (i + s - 1) * ws + (i - SHARE_R + 1 + WQ_OFF);  // W(i-r, i+s-1), r = R-1..0
+            const int *p = T.wp + (j - s + 1) * ws + j;                          // W(j-s+1, j+r), r = 0..R-1
+            v.qb = ldw(q); v.qbp = ldw(q + wpl); v.qp = ldw(q + 2 * wpl);
+            v.pb = ldw(p); v.pbp = ldw(p + wpl); v.pp = ldw(p + 2 * wpl);
+#else
+            // span-major rows: W(i-r, i+s-1) and W(j-s+1, j+r) have span s-1+r, coalesced along the lanes
+#pragma unroll
+            for (int r = 0; r < SHARE_R; ++r) {
+                const int o = (s - 1 + r) * rs;
+                v.qb[SHARE_R - 1 - r] = WB[o + i - r]; v.qbp[SHARE_R - 1 - r] = WBPr[o + i - r]; v.qp[SHARE_R - 1 - r] = WP[o + i - r];
+                v.pb[r] = WB[o + j - s + 1]; v.pbp[r] = WBPr[o + j - s + 1]; v.pp[r] = WP[o + j - s + 1];
+            }
+#endif
+            return v;
+        };
+        auto st = [&](const LA &v, int mask) {
+            const int Lm00i = lo16(v.wi.x), Mm00i = hi16(v.wi.x), Om00i = lo16(v.wi.y), fLi = hi16(v.wi.y);
+            const int fOi = lo16(v.wi.z);
+            const int Lm00j = lo16(v.wj.x), Mm00j = hi16(v.wj.x), fLj = hi16(v.wj.y), Lm10j = hi16(v.wj.z);
+            const int fMpj = lo16(v.wj.w), Kj = hi16(v.wj.w);
+#pragma unroll
+            for (int r = 0; r < SHARE_R; ++r) {
+                const int wbi = v.qb[SHARE_R - 1 - r], wbpi = v.qbp[SHARE_R - 1 - r], wpi = v.qp[SHARE_R - 1 - r];
+                const int wbj = v.pb[r], wbpj = v.pbp[r], wpj = v.pp[r];
+                int *I = AI_[r], *J = AJ_[r];
+                I[0] = imin(I[0], wbi + Lm00i);          // PLmloop00 :449-458
+                I[1] = imin(I[1], wbpi + Lm00i);         // PLmloop10 :481-483
+                I[2] = imin(I[2], wbpi + Mm00i);         // PMmloop10 :581-584
+                I[3] = imin(I[3], wbi + Om00i);          // POmloop00 :599-602
+                I[4] = imin(I[4], wbpi + Om00i);         // POmloop10 :632-635
+                I[5] = imin(I[5], fLi + wpi + mask);     // PfromL    :357-359
+                I[6] = imin(I[6], fOi + wpi + mask);     // PfromO    :425-427
+                J[0] = imin(J[0], Lm00j + wbj);          // PLmloop00
+                J[1] = imin(J[1], Lm00j + wbpj);         // PLmloop01 :468-471
+                J[2] = imin(J[2], Mm00j + wbj);          // PMmloop00 :548-551
+                J[3] = imin(J[3], Lm10j + wbj + mask);   // PLmloop10 :484-486
+                J[4] = imin(J[4], fLj + wpj + mask);     // PfromL    :360-361
+                J[5] = imin(J[5], fMpj + wpj + mask);    // PfromM    :399-401
+                J[6] = imin(J[6], Kj + wpj + mask);      // PK        :184-187
+            }
+        };
+        if (1 + part <= a) {
+            int s = 1 + part;
+            LA cur = ld(s);
+            for (;;) {
+                const int sn = s + split;
+                const LA nxt = ld(imin(sn, a));
+                st(cur, s < a ? 0 : INF);
+                if (sn > a) break;
+                cur = nxt;
+                s = sn;
+            }
+        }
+        if (split > 1) {  // the followers' slices (r >= 1) of the split waves meet in part 0
+            int *slot = red + (wib / split) * (split - 1) * LEAD_RED * 64 + lane;
+            if (part > 0) {
+#pragma unroll
+                for (int r = 1; r < SHARE_R; ++r)
+#pragma unroll
+                    for (int f = 0; f < 7; ++f) {
+                        slot[((part - 1) * LEAD_RED + (r - 1) * 14 + f) * 64] = AI_[r][f];
+                        slot[((part - 1) * LEAD_RED + (r - 1) * 14 + 7 + f) * 64] = AJ_[r][f];
+                    }
+            }
+            __syncthreads();
+            if (part == 0)
+                for (int p = 1; p < split; ++p)
+#pragma unroll
+                    for (int r = 1; r < SHARE_R; ++r)
+#pragma unroll
+                        for (int f = 0; f < 7; ++f) {
+                            AI_[r][f] = imin(AI_[r][f], slot[((p - 1) * LEAD_RED + (r - 1) * 14 + f) * 64]);
+                            AJ_[r][f] = imin(AJ_[r][f], slot[((p - 1) * LEAD_RED + (r - 1) * 14 + 7 + f) * 64]);
+                        }
+            __syncthreads();
+        }
+        pLm00 = imin(pLm00, imin(AI_[0][0], AJ_[0][0]));
+        pLm10 = imin(AI_[0][1], AJ_[0][3]);
+        pMm10 = AI_[0][2];
+        pOm00 = imin(pOm00, AI_[0][3]);
+        pOm10 = AI_[0][4];
+        fL1 = AI_[0][5];
+        fO1 = AI_[0][6];
+        pLm01 = AJ_[0][1];
+        pMm00 = imin(pMm00, AJ_[0][2]);
+        fL2 = AJ_[0][4];
+        fM = AJ_[0][5];
+        pK1 = AJ_[0][6];
+        if (!lane_ok || part != 0) return;
+#pragma unroll
+        for (int r = 1; r < SHARE_R; ++r) {
+            const int tf = t + r;
+            if (tf >= T.g_hi) break;
+            const int Mf = LD[tf].M, mf = m - r;
+            uint4 *ring = T.acc + (long long)((tf % SHARE_R) * SHARE_NACC) * T.accC;
+            if (i - r >= 1) {
+                const unsigned idx = (unsigned)((a + r) * Mf) + L0 - (unsigned)(r * (h + 1));
+                CHKA(idx);
+                ring[(long long)AI * T.accC + idx] = pack_acc(AI_[r], 7);
+            }
+            if (h - r >= 0) {
+                const int hh = h - r;
+                const unsigned idx = (unsigned)((a + r) * Mf + hh * mf - ((hh * (hh - 1)) >> 1) + i - 1);
+                CHKA(idx);
+                ring[(long long)AJ * T.accC + idx] = pack_acc(AJ_[r], 7);
+            }
+        }
+    };
 #ifdef CCJ_ABLATE_LINEAR
     if (a < 0)
 #endif
-    if (1 + part <= a) {
+    if (arole == 1) {
+        if constexpr (LEAD) lead_a();
+    } else if (1 + part <= a_stop) {
         int s = 1 + part;
         AV cur = load_a(s);
         for (;;) {
             const int sn = s + split;
-            const AV nxt = load_a(imin(sn, a));  // the last one re-reads step a (discarded)
+            const AV nxt = load_a(imin(sn, a_stop));  // the last one re-reads step a_stop (discarded)
             step_a(cur, s < a ? 0 : INF);
-            if (sn > a) break;
+            if (sn > a_stop) break;
             cur = nxt;
             s = sn;
         }
+    }
+    if (arole == 2) {  // follower: the leader's partial (split points a%R+1 .. a)
+        const uint4 *ring = T.acc + (long long)((t % SHARE_R) * SHARE_NACC) * T.accC;
+        const unsigned idx = (unsigned)(a * Mt) + L0;
+        CHKA(idx);
+        const uint4 pi = ring[(long long)AI * T.accC + idx], pj = ring[(long long)AJ * T.accC + idx];
+        pLm00 = imin(pLm00, imin(lo16(pi.x), lo16(pj.x)));
+        pLm10 = imin(pLm10, imin(hi16(pi.x), hi16(pj.y)));
+        pMm10 = imin(pMm10, lo16(pi.y));
+        pOm00 = imin(pOm00, hi16(pi.y));
+        pOm10 = imin(pOm10, lo16(pi.z));
+        fL1 = imin(fL1, hi16(pi.z));
+        fO1 = imin(fO1, lo16(pi.w));
+        pLm01 = imin(pLm01, hi16(pj.x));
+        pMm00 = imin(pMm00, lo16(pj.y));
+        fL2 = imin(fL2, lo16(pj.z));
+        fM = imin(fM, hi16(pj.z));
+        pK1 = imin(pK1, lo16(pj.w));
     }
     // ---- fused b-loop: split point d inside [k, l] ----
     int pRm00 = INTERN_INF + bp, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
@@ -822,20 +1019,181 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
         fR2 = imin(fR2, v.fRl + v.wp_l + mask);                    // PfromR(i,j,k,d) + WP(d+1,l)     :382-383
         fO2 = imin(fO2, v.fOl + v.wp_l + mask);                    // PfromO(i,j,k,d) + WP(d+1,l)     :429-431
     };
+    // b-leader: one scan of s = 1..b for this cell and its followers r = 1..R-1:
+    //   k side: cell (i, j, k-r, l) (level t+r, block a, row h-r), term X(i,j,k+s,l) + W(k-r, k+s-1)
+    //   l side: cell (i, j, k, l+r) (level t+r, block a, row h),   term X(i,j,k,l-s) + W(l-s+1, l+r)
+    auto lead_b = [&]() {
+        int AK_[SHARE_R][6], AL_[SHARE_R][9];
+#pragma unroll
+        for (int r = 0; r < SHARE_R; ++r) {
+#pragma unroll
+            for (int f = 0; f < 6; ++f) AK_[r][f] = INF;
+#pragma unroll
+            for (int f = 0; f < 9; ++f) AL_[r][f] = INF;
+        }
+        struct LB { uint4 wk, wl; wv_t qb, qbp, qp, pb, pbp, pp; };
+        auto ld = [&](int s) {
+            LB v;
+            const LvlDev L = LD[t - s];
+            const int Uk = a * L.M + s * m + ((s * (s + 1)) >> 1);
+            const int Ul = a * L.M;
+            const unsigned lh = L0 + uh * (unsigned)s;
+            const uint4 *rp = T.rec + L.lr;
+            CHKR(L.lr + L.C + (unsigned)Uk + L0);
+            CHKR(L.lr + 2 * L.C + (unsigned)Ul + lh);
+            v.wk = rp[(unsigned)(L.C + Uk) + L0];
+            v.wl = rp[(unsigned)(2 * L.C + Ul) + lh];
+#ifdef CCJ_SHARE_WVEC
+            const int *q = T.wq + (k + s - 1) * ws + (k - SHARE_R + 1 + WQ_OFF);  // W(k-r, k+s-1), r = R-1..0
+            const int *p = T.wp + (l - s + 1) * ws + l;                          // W(l-s+1, l+r), r = 0..R-1
+            v.qb = ldw(q); v.qbp = ldw(q + wpl); v.qp = ldw(q + 2 * wpl);
+            v.pb = ldw(p); v.pbp = ldw(p + wpl); v.pp = ldw(p + 2 * wpl);
+#else
+#pragma unroll
+            for (int r = 0; r < SHARE_R; ++r) {
+                const int o = (s - 1 + r) * rs;
+                v.qb[SHARE_R - 1 - r] = WB[o + k - r]; v.qbp[SHARE_R - 1 - r] = WBPr[o + k - r]; v.qp[SHARE_R - 1 - r] = WP[o + k - r];
+                v.pb[r] = WB[o + l - s + 1]; v.pbp[r] = WBPr[o + l - s + 1]; v.pp[r] = WP[o + l - s + 1];
+            }
+#endif
+            return v;
+        };
+        auto st = [&](const LB &v, int mask) {
+            const int Rm00k = lo16(v.wk.x), Mm00k = hi16(v.wk.x), fRk = lo16(v.wk.y), PLRk = hi16(v.wk.y);
+            const int Kk = lo16(v.wk.z);
+            const int Rm00l = lo16(v.wl.x), Mm00l = hi16(v.wl.x), Om00l = lo16(v.wl.y), Mm10l = hi16(v.wl.y);
+            const int Om10l = lo16(v.wl.z), fRl = hi16(v.wl.z), fOl = lo16(v.wl.w);
+#pragma unroll
+            for (int r = 0; r < SHARE_R; ++r) {
+                const int wbk = v.qb[SHARE_R - 1 - r], wbpk = v.qbp[SHARE_R - 1 - r], wpk = v.qp[SHARE_R - 1 - r];
+                const int wbl = v.pb[r], wbpl = v.pbp[r], wpl_ = v.pp[r];
+                int *K = AK_[r], *Q = AL_[r];
+                K[0] = imin(K[0], wbk + Rm00k);             // PRmloop00 :499-508
+                K[1] = imin(K[1], wbpk + Rm00k);            // PRmloop10 :534-537
+                K[2] = imin(K[2], Mm00k + wbk);             // PMmloop00 :552-555
+                K[3] = imin(K[3], fRk + wpk + mask);        // PfromR    :379-381
+                K[4] = imin(K[4], PLRk + PB + wpk + mask);  // PfromMprime :412-414
+                K[5] = imin(K[5], Kk + wpk + mask);         // PK        :189-192
+                Q[0] = imin(Q[0], Rm00l + wbl);             // PRmloop00
+                Q[1] = imin(Q[1], Rm00l + wbpl);            // PRmloop01 :520-523
+                Q[2] = imin(Q[2], Mm00l + wbpl);            // PMmloop01 :567-570
+                Q[3] = imin(Q[3], Om00l + wbl);             // POmloop00 :603-606
+                Q[4] = imin(Q[4], Om00l + wbpl);            // POmloop01 :618-621
+                Q[5] = imin(Q[5], Mm10l + wbl + mask);      // PMmloop10 :585-588
+                Q[6] = imin(Q[6], Om10l + wbl + mask);      // POmloop10 :636-639
+                Q[7] = imin(Q[7], fRl + wpl_ + mask);       // PfromR    :382-383
+                Q[8] = imin(Q[8], fOl + wpl_ + mask);       // PfromO    :429-431
+            }
+        };
+        if (1 + part <= b) {
+            int s = 1 + part;
+            LB cur = ld(s);
+            for (;;) {
+                const int sn = s + split;
+                const LB nxt = ld(imin(sn, b));
+                st(cur, s < b ? 0 : INF);
+                if (sn > b) break;
+                cur = nxt;
+                s = sn;
+            }
+        }
+        if (split > 1) {
+            int *slot = red + (wib / split) * (split - 1) * LEAD_RED * 64 + lane;
+            if (part > 0) {
+#pragma unroll
+                for (int r = 1; r < SHARE_R; ++r) {
+#pragma unroll
+                    for (int f = 0; f < 6; ++f) slot[((part - 1) * LEAD_RED + (r - 1) * 15 + f) * 64] = AK_[r][f];
+#pragma unroll
+                    for (int f = 0; f < 9; ++f) slot[((part - 1) * LEAD_RED + (r - 1) * 15 + 6 + f) * 64] = AL_[r][f];
+                }
+            }
+            __syncthreads();
+            if (part == 0)
+                for (int p = 1; p < split; ++p)
+#pragma unroll
+                    for (int r = 1; r < SHARE_R; ++r) {
+#pragma unroll
+                        for (int f = 0; f < 6; ++f)
+                            AK_[r][f] = imin(AK_[r][f], slot[((p - 1) * LEAD_RED + (r - 1) * 15 + f) * 64]);
+#pragma unroll
+                        for (int f = 0; f < 9; ++f)
+                            AL_[r][f] = imin(AL_[r][f], slot[((p - 1) * LEAD_RED + (r - 1) * 15 + 6 + f) * 64]);
+                    }
+            __syncthreads();
+        }
+        pRm00 = imin(pRm00, imin(AK_[0][0], AL_[0][0]));
+        pRm10 = AK_[0][1];
+        pMm00 = imin(pMm00, AK_[0][2]);
+        fR1 = AK_[0][3];
+        fMp = AK_[0][4];
+        pK2 = AK_[0][5];
+        pRm01 = AL_[0][1];
+        pMm01 = AL_[0][2];
+        pOm00 = imin(pOm00, AL_[0][3]);
+        pOm01 = AL_[0][4];
+        pMm10 = imin(pMm10, AL_[0][5]);
+        pOm10 = imin(pOm10, AL_[0][6]);
+        fR2 = AL_[0][7];
+        fO2 = AL_[0][8];
+        if (!lane_ok || part != 0) return;
+#pragma unroll
+        for (int r = 1; r < SHARE_R; ++r) {
+            const int tf = t + r;
+            if (tf >= T.g_hi) break;
+            const int Mf = LD[tf].M, mf = m - r;
+            uint4 *ring = T.acc + (long long)((tf % SHARE_R) * SHARE_NACC) * T.accC;
+            if (h - r >= 0) {  // k side: AK slots 0..5 (12 bytes; slot 6 belongs to the l-side leader)
+                const int hh = h - r;
+                const unsigned idx = (unsigned)(a * Mf + hh * mf - ((hh * (hh - 1)) >> 1) + i - 1);
+                CHKA(idx);
+                const uint4 v = pack_acc(AK_[r], 6);
+                *(uint3 *)(ring + (long long)AK * T.accC + idx) = make_uint3(v.x, v.y, v.z);
+            }
+            if (i <= m - h - r) {  // l side: AL, and its 9th field into AK slot 6 of the same cell
+                const unsigned idx = (unsigned)(a * Mf) + L0 - (unsigned)(h * r);
+                CHKA(idx);
+                ring[(long long)AL * T.accC + idx] = pack_acc(AL_[r], 8);
+                ((int16_t *)(ring + (long long)AK * T.accC + idx))[6] = (int16_t)clamp_store(AL_[r][8]);
+            }
+        }
+    };
 #ifdef CCJ_ABLATE_LINEAR
     if (b < 0)
 #endif
-    if (1 + part <= b) {
+    if (brole == 1) {
+        if constexpr (LEAD) lead_b();
+    } else if (1 + part <= b_stop) {
         int s = 1 + part;
         BV cur = load_b(s);
         for (;;) {
             const int sn = s + split;
-            const BV nxt = load_b(imin(sn, b));
+            const BV nxt = load_b(imin(sn, b_stop));
             step_b(cur, s < b ? 0 : INF);
-            if (sn > b) break;
+            if (sn > b_stop) break;
             cur = nxt;
             s = sn;
         }
+    }
+    if (brole == 2) {  // follower: the leaders' partials (split points b%R+1 .. b)
+        const uint4 *ring = T.acc + (long long)((t % SHARE_R) * SHARE_NACC) * T.accC;
+        const unsigned idx = (unsigned)(a * Mt) + L0;
+        CHKA(idx);
+        const uint4 pk = ring[(long long)AK * T.accC + idx], pl = ring[(long long)AL * T.accC + idx];
+        pRm00 = imin(pRm00, imin(lo16(pk.x), lo16(pl.x)));
+        pRm10 = imin(pRm10, hi16(pk.x));
+        pMm00 = imin(pMm00, lo16(pk.y));
+        fR1 = imin(fR1, hi16(pk.y));
+        fMp = imin(fMp, lo16(pk.z));
+        pK2 = imin(pK2, hi16(pk.z));
+        fO2 = imin(fO2, lo16(pk.w));
+        pRm01 = imin(pRm01, hi16(pl.x));
+        pMm01 = imin(pMm01, lo16(pl.y));
+        pOm00 = imin(pOm00, hi16(pl.y));
+        pOm01 = imin(pOm01, lo16(pl.z));
+        pMm10 = imin(pMm10, hi16(pl.z));
+        pOm10 = imin(pOm10, lo16(pl.w));
+        fR2 = imin(fR2, hi16(pl.w));
     }
     if (split > 1) {
         // min-reduce the split waves' partial a/b-loop results; part 0 finishes the cell
@@ -949,6 +1307,7 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
 #undef LDX
 #undef CHK
 #undef CHKR
+#undef CHKA
     // values as stored (Matrix4D::set clamp / never-set 32767), read back by same-cell terms
     const int sPL = clamp_store(vPL), sPR = clamp_store(vPR), sPM = clamp_store(vPM), sPO = clamp_store(vPO);
     const int vPfromL = imin(imin(fL1, fL2), imin(imin(sPR, sPM), sPO) + PB);   // :354-374
@@ -1096,6 +1455,16 @@ extern "C" int ccjk_copies(const DevTables *T, int t, int a_lo, int a_end, void 
     return (int)hipGetLastError();
 }
 
+// narrow levels: split each chunk's a/b loops over up to 8 waves so ~split_target waves run at once
+extern "C" int ccjk_level_split(int n, int t, int a_lo, int a_end, int split_target) {
+    const int m = n - t - 2;
+    if (m <= 0 || a_end <= a_lo) return 1;
+    const long waves = (long)(a_end - a_lo) * ((m * (m + 1) / 2 + 63) / 64);
+    int split = 1;
+    while (split_target > 0 && split < 8 && waves * split * 2 <= split_target) split *= 2;
+    return split;
+}
+
 extern "C" int ccjk_level4d(const DevTables *T, int t, int a_lo, int a_end, int copies, void *stream) {
     const int m = T->n - t - 2;
     if (m <= 0) return 0;
@@ -1103,17 +1472,33 @@ extern "C" int ccjk_level4d(const DevTables *T, int t, int a_lo, int a_end, int 
     const int wavesPerA = (Mt + 63) / 64;
     if (a_end <= a_lo) return 0;
     const long waves = (long)(a_end - a_lo) * wavesPerA;
-    // narrow levels: split each chunk's a/b loops over up to 8 waves so ~target waves run at once
-    static const long target = [] {
-        const char *e = getenv("CCJ_SPLIT_TARGET");
-        return e ? atol(e) : 6144L;
-    }();
-    int split = 1;
-    while (split < 8 && waves * split * 2 <= target) split *= 2;
+    const int split = ccjk_level_split(T->n, t, a_lo, a_end, T->split_target);
+    // split-point sharing needs one cell per lane on every level of its range
+    if (split > 1 && t >= T->g_lo && t < T->g_hi) return (int)hipErrorInvalidValue;
     const int threads = split <= 4 ? 256 : 64 * split;
     const int cpb = threads / 64 / split;
     const long blocks = (waves + cpb - 1) / cpb;
     const size_t shmem = split > 1 ? (size_t)cpb * (split - 1) * 22 * 64 * sizeof(int) : 0;
-    hipLaunchKernelGGL(k_level4d, dim3((unsigned)blocks), dim3(threads), shmem, (hipStream_t)stream, *T, t, wavesPerA, split, a_lo, a_end, copies);
+    hipLaunchKernelGGL(k_level4d<false>, dim3((unsigned)blocks), dim3(threads), shmem, (hipStream_t)stream, *T, t, wavesPerA, split, a_lo, a_end, copies);
+    return (int)hipGetLastError();
+}
+
+// the split-point-sharing leader waves of level t (no-op outside the sharing range)
+extern "C" int ccjk_level4d_lead(const DevTables *T, int t, void *stream) {
+    if (t < T->g_lo || t >= T->g_hi) return 0;
+    const int m = T->n - t - 2;
+    const int Mt = m * (m + 1) / 2;
+    const int wavesPerA = (Mt + 63) / 64;
+    const long waves = (long)(t + 1) * wavesPerA;
+    // each leader chunk's scans are split over `split` waves of one workgroup (the barriers inside
+    // the leader scans need every wave of the workgroup on the same chunk)
+    static const int lsplit = [] {
+        const char *e = getenv("CCJ_LEAD_SPLIT");
+        const int v = e ? atoi(e) : 2;
+        return v == 1 || v == 2 || v == 4 || v == 8 ? v : 2;
+    }();
+    const size_t shmem = lsplit > 1 ? (size_t)(lsplit - 1) * (LEAD_RED > 22 ? LEAD_RED : 22) * 64 * sizeof(int) : 0;
+    hipLaunchKernelGGL(k_level4d<true>, dim3((unsigned)waves), dim3(64 * lsplit), shmem, (hipStream_t)stream, *T, t, wavesPerA,
+                       lsplit, 0, t + 1, 1);
     return (int)hipGetLastError();
 }

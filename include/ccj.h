@@ -73,6 +73,14 @@ typedef struct ccj_options {
     /* 0 (default): W and the traceback run on the GPU (no host copy of the 4-D matrices; getters
      * copy them on first use).  1: on the host over the mirror (the reference restatement). */
     int host_traceback;
+    /* Level-kernel tuning (0 = default for both).
+     * split_target: narrow late levels split each cell's split-point loops over up to 8 waves so
+     *   about this many waves run at once (default 6144); < 0 never splits.
+     * share_splits: split-point sharing between the cells of one gap column: a
+     *   leader cell scans its whole split range once for itself and the next CCJ_SHARE_R-1 cells of
+     *   its column; < 0 turns it off (every cell scans its own range).  Unsharded fills only. */
+    int split_target;
+    int share_splits;
 } ccj_options;
 
 /* Create a context for one sequence: copies the problem, allocates device + pinned host

@@ -13,7 +13,10 @@ r = random.Random(5)
 seq = "".join(r.choice("ACGU") for _ in range(n))
 wf = W_final(seq, 2, params="Turner04")
 wf.ccj()
-wf.ccj()
+fills = []
+for _ in range(int(os.environ.get("CCJ_PROFILE_REPS", "5"))):
+    wf.ccj()
+    fills.append(wf.timing()["fill_ms"])
 L = lib()
 L.ccj_level_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int]
 lv = (ctypes.c_double * n)()
@@ -23,6 +26,8 @@ il = (ctypes.c_double * n)()
 L.ccj_iloop_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
 L.ccj_iloop_times(wf._h, il, n)
 tm = wf.timing()
+tm["fill_ms_median"] = sorted(fills)[len(fills) // 2]
+tm["fill_ms_min"] = min(fills)
 print(json.dumps(tm))
 for t in range(0, n, max(1, n // 25)):
     print(f"t={t:4d} level4d {lv[t]*1e3:9.1f} us   iloop {il[t]*1e3:8.1f} us   diag2d {dg[t]*1e3:8.1f} us")
