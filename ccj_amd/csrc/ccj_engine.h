@@ -27,8 +27,11 @@ enum Mat4 {
 };
 
 constexpr int IE_U = 29;  // u1,u2 in [0,28] for pseudoknot interior loops (pseudo_loop.cc:694-806)
-constexpr int IL_CAP = 856;  // candidate-list capacity per pair (>= 29*29 + IL_B null tail)
-constexpr int IL_B = 8;      // interior-loop candidates per load batch (k_iloop)
+#ifndef CCJ_ILB
+#define CCJ_ILB 8
+#endif
+constexpr int IL_B = CCJ_ILB;  // interior-loop candidates per load batch (k_iloop)
+constexpr int IL_CAP = (IE_U * IE_U + IL_B + 7) / 8 * 8;  // candidate-list capacity per pair (+ IL_B null tail)
 constexpr int IL_SEG = 64;   // per pair: seg[dt] = first list entry of source-level distance dt
 
 struct LevelDesc {

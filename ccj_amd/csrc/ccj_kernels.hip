@@ -462,15 +462,15 @@ __device__ __forceinline__ int il_u1(uint32_t x) { return (int)((x >> 16) & 31u)
 __device__ __forceinline__ int il_dt(uint32_t x) { return (int)(x >> 21); }
 __device__ __forceinline__ int il_e(uint32_t x) { return (int)(int16_t)(x & 0xffffu); }
 
-// min over the wave's candidate list of energy + partner value (PL/PR/PM interior loops)
+// min over the wave's candidate list of energy + partner value (PL/PR/PM interior loops).
+// Software-pipelined one batch deep: the entries and partner loads of batch k+1 are issued before
+// batch k is reduced, so a wave keeps 2*IL_B partner loads in flight.
 template <bool CROSS, bool PMWIN>
 __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restrict__ ent, int cnt,
                                        unsigned long long Atab, int Btab, unsigned lofs2, int as, int bs) {
     int b1 = INF;
-#pragma unroll 1
-    for (int e0 = 0; e0 < cnt; e0 += IL_B) {
-        uint2 E[IL_B];
-        int v[IL_B];
+    if (cnt <= 0) return b1;
+    auto fetch = [&](int e0, uint2 *E) {
         const uint2 *ep = ent + e0;
 #pragma unroll
         for (int u = 0; u < IL_B; ++u) {
@@ -478,6 +478,8 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
             // PM stops at dt <= t-2, before the list's null tail: past cnt, substitute a null entry
             if (PMWIN && e0 + u >= cnt) E[u] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0u);
         }
+    };
+    auto issue = [&](const uint2 *E, int *v) {
 #pragma unroll
         for (int u = 0; u < IL_B; ++u) {
             const int dt = il_dt(E[u].x), u1 = il_u1(E[u].x);
@@ -501,6 +503,8 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
             // global address space: a plain pointer rebuilt from an integer would become a flat load
             v[u] = *(const __attribute__((address_space(1))) int16_t *)(p + lofs2);
         }
+    };
+    auto reduce = [&](const uint2 *E, const int *v) {
 #pragma unroll
         for (int u = 0; u < IL_B; ++u) {
             const int c = il_e(E[u].x) + v[u];
@@ -511,7 +515,25 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
                 b1 = imin(b1, c);
             }
         }
+    };
+    uint2 E[IL_B];
+    int v[IL_B];
+    fetch(0, E);
+    issue(E, v);
+#pragma unroll 1
+    for (int e0 = IL_B; e0 < cnt; e0 += IL_B) {
+        uint2 En[IL_B];
+        int vn[IL_B];
+        fetch(e0, En);
+        issue(En, vn);
+        reduce(E, v);
+#pragma unroll
+        for (int u = 0; u < IL_B; ++u) {
+            E[u] = En[u];
+            v[u] = vn[u];
+        }
     }
+    reduce(E, v);
     return b1;
 }
 
