@@ -177,7 +177,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                      "algorithmic_bytes_per_launch": bytes_lv / nlaunch,
-                     "kernel": "k_level4d", "launches_per_fold": nlaunch,
+                     "kernel": "k_level4d (one level = k_level4d<false> + k_level4d<true> on the "
+                               "split-sharing levels, concurrent; duration = the level's span)",
+                     "launches_per_fold": nlaunch,
                      "avg_launch_us": avg_launch_s * 1e6, "algorithmic_bytes_per_fold": bytes_lv},
         "roofline_iloop": {"bound": "hbm", "achieved": il_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": il_achieved / HBM_PEAK_GBS, "kernel": "k_iloop",

@@ -10,6 +10,7 @@ bench.py reports profiles/traffic.json's k_level4d figure as roofline.traffic.
 import csv
 import json
 import os
+import re
 import shutil
 import sys
 from collections import defaultdict
@@ -26,10 +27,52 @@ def pmc(path, counter):
         for r in csv.DictReader(f):
             if r["Counter_Name"] != counter:
                 continue
-            k = r["Kernel_Name"].split("(")[0]
+            k = kname(r["Kernel_Name"])
             tot[k] += float(r["Counter_Value"]) * 1024.0  # KB -> bytes
             launches[k].add(r["Dispatch_Id"])
+            if k.startswith("k_level4d<"):
+                # one level = k_level4d<false> + (on sharing levels) k_level4d<true>: bytes summed,
+                # launches counted once per level
+                tot["k_level4d"] += float(r["Counter_Value"]) * 1024.0
+                if k == "k_level4d<false>":
+                    launches["k_level4d"].add(r["Dispatch_Id"])
     return {k: (tot[k], len(launches[k])) for k in tot}
+
+
+def kname(full):
+    """'void k_level4d<false>(ccj::DevTables, ...)' -> 'k_level4d<false>'"""
+    return re.sub(r"^void ", "", full.split("(")[0]).strip()
+
+
+def level_spans(trace_csv):
+    """Per-level span of the level kernels from the kernel trace: each k_level4d<true> dispatch
+    runs beside the k_level4d<false> dispatch of the same level (they overlap in time); the level's
+    span is first start to last end, the figure bench.py measures with HIP events on the level
+    stream (roofline.avg_launch_us)."""
+    plain, lead = [], []
+    with open(trace_csv) as f:
+        for r in csv.DictReader(f):
+            k = kname(r["Kernel_Name"])
+            iv = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+            if k == "k_level4d<false>":
+                plain.append(iv)
+            elif k == "k_level4d<true>":
+                lead.append(iv)
+    plain.sort()
+    lead.sort()
+    # both launches of a level wait for the same events, so a leader dispatch belongs to the plain
+    # dispatch whose start is nearest to its own
+    import bisect
+    starts = [p[0] for p in plain]
+    span = [list(p) for p in plain]
+    for s0, e0 in lead:
+        x = bisect.bisect_left(starts, s0)
+        cand = [y for y in (x - 1, x) if 0 <= y < len(plain)]
+        y = min(cand, key=lambda y: abs(starts[y] - s0))
+        span[y][0], span[y][1] = min(span[y][0], s0), max(span[y][1], e0)
+    spans = [e - s for s, e in span]
+    return {"levels": len(spans), "avg_level_span_us": sum(spans) / max(len(spans), 1) / 1e3,
+            "plain_dispatches": len(plain), "leader_dispatches": len(lead)}
 
 
 def main():
@@ -55,6 +98,10 @@ def main():
     with open(os.path.join(out, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(traffic, indent=1))
+    sp = level_spans(os.path.join(PROF, "kt", "kt_kernel_trace.csv"))
+    with open(os.path.join(out, f"{rnd}_level_span.json"), "w") as f:
+        json.dump(sp, f, indent=1)
+    print(json.dumps(sp, indent=1))
 
 
 if __name__ == "__main__":
