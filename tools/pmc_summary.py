@@ -19,7 +19,7 @@ def main(argv):
     for path in argv[2:]:
         with open(path) as f:
             for r in csv.DictReader(f):
-                if not r["Kernel_Name"].startswith(kern):
+                if not r["Kernel_Name"].replace("void ", "", 1).startswith(kern):
                     continue
                 tot[r["Counter_Name"]] += float(r["Counter_Value"])
                 dur[(path, r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
