@@ -1744,6 +1744,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     HIPCHK(c, hipSetDevice(c->device));
     const int n = c->n;
     hipStream_t st = c->st;
+    const auto enq0 = std::chrono::steady_clock::now();
     const size_t plane = (size_t)(n + 1) * c->rs;
     c->filled = c->mirrored = false;
     HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), st));
@@ -1754,7 +1755,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     HIPCHK(c, hipEventRecord(c->ev_pre, st));
     // Four streams:
     //   st_d : k_diag2d(s)  needs P(s) (p_done) and spans < s (stream order)
-    //   st_il: k_iloop(t)   needs 4-D levels <= t-2 (lev_done[t-2])
+    //   st_il: k_iloop(t)   needs 4-D levels <= t-3 (lev_done[t-3]; the dt = 2 term is in k_level4d)
     //   st   : k_level4d(t) needs level t-1 (stream order), k_iloop(t), k_diag2d(t-1)
     //   st_p : k_pterm(s)   needs PK levels <= s-3 (lev_done[s-3])
     // so k_diag2d(t) and k_iloop(t+1) overlap k_level4d(t).  Every event is recorded (enqueued)
@@ -1770,7 +1771,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
         HIPCHK(c, hipEventRecord(ev[1], c->st_d));
         HIPCHK(c, hipEventRecord(c->dg_done[s], c->st_d));
         if (s < c->nlev) {
-            if (s >= 2) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 2], 0));
+            if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 3], 0));
             HIPCHK(c, hipEventRecord(ev[2], c->st_il));
             const int G = c->world;
             for (int r = 0; r < G; ++r) {
@@ -1840,6 +1841,9 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
             HIPCHK(c, hipEventRecord(c->p_done[s + 3], c->st_p));
         }
     }
+    if (getenv("CCJ_TRACE_ENQUEUE"))
+        fprintf(stderr, "ccj_fill_device: enqueue %.2f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - enq0).count());
     // join: the fill ends when the last level and the last span are done
     HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[n - 1], 0));
     HIPCHK(c, hipEventRecord(c->ev_end, st));

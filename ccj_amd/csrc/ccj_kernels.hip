@@ -445,7 +445,9 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
 //   PR: wave = (a, q, i-chunk), lanes i  — closing pair (k, l), q = i+h-1 = k-a-3
 //   PM: wave = (h, j, a-chunk), lanes a  — pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
 // The minimum (clamped like a store) goes into the cell's PL/PR/PM slot of level t, where
-// k_level4d(t) picks it up.  Needs levels <= t-2 only.
+// k_level4d(t) picks it up.  The candidate with no unpaired base (u1 = u2 = 0, source level t-2)
+// reads the same inner cell as the stack term, so k_level4d(t) evaluates it there; k_iloop(t)
+// walks the lists from dt = 3 on and needs levels <= t-3 only, a whole level of slack.
 // ------------------------------------------------------------------------------------------
 // Each list entry's partner address is A[dt] + B[u1] (+ 2*u1*dt for PL/PM) bytes + the lane's
 // offset: A (64-bit, per source level) and B (per u1) are per-wave tables held one value per lane
@@ -567,7 +569,8 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
                    2 * (T.ldx[tl].lbx + (long long)(a - lane) * T.ld[tl].M + (long long)i * m + (long long)i * lane + lane - 1 - BIAS);
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
         if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
-        const int b1 = il_scan<true, false>(T, T.il + pidx * IL_CAP, (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1], Atab, Btab, lofs2, 0, 0);
+        const int e0 = (int)T.ilseg[pidx * IL_SEG + 3];
+        const int b1 = il_scan<true, false>(T, T.il + pidx * IL_CAP + e0, (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0, Atab, Btab, lofs2, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
         if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
             atomicOr(T.err, 128);
@@ -592,7 +595,8 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         if (lvl_ok) Atab = (unsigned long long)T.d4x + 2 * (T.ldx[tl].lbx + T.ld[tl].C + (long long)a * T.ld[tl].M);
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
         if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
-        const int b1 = il_scan<false, false>(T, T.il + pidx * IL_CAP, (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1], Atab, Btab, lofs2, 0, 0);
+        const int e0 = (int)T.ilseg[pidx * IL_SEG + 3];
+        const int b1 = il_scan<false, false>(T, T.il + pidx * IL_CAP + e0, (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0, Atab, Btab, lofs2, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
         if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
             atomicOr(T.err, 128);
@@ -623,7 +627,8 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
         // entries with dt > t-2 fit no cell of this level
         const int cnt = (int)T.ilmseg[pidx * IL_SEG + imin(t - 1, IL_SEG - 1)];
-        const int b1 = il_scan<true, true>(T, T.ilm + pidx * IL_CAP, cnt, Atab, Btab, lofs2, as, t - as);
+        const int e0 = (int)T.ilmseg[pidx * IL_SEG + 3];
+        const int b1 = il_scan<true, true>(T, T.ilm + pidx * IL_CAP + e0, cnt - e0, Atab, Btab, lofs2, as, t - as);
 #ifdef CCJ_DEBUG_BOUNDS
         if (act && (a < 0 || a > t || h < 0 || h >= m || (j - a) < 1 || (j - a) > m - h)) {
             atomicOr(T.err, 128);
@@ -1271,10 +1276,13 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     if (pl_ok) {
         int b1 = INF;
         const int Uin = (a - 2) * L2.M + m + 3;  // (i+1, j-1, k, l): lane L0 + h
-        if (a > TURN) {
-            if (a > TURN + 2) b1 = LDX(lp2, L2, PL, Uin, L0 + uh) + W2E(T.est, i, j);
+        if (a > TURN + 2) {
+            // stack (:692-694) and, on the same inner cell, the interior loop with no unpaired base
+            // (d, dp) = (i+1, j-1); k_iloop(t) did the rest of get_PLiloop (source levels <= t-3)
+            const int pin = LDX(lp2, L2, PL, Uin, L0 + uh);
+            b1 = pin + W2E(T.est, i, j);
 #ifndef CCJ_ABLATE_ILOOP
-            if (a >= 6) b1 = imin(b1, (int)dst[PL * C]);
+            b1 = imin(b1, imin(pin + W2E(T.ie, i, j), (int)dst[PL * C]));
 #endif
         }
         const int b2 = (a >= 2) ? imin(LDX(lp2, L2, PLmloop10, Uin, L0 + uh), LDX(lp2, L2, PLmloop01, Uin, L0 + uh)) + apbp2 : INF;
@@ -1287,10 +1295,11 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     if (pr_ok) {
         int b1 = INF;
         const int Uin = a * L2.M + m + 2;  // (i, j, k+1, l-1): lane L0 + h
-        if (b > TURN) {
-            if (b > TURN + 2) b1 = LDX(lp2, L2, PR, Uin, L0 + uh) + W2E(T.est, k, l);
+        if (b > TURN + 2) {
+            const int pin = LDX(lp2, L2, PR, Uin, L0 + uh);  // stack and (d, dp) = (k+1, l-1)
+            b1 = pin + W2E(T.est, k, l);
 #ifndef CCJ_ABLATE_ILOOP
-            if (b >= 6) b1 = imin(b1, (int)dst[PR * C]);
+            b1 = imin(b1, imin(pin + W2E(T.ie, k, l), (int)dst[PR * C]));
 #endif
         }
         const int b2 = (b >= 2) ? imin(LDX(lp2, L2, PRmloop10, Uin, L0 + uh), LDX(lp2, L2, PRmloop01, Uin, L0 + uh)) + apbp2 : INF;
@@ -1304,10 +1313,11 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
         int b1 = INF;
         const bool inner = (a >= 1 && b >= 1);
         const int Uin = (a - 1) * L2.M + 2 * m + 3;  // (i, j-1, k+1, l): lane L0
-        if (g > TURN) {
-            if (inner) b1 = LDX(lp2, L2, PM, Uin, L0) + W2E(T.est, j - 1, k + 1);
+        if (g > TURN && inner) {
+            const int pin = LDX(lp2, L2, PM, Uin, L0);  // stack and (d, dp) = (j-1, k+1)
+            b1 = pin + W2E(T.est, j - 1, k + 1);
 #ifndef CCJ_ABLATE_ILOOP
-            if (a >= 2 && b >= 2) b1 = imin(b1, (int)dst[PM * C]);
+            if (a >= 2 && b >= 2) b1 = imin(b1, imin(pin + W2E(T.ie, j - 1, k + 1), (int)dst[PM * C]));
 #endif
         }
         const int b2 = inner ? imin(LDX(lp2, L2, PMmloop10, Uin, L0), LDX(lp2, L2, PMmloop01, Uin, L0)) + apbp2 : INF;

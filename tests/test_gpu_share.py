@@ -64,3 +64,21 @@ def test_sharing_on_off_identical(n, seed):
     h_on = _hashes(seq, "Turner04")
     assert _hashes(seq, "Turner04", share_splits=-1) == h_on
     assert _hashes(seq, "Turner04", split_target=-1) == h_on
+
+
+def test_sharing_n400_same_result():
+    """BASELINE config-5 size (n = 400, past the stock reference's n >= 214 abort): sharing on and
+    off give the same MFE, structure and W array (full hashes would copy 47 GB to the host)."""
+    from ccj_amd import W_final
+    n = 400
+    seq = _rseq(6, n)
+    out = []
+    for kw in ({}, {"share_splits": -1}):
+        wf = W_final(seq, 2, params="Turner04", **kw)
+        try:
+            e = wf.ccj()
+            out.append((e, wf.structure, [wf.W(j) for j in range(n + 1)]))
+        finally:
+            wf.close()
+    assert out[0] == out[1]
+    assert len(out[0][1]) == n and out[0][0] == out[0][2][n] / 100.0
