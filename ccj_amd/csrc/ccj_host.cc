@@ -1464,10 +1464,19 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     int g_lo = 0, g_hi = 0;
     long long accC = 0;
     if (c->share && c->world == 1) {
-        for (int t = 0; t < c->nlev; ++t) {
-            const bool unsplit = ccjk_level_split(n, t, 0, t + 1, c->split_target) == 1;
-            if (unsplit && g_hi == 0) g_lo = t, g_hi = t + 1;
-            else if (unsplit && g_hi == t) g_hi = t + 1;
+        // the levels that run unsplit (the middle ones).  CCJ_SHARE_LATE=1 extends the range to
+        // the narrow late levels too, where k_level4d<true> splits the long scans
+        // (ccjk_level4d_lead): measured 1.2 ms slower at n=200, so off by default
+        g_lo = -1;
+        for (int t = 0; t < c->nlev && g_lo < 0; ++t)
+            if (ccjk_level_split(n, t, 0, t + 1, c->split_target) == 1) g_lo = t;
+        if (g_lo < 0 || !(getenv("CCJ_SHARE_LATE") && atoi(getenv("CCJ_SHARE_LATE")) == 1)) {
+            g_hi = g_lo < 0 ? 0 : g_lo;
+            for (int t = std::max(g_lo, 0); g_lo >= 0 && t < c->nlev; ++t)
+                if (ccjk_level_split(n, t, 0, t + 1, c->split_target) == 1 && g_hi == t) g_hi = t + 1;
+            if (g_lo < 0) g_lo = 0;
+        } else {
+            g_hi = c->nlev;
         }
         for (int t = g_lo; t < g_hi; ++t) accC = std::max<long long>(accC, c->lv_host[t].C);
     }

@@ -1504,9 +1504,8 @@ extern "C" int ccjk_level4d(const DevTables *T, int t, int a_lo, int a_end, int 
     const int wavesPerA = (Mt + 63) / 64;
     if (a_end <= a_lo) return 0;
     const long waves = (long)(a_end - a_lo) * wavesPerA;
-    const int split = ccjk_level_split(T->n, t, a_lo, a_end, T->split_target);
-    // split-point sharing needs one cell per lane on every level of its range
-    if (split > 1 && t >= T->g_lo && t < T->g_hi) return (int)hipErrorInvalidValue;
+    // on the sharing levels this launch only has follower cells (short scans): never split
+    const int split = (t >= T->g_lo && t < T->g_hi) ? 1 : ccjk_level_split(T->n, t, a_lo, a_end, T->split_target);
     const int threads = split <= 4 ? 256 : 64 * split;
     const int cpb = threads / 64 / split;
     const long blocks = (waves + cpb - 1) / cpb;
@@ -1529,8 +1528,10 @@ extern "C" int ccjk_level4d_lead(const DevTables *T, int t, void *stream) {
         const int v = e ? atoi(e) : 2;
         return v == 1 || v == 2 || v == 4 || v == 8 ? v : 2;
     }();
-    const size_t shmem = lsplit > 1 ? (size_t)(lsplit - 1) * (LEAD_RED > 22 ? LEAD_RED : 22) * 64 * sizeof(int) : 0;
-    hipLaunchKernelGGL(k_level4d<true>, dim3((unsigned)waves), dim3(64 * lsplit), shmem, (hipStream_t)stream, *T, t, wavesPerA,
-                       lsplit, 0, t + 1, 1);
+    // narrow late levels: as many split waves as the plain heuristic would give the whole level
+    const int sp = imax(lsplit, ccjk_level_split(T->n, t, 0, t + 1, T->split_target));
+    const size_t shmem = sp > 1 ? (size_t)(sp - 1) * (LEAD_RED > 22 ? LEAD_RED : 22) * 64 * sizeof(int) : 0;
+    hipLaunchKernelGGL(k_level4d<true>, dim3((unsigned)waves), dim3(64 * sp), shmem, (hipStream_t)stream, *T, t, wavesPerA,
+                       sp, 0, t + 1, 1);
     return (int)hipGetLastError();
 }
