@@ -77,7 +77,7 @@ enum RecType { RA = 0, RK = 1, RL = 2, NREC = 3 };
 // two transposed copies of WB/WBP/WP (wq: row q, p contiguous; wp: row p, q contiguous), one
 // SHARE_R-wide vector load per array.
 #ifndef CCJ_SHARE_R
-#define CCJ_SHARE_R 3
+#define CCJ_SHARE_R 4
 #endif
 constexpr int SHARE_R = CCJ_SHARE_R;
 constexpr int SHARE_NACC = 4;

@@ -1526,7 +1526,7 @@ extern "C" int ccjk_level4d_lead(const DevTables *T, int t, void *stream) {
     static const int lsplit = [] {
         const char *e = getenv("CCJ_LEAD_SPLIT");
         const int v = e ? atoi(e) : 2;
-        return v == 1 || v == 2 || v == 4 || v == 8 ? v : 2;
+        return v >= 1 && v <= 8 ? v : 2;
     }();
     // narrow late levels: as many split waves as the plain heuristic would give the whole level
     const int sp = imax(lsplit, ccjk_level_split(T->n, t, 0, t + 1, T->split_target));
