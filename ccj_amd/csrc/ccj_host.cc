@@ -110,7 +110,7 @@ struct ccj_ctx {
     int8_t *d_vt = nullptr;
     hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr, st_il = nullptr, st_d = nullptr;
     hipStream_t st_lead = nullptr;   // k_level4d<true>: split-point-sharing leaders of the level
-    std::vector<hipEvent_t> ld_done;
+    std::vector<hipEvent_t> ld_done, pl_done;  // k_level4d<true>(t) / k_level4d<false>(t) finished
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<double> lev_ms_v, diag_ms_v, il_ms_v;
     std::vector<hipEvent_t> il_done, dg_done;  // k_iloop(t) / k_diag2d(sigma) finished
@@ -1437,6 +1437,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_lead, hipStreamNonBlocking));
     c->ld_done.resize(n + 1);
     for (auto &e : c->ld_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->pl_done.resize(n + 1);
+    for (auto &e : c->pl_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->il_done.resize(n + 1);
     for (auto &e : c->il_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->dg_done.resize(n + 1);
@@ -1802,13 +1804,20 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
                 ccj_shard_range(n, s, G, r, &lo, &hi);
                 HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, lo, hi, G == 1 ? 1 : 0, st));
             }
+            HIPCHK(c, hipEventRecord(c->pl_done[s], st));
             if (s >= c->T.g_lo && s < c->T.g_hi) {
                 // leaders on their own stream, same inputs as the level kernel (level s-1 complete,
-                // k_iloop(s), k_diag2d(s-1)); the level is done when both launches are
+                // k_iloop(s), k_diag2d(s-1)); the level is done when both launches are.  Level s-1
+                // is waited for as its plain launch (pl_done) plus, in stream order, its leaders
+                // (st_lead), not as the joined lev_done, which would put a second cross-stream hop
+                // between two leader launches.
                 HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->il_done[s], 0));
                 if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->dg_done[s - 1], 0));
-                if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->lev_done[s - 1], 0));
-                else HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->ev_pre, 0));
+                if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->pl_done[s - 1], 0));
+                if (s - 1 >= c->T.g_hi || s - 1 < c->T.g_lo) {  // level s-1 had no leader launch on st_lead
+                    if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->lev_done[s - 1], 0));
+                    else HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->ev_pre, 0));
+                }
                 HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, c->st_lead));
                 HIPCHK(c, hipEventRecord(c->ld_done[s], c->st_lead));
                 HIPCHK(c, hipStreamWaitEvent(st, c->ld_done[s], 0));
@@ -2322,6 +2331,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->st_d) hipStreamDestroy(c->st_d);
     if (c->st_lead) hipStreamDestroy(c->st_lead);
     for (auto e : c->ld_done) hipEventDestroy(e);
+    for (auto e : c->pl_done) hipEventDestroy(e);
     for (auto e : c->il_done) hipEventDestroy(e);
     for (auto e : c->dg_done) hipEventDestroy(e);
     for (auto e : c->tev) hipEventDestroy(e);
