@@ -1450,7 +1450,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     for (auto &e : c->lev_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->p_done.resize(n + 1);
     for (auto &e : c->p_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    c->tev.resize(6 * (size_t)n + 6);
+    c->tev.resize(7 * (size_t)n + 7);
     for (auto &e : c->tev) HIPCHK(cp, hipEventCreate(&e));
 
     const size_t plane = (size_t)(n + 1) * c->rs;
@@ -1775,7 +1775,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     HIPCHK(c, hipStreamWaitEvent(c->st_il, c->ev_pre, 0));
     HIPCHK(c, hipStreamWaitEvent(c->st_p, c->ev_pre, 0));
     for (int s = 0; s < n; ++s) {
-        hipEvent_t *ev = &c->tev[6 * (size_t)s];
+        hipEvent_t *ev = &c->tev[7 * (size_t)s];
         if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_d, c->p_done[s], 0));
         HIPCHK(c, hipEventRecord(ev[0], c->st_d));
         HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, s, c->st_d));
@@ -1818,6 +1818,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
                     if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->lev_done[s - 1], 0));
                     else HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->ev_pre, 0));
                 }
+                HIPCHK(c, hipEventRecord(ev[6], c->st_lead));
                 HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, c->st_lead));
                 HIPCHK(c, hipEventRecord(c->ld_done[s], c->st_lead));
                 HIPCHK(c, hipStreamWaitEvent(st, c->ld_done[s], 0));
@@ -1883,7 +1884,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     c->diag_ms_v.assign(n, 0.0);
     c->il_ms_v.assign(n, 0.0);
     for (int s = 0; s < n; ++s) {
-        const hipEvent_t *ev = &c->tev[6 * (size_t)s];
+        const hipEvent_t *ev = &c->tev[7 * (size_t)s];
         HIPCHK(c, hipEventElapsedTime(&ms, ev[0], ev[1]));
         dsum += ms;
         c->diag_ms_v[s] = ms;
@@ -1891,7 +1892,15 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
             HIPCHK(c, hipEventElapsedTime(&ms, ev[2], ev[3]));
             isum += ms;
             c->il_ms_v[s] = ms;
-            HIPCHK(c, hipEventElapsedTime(&ms, ev[4], ev[5]));
+            // the level's span: from the first of its two launches to the join (ev[6] = leaders)
+            float t4 = 0, t5 = 0, t6 = 0;
+            HIPCHK(c, hipEventElapsedTime(&t4, c->ev_start, ev[4]));
+            HIPCHK(c, hipEventElapsedTime(&t5, c->ev_start, ev[5]));
+            if (s >= c->T.g_lo && s < c->T.g_hi) {
+                HIPCHK(c, hipEventElapsedTime(&t6, c->ev_start, ev[6]));
+                t4 = std::min(t4, t6);
+            }
+            ms = t5 - t4;
             lsum += ms;
             c->lev_ms_v[s] = ms;
         }
