@@ -71,6 +71,7 @@ struct ccj_ctx {
     bool host_tb = false;                   // W + traceback on the host over the mirror (else on the GPU)
     int split_target = 6144;                // k_level4d split heuristic (0: never split)
     bool share = true;                      // split-point sharing
+    bool lead_same_stream = false;          // CCJ_LEAD_SAME_STREAM=1: leaders serialized after the plain launch
     ncclComm_t comm = nullptr;
 
     // layout
@@ -1369,6 +1370,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         const char *e = getenv("CCJ_SPLIT_TARGET");
         c->split_target = e ? atoi(e) : 6144;
         if (opts && opts->split_target) c->split_target = opts->split_target < 0 ? 0 : opts->split_target;
+        const char *ls = getenv("CCJ_LEAD_SAME_STREAM");
+        c->lead_same_stream = ls && atoi(ls) == 1;
         const char *g = getenv("CCJ_SHARE_SPLITS");
         c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
     }
@@ -1805,7 +1808,10 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
                 HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, lo, hi, G == 1 ? 1 : 0, st));
             }
             HIPCHK(c, hipEventRecord(c->pl_done[s], st));
-            if (s >= c->T.g_lo && s < c->T.g_hi) {
+            if (s >= c->T.g_lo && s < c->T.g_hi && c->lead_same_stream) {
+                HIPCHK(c, hipEventRecord(ev[6], st));  // timing experiment: leaders after the plain launch
+                HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, st));
+            } else if (s >= c->T.g_lo && s < c->T.g_hi) {
                 // leaders on their own stream, same inputs as the level kernel (level s-1 complete,
                 // k_iloop(s), k_diag2d(s-1)); the level is done when both launches are.  Level s-1
                 // is waited for as its plain launch (pl_done) plus, in stream order, its leaders

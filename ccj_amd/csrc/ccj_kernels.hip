@@ -749,6 +749,13 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     const LvlDev *__restrict__ LD = T.ld;
     const int16_t *__restrict__ D4 = T.d4;
 #define LDX(lp, L, x, U, ln) ((int)(lp)[(unsigned)((x) * (L).C + (U)) + (ln)])
+    // WB of an interval of `len` bases from its WBP, as k_diag2d stores it (get_WB,
+    // pseudo_loop.cc:647-653: min(cp*len, WBP)): one load fewer per split side
+#ifdef CCJ_WB_LOAD
+#define WBD(wbp, len, idx) ((int)WB[idx])
+#else
+#define WBD(wbp, len, idx) imin(cp * (len), (wbp))
+#endif
 #ifdef CCJ_DEBUG_BOUNDS
 #define CHK(dt, ap_, dh, di) \
     if ((dt) < 1 || (dt) > t || (ap_) < 0 || (ap_) > t - (dt) || h + (dh) >= m + (dt) || i + (di) < 1 || \
@@ -793,8 +800,10 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     auto load_a = [&](int s) {
         AV v;
         const int r2 = (s - 1) * rs, jl = j - s + 1;
-        v.wb_i = WB[r2 + i]; v.wbp_i = WBPr[r2 + i]; v.wp_i = WP[r2 + i];      // (i, i+s-1)
-        v.wb_j = WB[r2 + jl]; v.wbp_j = WBPr[r2 + jl]; v.wp_j = WP[r2 + jl];   // (j-s+1, j)
+        v.wbp_i = WBPr[r2 + i]; v.wp_i = WP[r2 + i];      // (i, i+s-1)
+        v.wbp_j = WBPr[r2 + jl]; v.wp_j = WP[r2 + jl];   // (j-s+1, j)
+        v.wb_i = WBD(v.wbp_i, s, r2 + i);
+        v.wb_j = WBD(v.wbp_j, s, r2 + jl);
         CHK(s, a - s, 0, s);
         CHK(s, a - s, s, 0);
 #ifdef CCJ_ABLATE_LOCAL
@@ -864,8 +873,10 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
-                v.qb[SHARE_R - 1 - r] = WB[o + i - r]; v.qbp[SHARE_R - 1 - r] = WBPr[o + i - r]; v.qp[SHARE_R - 1 - r] = WP[o + i - r];
-                v.pb[r] = WB[o + j - s + 1]; v.pbp[r] = WBPr[o + j - s + 1]; v.pp[r] = WP[o + j - s + 1];
+                v.qbp[SHARE_R - 1 - r] = WBPr[o + i - r]; v.qp[SHARE_R - 1 - r] = WP[o + i - r];
+                v.pbp[r] = WBPr[o + j - s + 1]; v.pp[r] = WP[o + j - s + 1];
+                v.qb[SHARE_R - 1 - r] = WBD(v.qbp[SHARE_R - 1 - r], s + r, o + i - r);
+                v.pb[r] = WBD(v.pbp[r], s + r, o + j - s + 1);
             }
 #endif
             return v;
@@ -1005,8 +1016,10 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     auto load_b = [&](int s) {
         BV v;
         const int r2 = (s - 1) * rs, ll = l - s + 1;
-        v.wb_k = WB[r2 + k]; v.wbp_k = WBPr[r2 + k]; v.wp_k = WP[r2 + k];      // (k, k+s-1)
-        v.wb_l = WB[r2 + ll]; v.wbp_l = WBPr[r2 + ll]; v.wp_l = WP[r2 + ll];   // (l-s+1, l)
+        v.wbp_k = WBPr[r2 + k]; v.wp_k = WP[r2 + k];      // (k, k+s-1)
+        v.wbp_l = WBPr[r2 + ll]; v.wp_l = WP[r2 + ll];   // (l-s+1, l)
+        v.wb_k = WBD(v.wbp_k, s, r2 + k);
+        v.wb_l = WBD(v.wbp_l, s, r2 + ll);
         CHK(s, a, s, 0);
         CHK(s, a, 0, 0);
 #ifdef CCJ_ABLATE_LOCAL
@@ -1079,8 +1092,10 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
-                v.qb[SHARE_R - 1 - r] = WB[o + k - r]; v.qbp[SHARE_R - 1 - r] = WBPr[o + k - r]; v.qp[SHARE_R - 1 - r] = WP[o + k - r];
-                v.pb[r] = WB[o + l - s + 1]; v.pbp[r] = WBPr[o + l - s + 1]; v.pp[r] = WP[o + l - s + 1];
+                v.qbp[SHARE_R - 1 - r] = WBPr[o + k - r]; v.qp[SHARE_R - 1 - r] = WP[o + k - r];
+                v.pbp[r] = WBPr[o + l - s + 1]; v.pp[r] = WP[o + l - s + 1];
+                v.qb[SHARE_R - 1 - r] = WBD(v.qbp[SHARE_R - 1 - r], s + r, o + k - r);
+                v.pb[r] = WBD(v.pbp[r], s + r, o + l - s + 1);
             }
 #endif
             return v;
@@ -1337,6 +1352,7 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
         vPO = imin(imin(b1, b2), b3);
     }
 #undef LDX
+#undef WBD
 #undef CHK
 #undef CHKR
 #undef CHKA
