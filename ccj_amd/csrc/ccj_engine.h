@@ -110,6 +110,7 @@ struct DevTables {
     const int16_t *est;            // [w][p] e_stP, saturated at 32767
     int16_t *ie;                   // [u1][u2][w][p] e_intP, saturated at 32767
     int *V; int8_t *Vt; int *WM, *WMv, *WMp, *P, *WBP, *WPP, *WB, *WP;  // [w][p]
+    int2 *WBW;                     // [w][p] (WBP, WP): the two 2-D operands of a k_level4d split step, one load
     unsigned long long *Pk;        // [w][p] (P + 2^31) << 32 | first (j,d,k) split of the minimum (k_pterm)
     const LevelDesc *lv;           // per level t
     int16_t *d4;                   // 4-D storage base

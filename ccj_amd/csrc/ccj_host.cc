@@ -94,6 +94,7 @@ struct ccj_ctx {
     uint4 *d_rec = nullptr;                  // AoS loop records
     int *d_wq = nullptr, *d_wp = nullptr;    // transposed WB/WBP/WP copies (split-point sharing)
     uint4 *d_acc = nullptr;                  // partial-record ring (split-point sharing)
+    int2 *d_wbw = nullptr;                   // (WBP, WP) pairs [w][p]
     long long nrec = 0;
     long long nx = 0, npm = 0;
     LvlX *d_ldx = nullptr;
@@ -1540,6 +1541,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         HIPCHK(cp, hipMemset(c->d_ilmseg, 0, pairs * IL_SEG * sizeof(uint32_t)));
     }
     HIPCHK(cp, hipMalloc(&c->d2i, A2_N * plane * sizeof(int)));
+    HIPCHK(cp, hipMalloc(&c->d_wbw, plane * sizeof(int2)));
     HIPCHK(cp, hipMalloc(&c->d_pk, plane * sizeof(unsigned long long)));
     HIPCHK(cp, hipMalloc(&c->d_W, (n + 1) * sizeof(int)));
     HIPCHK(cp, hipMalloc(&c->d_fpair, (n + 1) * sizeof(int)));
@@ -1703,6 +1705,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.WPP = c->d2i + A2_WPP * plane;
     T.WB = c->d2i + A2_WB * plane;
     T.WP = c->d2i + A2_WP * plane;
+    T.WBW = c->d_wbw;
     T.Vt = c->d_vt;
     T.lv = c->d_lv;
     T.d4 = c->d4;
@@ -2322,6 +2325,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_wq);
     hipFree(c->d_wp);
     hipFree(c->d_acc);
+    hipFree(c->d_wbw);
     hipFree(c->pmx);
     hipFree(c->d_ldx);
     hipFree(c->d_il);

@@ -151,6 +151,7 @@ __global__ void k_init2d(DevTables T, int total) {
         T.Pk[x] = ~0ull;
         T.WB[x] = 0;
         T.WP[x] = 0;
+        T.WBW[x] = make_int2(INF + 1, 0);
     }
 }
 
@@ -289,6 +290,7 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
             int wpp = INF + 1;
             if (m < INF / 2) { wpp = m; T.WPP[cell] = m; }
             T.WP[cell] = imin(pe.PUP * (sigma + 1), wpp);
+            T.WBW[cell] = make_int2(wbp, T.WP[cell]);  // the pair the level loops load
             if (T.wq) {  // transposed copies for the split-point-sharing leaders of k_level4d
                 const long long q0 = (long long)l * T.ws + i + WQ_OFF, p0 = (long long)i * T.ws + l;
                 const int wb = imin(pe.cp * (sigma + 1), wbp), wp = imin(pe.PUP * (sigma + 1), wpp);
@@ -746,6 +748,7 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     const int *__restrict__ WB = T.WB;
     const int *__restrict__ WP = T.WP;
     const int *__restrict__ WBPr = T.WBP;
+    const int2 *__restrict__ WBW = T.WBW;
     const LvlDev *__restrict__ LD = T.ld;
     const int16_t *__restrict__ D4 = T.d4;
 #define LDX(lp, L, x, U, ln) ((int)(lp)[(unsigned)((x) * (L).C + (U)) + (ln)])
@@ -800,8 +803,9 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     auto load_a = [&](int s) {
         AV v;
         const int r2 = (s - 1) * rs, jl = j - s + 1;
-        v.wbp_i = WBPr[r2 + i]; v.wp_i = WP[r2 + i];      // (i, i+s-1)
-        v.wbp_j = WBPr[r2 + jl]; v.wp_j = WP[r2 + jl];   // (j-s+1, j)
+        const int2 w2i = WBW[r2 + i], w2j = WBW[r2 + jl];  // (WBP, WP) of (i, i+s-1) and (j-s+1, j)
+        v.wbp_i = w2i.x; v.wp_i = w2i.y;
+        v.wbp_j = w2j.x; v.wp_j = w2j.y;
         v.wb_i = WBD(v.wbp_i, s, r2 + i);
         v.wb_j = WBD(v.wbp_j, s, r2 + jl);
         CHK(s, a - s, 0, s);
@@ -873,8 +877,9 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
-                v.qbp[SHARE_R - 1 - r] = WBPr[o + i - r]; v.qp[SHARE_R - 1 - r] = WP[o + i - r];
-                v.pbp[r] = WBPr[o + j - s + 1]; v.pp[r] = WP[o + j - s + 1];
+                const int2 wq = WBW[o + i - r], wp2 = WBW[o + j - s + 1];
+                v.qbp[SHARE_R - 1 - r] = wq.x; v.qp[SHARE_R - 1 - r] = wq.y;
+                v.pbp[r] = wp2.x; v.pp[r] = wp2.y;
                 v.qb[SHARE_R - 1 - r] = WBD(v.qbp[SHARE_R - 1 - r], s + r, o + i - r);
                 v.pb[r] = WBD(v.pbp[r], s + r, o + j - s + 1);
             }
@@ -1016,8 +1021,9 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     auto load_b = [&](int s) {
         BV v;
         const int r2 = (s - 1) * rs, ll = l - s + 1;
-        v.wbp_k = WBPr[r2 + k]; v.wp_k = WP[r2 + k];      // (k, k+s-1)
-        v.wbp_l = WBPr[r2 + ll]; v.wp_l = WP[r2 + ll];   // (l-s+1, l)
+        const int2 w2k = WBW[r2 + k], w2l = WBW[r2 + ll];  // (WBP, WP) of (k, k+s-1) and (l-s+1, l)
+        v.wbp_k = w2k.x; v.wp_k = w2k.y;
+        v.wbp_l = w2l.x; v.wp_l = w2l.y;
         v.wb_k = WBD(v.wbp_k, s, r2 + k);
         v.wb_l = WBD(v.wbp_l, s, r2 + ll);
         CHK(s, a, s, 0);
@@ -1092,8 +1098,9 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
-                v.qbp[SHARE_R - 1 - r] = WBPr[o + k - r]; v.qp[SHARE_R - 1 - r] = WP[o + k - r];
-                v.pbp[r] = WBPr[o + l - s + 1]; v.pp[r] = WP[o + l - s + 1];
+                const int2 wq = WBW[o + k - r], wp2 = WBW[o + l - s + 1];
+                v.qbp[SHARE_R - 1 - r] = wq.x; v.qp[SHARE_R - 1 - r] = wq.y;
+                v.pbp[r] = wp2.x; v.pp[r] = wp2.y;
                 v.qb[SHARE_R - 1 - r] = WBD(v.qbp[SHARE_R - 1 - r], s + r, o + k - r);
                 v.pb[r] = WBD(v.pbp[r], s + r, o + l - s + 1);
             }
