@@ -140,7 +140,7 @@ def main():
     tp = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tp) and a.n == 200 and a.seed == 5 and a.params == "Turner04":
         with open(tp) as f:
-            tk = json.load(f)["kernels"].get("k_level4d")
+            tk = json.load(f)["kernels"].get("k_level4d_level")
         if tk:
             traffic = tk["hbm_bytes_per_launch"]
 
@@ -177,7 +177,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                      "algorithmic_bytes_per_launch": bytes_lv / nlaunch,
-                     "kernel": "k_level4d (one level = k_level4d<false> + k_level4d<true> on the "
+                     "kernel": "k_level4d (one level = k_level4d + k_level4d_lead on the "
                                "split-sharing levels, concurrent; duration = the level's span)",
                      "launches_per_fold": nlaunch,
                      "avg_launch_us": avg_launch_s * 1e6, "algorithmic_bytes_per_fold": bytes_lv},

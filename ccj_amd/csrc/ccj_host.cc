@@ -111,8 +111,8 @@ struct ccj_ctx {
     std::vector<unsigned long long> h_pk;
     int8_t *d_vt = nullptr;
     hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr, st_il = nullptr, st_d = nullptr;
-    hipStream_t st_lead = nullptr;   // k_level4d<true>: split-point-sharing leaders of the level
-    std::vector<hipEvent_t> ld_done, pl_done;  // k_level4d<true>(t) / k_level4d<false>(t) finished
+    hipStream_t st_lead = nullptr;   // k_level4d_lead: split-point-sharing leaders of the level
+    std::vector<hipEvent_t> ld_done, pl_done;  // k_level4d_lead(t) / k_level4d(t) finished
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<double> lev_ms_v, diag_ms_v, il_ms_v;
     std::vector<hipEvent_t> il_done, dg_done;  // k_iloop(t) / k_diag2d(sigma) finished
@@ -1471,7 +1471,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     long long accC = 0;
     if (c->share && c->world == 1) {
         // the levels that run unsplit (the middle ones).  CCJ_SHARE_LATE=1 extends the range to
-        // the narrow late levels too, where k_level4d<true> splits the long scans
+        // the narrow late levels too, where k_level4d_lead splits the long scans
         // (ccjk_level4d_lead): measured 1.2 ms slower at n=200, so off by default
         g_lo = -1;
         for (int t = 0; t < c->nlev && g_lo < 0; ++t)

@@ -692,11 +692,8 @@ __device__ __forceinline__ void write_records(const DevTables &T, long long lr, 
 // windows are walked by source level dt (outer) so the level descriptor is loaded once per dt.
 // ------------------------------------------------------------------------------------------
 template <bool LEAD>
-__global__ __launch_bounds__(512)
-#ifdef CCJ_WAVES_EU
-__attribute__((amdgpu_waves_per_eu(CCJ_WAVES_EU, CCJ_WAVES_EU)))
-#endif
-void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end, int copies) {
+__device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wavesPerA, int split, int a_lo, int a_end,
+                                             int copies) {
 #ifdef CCJ_DEBUG_BOUNDS
     g_dbg_err = T.err;
 #endif
@@ -787,7 +784,7 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     const int arole = (grp && b >= SHARE_R - 1) ? (ra == 0 ? 1 : (t - ra >= T.g_lo ? 2 : 0)) : 0;
     const int brole = (grp && a >= SHARE_R - 1) ? (rb == 0 ? 1 : (t - rb >= T.g_lo ? 2 : 0)) : 0;
     // On sharing levels every wave with a long scan (a leader, or a full scan on either side) runs
-    // in its own launch (k_level4d<true>: more registers, scans split over several waves, side
+    // in its own launch (k_level4d_lead: more registers, scans split over several waves, side
     // stream); the plain kernel keeps the cells that only follow (short scans, full occupancy).
     if (grp && LEAD != (arole != 2 || brole != 2)) return;
     const int a_stop = arole == 2 ? ra : a;  // last split step this cell scans itself
@@ -1414,6 +1411,20 @@ void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end
     if (pm_ok) T.pmx[X.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = (int16_t)sPM;
 }
 
+// The two launches of a level (ccjk_level4d / ccjk_level4d_lead): the plain cells (short scans)
+// and, on the split-sharing levels, the long-scan cells with their larger register budget.
+__global__ __launch_bounds__(512)
+#ifdef CCJ_WAVES_EU
+__attribute__((amdgpu_waves_per_eu(CCJ_WAVES_EU, CCJ_WAVES_EU)))
+#endif
+void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end, int copies) {
+    level4d_body<false>(T, t, wavesPerA, split, a_lo, a_end, copies);
+}
+__global__ __launch_bounds__(512) void k_level4d_lead(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end,
+                                                      int copies) {
+    level4d_body<true>(T, t, wavesPerA, split, a_lo, a_end, copies);
+}
+
 // ------------------------------------------------------------------------------------------
 extern "C" int ccjk_init2d(const DevTables *T, void *stream) {
     const int total = (T->n + 1) * T->rs;
@@ -1533,7 +1544,7 @@ extern "C" int ccjk_level4d(const DevTables *T, int t, int a_lo, int a_end, int 
     const int cpb = threads / 64 / split;
     const long blocks = (waves + cpb - 1) / cpb;
     const size_t shmem = split > 1 ? (size_t)cpb * (split - 1) * 22 * 64 * sizeof(int) : 0;
-    hipLaunchKernelGGL(k_level4d<false>, dim3((unsigned)blocks), dim3(threads), shmem, (hipStream_t)stream, *T, t, wavesPerA, split, a_lo, a_end, copies);
+    hipLaunchKernelGGL(k_level4d, dim3((unsigned)blocks), dim3(threads), shmem, (hipStream_t)stream, *T, t, wavesPerA, split, a_lo, a_end, copies);
     return (int)hipGetLastError();
 }
 
@@ -1554,7 +1565,7 @@ extern "C" int ccjk_level4d_lead(const DevTables *T, int t, void *stream) {
     // narrow late levels: as many split waves as the plain heuristic would give the whole level
     const int sp = imax(lsplit, ccjk_level_split(T->n, t, 0, t + 1, T->split_target));
     const size_t shmem = sp > 1 ? (size_t)(sp - 1) * (LEAD_RED > 22 ? LEAD_RED : 22) * 64 * sizeof(int) : 0;
-    hipLaunchKernelGGL(k_level4d<true>, dim3((unsigned)waves), dim3(64 * sp), shmem, (hipStream_t)stream, *T, t, wavesPerA,
+    hipLaunchKernelGGL(k_level4d_lead, dim3((unsigned)waves), dim3(64 * sp), shmem, (hipStream_t)stream, *T, t, wavesPerA,
                        sp, 0, t + 1, 1);
     return (int)hipGetLastError();
 }

@@ -30,23 +30,24 @@ def pmc(path, counter):
             k = kname(r["Kernel_Name"])
             tot[k] += float(r["Counter_Value"]) * 1024.0  # KB -> bytes
             launches[k].add(r["Dispatch_Id"])
-            if k.startswith("k_level4d<"):
-                # one level = k_level4d<false> + (on sharing levels) k_level4d<true>: bytes summed,
-                # launches counted once per level
-                tot["k_level4d"] += float(r["Counter_Value"]) * 1024.0
-                if k == "k_level4d<false>":
-                    launches["k_level4d"].add(r["Dispatch_Id"])
+            if k == "k_level4d_lead":
+                # one level = k_level4d + (on sharing levels) k_level4d_lead: bytes summed under
+                # "k_level4d_level", launches counted once per level
+                tot["k_level4d_level"] += float(r["Counter_Value"]) * 1024.0
+            elif k == "k_level4d":
+                tot["k_level4d_level"] += float(r["Counter_Value"]) * 1024.0
+                launches["k_level4d_level"].add(r["Dispatch_Id"])
     return {k: (tot[k], len(launches[k])) for k in tot}
 
 
 def kname(full):
-    """'void k_level4d<false>(ccj::DevTables, ...)' -> 'k_level4d<false>'"""
+    """'void k_level4d(ccj::DevTables, ...)' -> 'k_level4d'"""
     return re.sub(r"^void ", "", full.split("(")[0]).strip()
 
 
 def level_spans(trace_csv):
-    """Per-level span of the level kernels from the kernel trace: each k_level4d<true> dispatch
-    runs beside the k_level4d<false> dispatch of the same level (they overlap in time); the level's
+    """Per-level span of the level kernels from the kernel trace: each k_level4d_lead dispatch
+    runs beside the k_level4d dispatch of the same level (they overlap in time); the level's
     span is first start to last end, the figure bench.py measures with HIP events on the level
     stream (roofline.avg_launch_us)."""
     plain, lead = [], []
@@ -54,9 +55,9 @@ def level_spans(trace_csv):
         for r in csv.DictReader(f):
             k = kname(r["Kernel_Name"])
             iv = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
-            if k == "k_level4d<false>":
+            if k == "k_level4d":
                 plain.append(iv)
-            elif k == "k_level4d<true>":
+            elif k == "k_level4d_lead":
                 lead.append(iv)
     plain.sort()
     lead.sort()
