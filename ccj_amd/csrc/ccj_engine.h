@@ -138,6 +138,11 @@ struct DevTables {
     // of wpl ints per array (WB, WBP, WP); partial-record ring of SHARE_R slots x SHARE_NACC x accC
     int split_target;              // k_level4d: narrow levels split loops so ~this many waves run (0: never)
     int g_lo, g_hi;
+    // k_level4d_lead walks only the long-scan a-blocks of a sharing level, longest scan first:
+    // lord[lord_off[t] .. lord_off[t+1]) (device), lord_off_h = the same offsets on the host
+    const int16_t *lord;
+    const int *lord_off;
+    const int *lord_off_h;
     int ws;
     long long wpl;
     int *wq, *wp;

@@ -94,6 +94,9 @@ struct ccj_ctx {
     uint4 *d_rec = nullptr;                  // AoS loop records
     int *d_wq = nullptr, *d_wp = nullptr;    // transposed WB/WBP/WP copies (split-point sharing)
     uint4 *d_acc = nullptr;                  // partial-record ring (split-point sharing)
+    int16_t *d_lord = nullptr;               // long-scan a-blocks per sharing level, longest first
+    int *d_lord_off = nullptr;
+    std::vector<int> lord_off;
     int2 *d_wbw = nullptr;                   // (WBP, WP) pairs [w][p]
     long long nrec = 0;
     long long nx = 0, npm = 0;
@@ -1488,6 +1491,35 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     }
     const int ws = n + 8;
     const long long wpl = (long long)(n + 2) * ws;
+    if (g_hi > g_lo && !(getenv("CCJ_LEAD_ORDER") && atoi(getenv("CCJ_LEAD_ORDER")) == 0)) {
+        // the a-blocks k_level4d_lead runs on each sharing level (a leader or a full scan on either
+        // side; the roles of level4d_body), ordered by scan cost, longest first, so the longest
+        // waves do not start last.  A leader step costs about 2.5 plain steps.
+        std::vector<int16_t> lord;
+        c->lord_off.assign((size_t)n + 1, 0);
+        std::vector<std::pair<double, int>> blk;
+        for (int t = 0; t < n; ++t) {
+            c->lord_off[t] = (int)lord.size();
+            if (t < g_lo || t >= g_hi) continue;
+            blk.clear();
+            for (int a = 0; a <= t; ++a) {
+                const int b = t - a, ra = a % SHARE_R, rb = b % SHARE_R;
+                const int ar = b >= SHARE_R - 1 ? (ra == 0 ? 1 : (t - ra >= g_lo ? 2 : 0)) : 0;
+                const int br = a >= SHARE_R - 1 ? (rb == 0 ? 1 : (t - rb >= g_lo ? 2 : 0)) : 0;
+                if (ar == 2 && br == 2) continue;
+                const double cost = (ar == 1 ? 2.5 : 1.0) * (ar == 2 ? ra : a) + (br == 1 ? 2.5 : 1.0) * (br == 2 ? rb : b);
+                blk.push_back({cost, a});
+            }
+            std::stable_sort(blk.begin(), blk.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
+            for (auto &e : blk) lord.push_back((int16_t)e.second);
+        }
+        c->lord_off[n] = (int)lord.size();
+        HIPCHK(cp, hipMalloc(&c->d_lord, std::max<size_t>(lord.size(), 1) * sizeof(int16_t)));
+        HIPCHK(cp, hipMalloc(&c->d_lord_off, c->lord_off.size() * sizeof(int)));
+        if (!lord.empty())
+            HIPCHK(cp, hipMemcpy(c->d_lord, lord.data(), lord.size() * sizeof(int16_t), hipMemcpyHostToDevice));
+        HIPCHK(cp, hipMemcpy(c->d_lord_off, c->lord_off.data(), c->lord_off.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
     if (g_hi > g_lo) {
         HIPCHK(cp, hipMalloc(&c->d_wq, 3 * wpl * sizeof(int)));
         HIPCHK(cp, hipMalloc(&c->d_wp, 3 * wpl * sizeof(int)));
@@ -1733,6 +1765,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.wq = c->d_wq;
     T.wp = c->d_wp;
     T.acc = c->d_acc;
+    T.lord = c->d_lord;
+    T.lord_off = c->d_lord_off;
+    T.lord_off_h = c->lord_off.empty() ? nullptr : c->lord_off.data();
     T.accC = accC;
     *out = c.release();
     return CCJ_OK;
@@ -2325,6 +2360,8 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_wq);
     hipFree(c->d_wp);
     hipFree(c->d_acc);
+    hipFree(c->d_lord);
+    hipFree(c->d_lord_off);
     hipFree(c->d_wbw);
     hipFree(c->pmx);
     hipFree(c->d_ldx);

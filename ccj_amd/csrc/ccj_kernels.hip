@@ -718,7 +718,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     const int a_raw = a_lo + a_rel;
     if (split == 1 && a_raw >= a_end) return;
     const bool wave_ok = a_raw < a_end;  // grid tail (split > 1 keeps the wave for the barrier)
-    const int a = wave_ok ? a_raw : a_end - 1;
+    int a = wave_ok ? a_raw : a_end - 1;
+    if (LEAD && T.lord) a = T.lord[T.lord_off[t] + a];  // leader launches: [a_lo, a_end) indexes the list
     const int chunk = wave_ok ? gw - a_rel * wavesPerA : 0;
     const int m = n - t - 2;
     const int Mt = (m * (m + 1)) >> 1;
@@ -1554,7 +1555,10 @@ extern "C" int ccjk_level4d_lead(const DevTables *T, int t, void *stream) {
     const int m = T->n - t - 2;
     const int Mt = m * (m + 1) / 2;
     const int wavesPerA = (Mt + 63) / 64;
-    const long waves = (long)(t + 1) * wavesPerA;
+    // only the long-scan a-blocks (T->lord, longest first) when the list is there
+    const int nblk = T->lord ? T->lord_off_h[t + 1] - T->lord_off_h[t] : t + 1;
+    if (nblk <= 0) return 0;
+    const long waves = (long)nblk * wavesPerA;
     // each leader chunk's scans are split over `split` waves of one workgroup (the barriers inside
     // the leader scans need every wave of the workgroup on the same chunk)
     static const int lsplit = [] {
@@ -1566,6 +1570,6 @@ extern "C" int ccjk_level4d_lead(const DevTables *T, int t, void *stream) {
     const int sp = imax(lsplit, ccjk_level_split(T->n, t, 0, t + 1, T->split_target));
     const size_t shmem = sp > 1 ? (size_t)(sp - 1) * (LEAD_RED > 22 ? LEAD_RED : 22) * 64 * sizeof(int) : 0;
     hipLaunchKernelGGL(k_level4d_lead, dim3((unsigned)waves), dim3(64 * sp), shmem, (hipStream_t)stream, *T, t, wavesPerA,
-                       sp, 0, t + 1, 1);
+                       sp, 0, nblk, 1);
     return (int)hipGetLastError();
 }
