@@ -336,6 +336,12 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
 // the P_P traceback its split (pseudo_loop.cc:867-896), without a rescan.  Needs PK levels
 // <= sigma-3 only, so it runs on a side stream three levels ahead of k_diag2d(sigma).
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long rdl64(unsigned long long v, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 constexpr int PT_WAVES = 4;  // waves per k_pterm workgroup = consecutive do values sharing jo
 
 __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngroups) {
@@ -349,10 +355,13 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
     const int dd0 = jo + 1 + ddc * PT_WAVES;
     if (dd0 > sigma - 2) return;  // whole workgroup
     const int dd = dd0 + w;
-    const int i = grp * 64 + lane + 1;
+    const int i0_ = grp * 64 + lane + 1;
+    const int i = i0_;
     // (value, key) of the first minimum in the reference's loop order, key = (jo*sigma + do)*sigma + ko
     unsigned long long best = ~0ull;
-    if (dd <= sigma - 2 && i + sigma <= n) {
+    // wave-uniform guard only: the readlane tables below need every lane; lanes past the last
+    // interval re-read the last one and drop their result
+    if (dd <= sigma - 2) {
         // PK(i, j, d+1, k): level jo+(ko-dd-1), a = jo, h = dd-jo-1, interval start i
         // PK(j+1, d, k+1, l): level (dd-jo-1)+(sigma-ko-1), a = dd-jo-1, h = ko-dd-1, start i+jo+1
         const int a1 = jo, h1 = dd - jo - 1, a2 = dd - jo - 1;
@@ -361,6 +370,8 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
         const LvlDev *__restrict__ LD = T.ld;
         const unsigned kbase = ((unsigned)jo * (unsigned)sigma + (unsigned)dd) * (unsigned)sigma;
         int bv = INF + 1, bk = 0;
+#ifdef CCJ_PTERM_SLOAD
+        const int i = imin(i0_, n - sigma);
 #pragma unroll 4
         for (int ko = dd + 1; ko < sigma; ++ko) {
             const int h2 = ko - dd - 1;
@@ -374,7 +385,40 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
                 bk = ko;
             }
         }
-        if (bv <= INF) best = ((unsigned long long)((unsigned)bv + 0x80000000u) << 32) | (kbase + (unsigned)bk);
+#else
+        // the row bases of both operands for 64 consecutive ko at a time, one per lane, fetched
+        // with readlane in the loop: no scalar descriptor load on the load chain
+        const unsigned ioff = 2u * (unsigned)imin(i, n - sigma);
+        for (int kb = dd + 1; kb < sigma; kb += 64) {
+            const int kl = imin(kb + lane, sigma - 1);
+            const int h2 = kl - dd - 1;
+            const int t1 = a1 + h2, t2 = a2 + (sigma - kl - 1);
+            const LvlDev L1 = LD[t1], L2 = LD[t2];
+            const long long o1 = L1.lb + PK * (long long)L1.C + a1 * L1.M + h1 * (n - t1 - 2) - g1 - 1;
+            const long long o2 = L2.lb + PK * (long long)L2.C + a2 * L2.M + h2 * (n - t2 - 2) - ((h2 * (h2 - 1)) >> 1) + jo;
+            const unsigned long long p1 = (unsigned long long)(D4 + o1), p2 = (unsigned long long)(D4 + o2);
+            const int cnt = imin(64, sigma - kb);
+            // 8 terms per batch: all 16 loads in flight before the first compare (entries past cnt
+            // re-read lane cnt-1's rows and are masked)
+            for (int x0 = 0; x0 < cnt; x0 += 8) {
+                int v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int x = imin(x0 + u, cnt - 1);
+                    const char *q1 = (const char *)rdl64(p1, x) + ioff, *q2 = (const char *)rdl64(p2, x) + ioff;
+                    v[u] = (int)*(const __attribute__((address_space(1))) int16_t *)q1 +
+                           (int)*(const __attribute__((address_space(1))) int16_t *)q2;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (x0 + u < cnt && v[u] < bv) {  // strict: keeps the first ko of the minimum
+                        bv = v[u];
+                        bk = kb + x0 + u;
+                    }
+            }
+        }
+#endif
+        if (bv <= INF && i0_ + sigma <= n) best = ((unsigned long long)((unsigned)bv + 0x80000000u) << 32) | (kbase + (unsigned)bk);
     }
     red[w][lane] = best;
     __syncthreads();
@@ -457,11 +501,6 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
 // IL_B entries are loaded together (one s_load burst), then IL_B partner values, then reduced.
 // Null tail entries (dt 63) hit T.dummy, so the last batch needs no masking (PL/PR: cnt is the
 // whole list; PM stops early and substitutes null entries).
-__device__ __forceinline__ unsigned long long rdl64(unsigned long long v, int l) {
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
-    return ((unsigned long long)hi << 32) | lo;
-}
 __device__ __forceinline__ int il_u1(uint32_t x) { return (int)((x >> 16) & 31u); }
 __device__ __forceinline__ int il_dt(uint32_t x) { return (int)(x >> 21); }
 __device__ __forceinline__ int il_e(uint32_t x) { return (int)(int16_t)(x & 0xffffu); }
