@@ -1473,13 +1473,14 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     int g_lo = 0, g_hi = 0;
     long long accC = 0;
     if (c->share && c->world == 1) {
-        // the levels that run unsplit (the middle ones).  CCJ_SHARE_LATE=1 extends the range to
-        // the narrow late levels too, where k_level4d_lead splits the long scans
-        // (ccjk_level4d_lead): measured 1.2 ms slower at n=200, so off by default
+        // from the first level that runs unsplit to the last level: the narrow early levels keep
+        // their split loops (short scans); on the narrow late levels k_level4d_lead splits the long
+        // scans like the level heuristic would (ccjk_level4d_lead).  CCJ_SHARE_LATE=0 limits
+        // sharing to the unsplit middle levels (measured 0.6 ms slower at n=200).
         g_lo = -1;
         for (int t = 0; t < c->nlev && g_lo < 0; ++t)
             if (ccjk_level_split(n, t, 0, t + 1, c->split_target) == 1) g_lo = t;
-        if (g_lo < 0 || !(getenv("CCJ_SHARE_LATE") && atoi(getenv("CCJ_SHARE_LATE")) == 1)) {
+        if (g_lo < 0 || (getenv("CCJ_SHARE_LATE") && atoi(getenv("CCJ_SHARE_LATE")) == 0)) {
             g_hi = g_lo < 0 ? 0 : g_lo;
             for (int t = std::max(g_lo, 0); g_lo >= 0 && t < c->nlev; ++t)
                 if (ccjk_level_split(n, t, 0, t + 1, c->split_target) == 1 && g_hi == t) g_hi = t + 1;
