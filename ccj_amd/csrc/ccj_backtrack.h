@@ -97,7 +97,7 @@ inline const char *bt_case_name(int type) {
 extern "C" {
 // One-workgroup kernels (ccj_backtrack.hip): W (W_final.cc:68-79) into W[0..n], then the whole
 // traceback into f_pair/f_type (h_struct.hh:9-19) and *out.  stack_cap = device stack entries.
-int ccjk_compute_W(const void *T, int *W, void *stream);
+int ccjk_compute_W(const void *T, int *W, int *S, void *stream);  // S: (n+1)*rs ints of scratch
 int ccjk_backtrack(const void *T, const int *W, int *f_pair, int8_t *f_type, ccj::BtOut *out, int stack_cap,
                    void *stream);
 }

@@ -148,24 +148,33 @@ __device__ int E_ext_Stem(const DV &H, int dangles, int vij, int vi1j, int vij1,
     return e;
 }
 
-// W_final.cc:68-79, one wave: W[j] for j ascending, the k-loop spread over the lanes
-__global__ __launch_bounds__(64) void k_compute_W(DevTables T, int *Wout) {
-    extern __shared__ int Ws[];
+// W_final.cc:68-79.  W[j] = min(W[j-1], min_k W[k-1] + S(k,j)) with
+//   S(k,j) = min(E_ext_Stem(V(k..j) ...), min(P(k,j), P(k+1,j), P(k,j-1), P(k+1,j-1)) + PS),
+// since the reference's two terms share the W[k-1] addend.  k_w_terms evaluates every S(k,j) in
+// parallel; k_compute_W then runs the recurrence in one wave, j ascending, k over the lanes.
+__global__ __launch_bounds__(256) void k_w_terms(DevTables T, int *S) {
     const int n = T.n;
     DV H{T, n, T.rs, nullptr, 0};
+    const int j = blockIdx.y + TURN + 1;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    if (j > n || k > j - TURN - 1) return;
+    const int e2 = E_ext_Stem(H, T.dangles, H.V(k, j), H.V(k + 1, j), H.V(k, j - 1), H.V(k + 1, j - 1), k, j);
+    const int e3 = imin(imin(H.Pg(k, j), H.Pg(k + 1, j)), imin(H.Pg(k, j - 1), H.Pg(k + 1, j - 1))) + T.pen.PS;
+    S[(size_t)j * T.rs + k] = imin(e2, e3);
+}
+
+__global__ __launch_bounds__(64) void k_compute_W(DevTables T, const int *S, int *Wout) {
+    extern __shared__ int Ws[];
+    const int n = T.n;
     for (int j = lane_id(); j <= n; j += 64) Ws[j] = 0;
     __syncthreads();
     for (int j = TURN + 1; j <= n; ++j) {
-        int m2 = INF, m3 = INF;
-        for (int k = 1 + lane_id(); k <= j - TURN - 1; k += 64) {
-            const int acc = (k > 1) ? Ws[k - 1] : 0;
-            m2 = imin(m2, acc + E_ext_Stem(H, T.dangles, H.V(k, j), H.V(k + 1, j), H.V(k, j - 1), H.V(k + 1, j - 1), k, j));
-            m3 = imin(m3, acc + imin(imin(H.Pg(k, j), H.Pg(k + 1, j)), imin(H.Pg(k, j - 1), H.Pg(k + 1, j - 1))) + T.pen.PS);
-        }
+        const int *Sj = S + (size_t)j * T.rs;
+        int m = INF;
+        for (int k = 1 + lane_id(); k <= j - TURN - 1; k += 64) m = imin(m, ((k > 1) ? Ws[k - 1] : 0) + Sj[k]);
         int x = 0;
-        wreduce(m2, x);
-        wreduce(m3, x);
-        if (lane_id() == 0) Ws[j] = imin(Ws[j - 1], imin(m2, m3));
+        wreduce(m, x);
+        if (lane_id() == 0) Ws[j] = imin(Ws[j - 1], m);
         __syncthreads();
     }
     for (int j = lane_id(); j <= n; j += 64) Wout[j] = Ws[j];
@@ -1077,9 +1086,16 @@ __global__ __launch_bounds__(64) void k_backtrack(DevTables T, const int *W, int
 
 }  // namespace
 
-extern "C" int ccjk_compute_W(const void *Tv, int *W, void *stream) {
+extern "C" int ccjk_compute_W(const void *Tv, int *W, int *S, void *stream) {
     const DevTables *T = (const DevTables *)Tv;
-    hipLaunchKernelGGL(k_compute_W, dim3(1), dim3(64), (T->n + 1) * sizeof(int), (hipStream_t)stream, *T, W);
+    const int n = T->n;
+    if (n > TURN) {
+        hipLaunchKernelGGL(k_w_terms, dim3((unsigned)((n + 255) / 256), (unsigned)(n - TURN)), dim3(256), 0,
+                           (hipStream_t)stream, *T, S);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+    }
+    hipLaunchKernelGGL(k_compute_W, dim3(1), dim3(64), (n + 1) * sizeof(int), (hipStream_t)stream, *T, S, W);
     return (int)hipGetLastError();
 }
 

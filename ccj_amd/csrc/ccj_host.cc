@@ -109,6 +109,7 @@ struct ccj_ctx {
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
     unsigned long long *d_pk = nullptr;  // P with its first split (k_pterm), [w][p]
     int *d_W = nullptr, *d_fpair = nullptr;  // device traceback outputs
+    int *d_wterm = nullptr;                  // W's (k, j) terms [j][k] (ccjk_compute_W scratch)
     int8_t *d_ftype = nullptr;
     BtOut *d_btout = nullptr;
     std::vector<unsigned long long> h_pk;
@@ -1577,6 +1578,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipMalloc(&c->d_wbw, plane * sizeof(int2)));
     HIPCHK(cp, hipMalloc(&c->d_pk, plane * sizeof(unsigned long long)));
     HIPCHK(cp, hipMalloc(&c->d_W, (n + 1) * sizeof(int)));
+    HIPCHK(cp, hipMalloc(&c->d_wterm, plane * sizeof(int)));
     HIPCHK(cp, hipMalloc(&c->d_fpair, (n + 1) * sizeof(int)));
     HIPCHK(cp, hipMalloc(&c->d_ftype, (n + 1)));
     HIPCHK(cp, hipMalloc(&c->d_btout, sizeof(BtOut)));
@@ -2001,7 +2003,7 @@ int device_result(ccj_ctx *c, std::string &structure, std::string &out) {
     const auto t0 = std::chrono::steady_clock::now();
     const int n = c->n;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, (hipError_t)ccjk_compute_W(&c->T, c->d_W, c->st));
+    HIPCHK(c, (hipError_t)ccjk_compute_W(&c->T, c->d_W, c->d_wterm, c->st));
     const int cap = std::min(4 * n + 64, 3000);
     HIPCHK(c, (hipError_t)ccjk_backtrack(&c->T, c->d_W, c->d_fpair, c->d_ftype, c->d_btout, cap, c->st));
     BtOut bo{};
@@ -2361,6 +2363,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_wq);
     hipFree(c->d_wp);
     hipFree(c->d_acc);
+    hipFree(c->d_wterm);
     hipFree(c->d_lord);
     hipFree(c->d_lord_off);
     hipFree(c->d_wbw);
