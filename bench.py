@@ -3,9 +3,11 @@
 
 One "step" = one complete CCJ MFE fold of the 200-nt synthetic RNA (random.Random(5), ACGU) with
 rna_Turner04 tables and dangles 2: GPU fill of all 22 four-dimensional gap matrices and the
-2-D matrices, the host mirror (levels streamed D2H while later levels compute), exterior W,
-backtrack and bracket emission — everything W_final::ccj() does in the reference.  Inputs are
-resident in HBM/host memory before the timed region (the context is created during setup).
+2-D matrices, exterior W, traceback and bracket emission (on the GPU; the structure string and
+MFE are copied back) — everything W_final::ccj() does in the reference.  Inputs are resident in
+HBM before the timed region (the context is created during setup).  Every ccj() call returns
+only after all of its streams are synchronized, so the barrier + wall clock around the K steps
+brackets finished GPU work (the engine's own stream sync plays the role of a device sync).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
