@@ -73,16 +73,14 @@ enum RecType { RA = 0, RK = 1, RL = 2, NREC = 3 };
 //   AL (l side): PRmloop00 PRmloop01 | PMmloop01 POmloop00 | POmloop01 PMmloop10 | POmloop10 PfromR
 // (AK's 7th slot carries the l side's 9th field; it is written by the l-side leader, the first six
 // by the k-side leader, so the two never write the same bytes.)  Values are min-clamped at 32767
-// like a store (clamp commutes with min).  The leader's W(i-r, .) / W(., j+r) operands come from
-// two transposed copies of WB/WBP/WP (wq: row q, p contiguous; wp: row p, q contiguous), one
-// SHARE_R-wide vector load per array.
+// like a store (clamp commutes with min).  The leader's W(i-r, .) / W(., j+r) operands are read
+// from the span-major WBW pairs (span s-1+r, coalesced along the lanes).
 #ifndef CCJ_SHARE_R
 #define CCJ_SHARE_R 4
 #endif
 constexpr int SHARE_R = CCJ_SHARE_R;
 constexpr int SHARE_NACC = 4;
 enum AccRec { AI = 0, AJ = 1, AK = 2, AL = 3 };
-constexpr int WQ_OFF = 4;  // wq column of p is p + WQ_OFF (p >= 1-SHARE_R+1)
 
 struct LvlX {        // per-level bases of the interior-loop copies
     long long lbx;  // element offset of level t in d4x: PLx (C_t elements) then PRx (C_t)
@@ -134,8 +132,8 @@ struct DevTables {
     const uint32_t *items;         // k_iloop work items (role << 30 | f1 << 20 | f2 << 10 | chunk)
     uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
     int *err;                      // device error word
-    // split-point sharing (above): levels [g_lo, g_hi) share; W copies of row stride ws, one plane
-    // of wpl ints per array (WB, WBP, WP); partial-record ring of SHARE_R slots x SHARE_NACC x accC
+    // split-point sharing (above): levels [g_lo, g_hi) share; partial-record ring of SHARE_R
+    // slots x SHARE_NACC x accC
     int split_target;              // k_level4d: narrow levels split loops so ~this many waves run (0: never)
     int g_lo, g_hi;
     // k_level4d_lead walks only the long-scan a-blocks of a sharing level, longest scan first:
@@ -143,9 +141,6 @@ struct DevTables {
     const int16_t *lord;
     const int *lord_off;
     const int *lord_off_h;
-    int ws;
-    long long wpl;
-    int *wq, *wp;
     uint4 *acc;
     long long accC;
 };

@@ -92,7 +92,6 @@ struct ccj_ctx {
     LvlDev *d_ld = nullptr;
     int16_t *d4x = nullptr, *pmx = nullptr;  // interior-loop copies of PL/PR and PM
     uint4 *d_rec = nullptr;                  // AoS loop records
-    int *d_wq = nullptr, *d_wp = nullptr;    // transposed WB/WBP/WP copies (split-point sharing)
     uint4 *d_acc = nullptr;                  // partial-record ring (split-point sharing)
     int16_t *d_lord = nullptr;               // long-scan a-blocks per sharing level, longest first
     int *d_lord_off = nullptr;
@@ -1470,7 +1469,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     if (c->nrec > 0 && hipMalloc(&c->d_rec, (size_t)c->nrec * sizeof(uint4)) != hipSuccess)
         return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for loop records failed", c->nrec * 16e-9);
     // split-point sharing: the level range it covers (every level of it runs unsplit, so each leader
-    // and its followers run one cell per lane), the transposed W copies and the partial-record ring
+    // and its followers run one cell per lane) and the partial-record ring
     int g_lo = 0, g_hi = 0;
     long long accC = 0;
     if (c->share && c->world == 1) {
@@ -1491,8 +1490,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         }
         for (int t = g_lo; t < g_hi; ++t) accC = std::max<long long>(accC, c->lv_host[t].C);
     }
-    const int ws = n + 8;
-    const long long wpl = (long long)(n + 2) * ws;
     if (g_hi > g_lo && !(getenv("CCJ_LEAD_ORDER") && atoi(getenv("CCJ_LEAD_ORDER")) == 0)) {
         // the a-blocks k_level4d_lead runs on each sharing level (a leader or a full scan on either
         // side; the roles of level4d_body), ordered by scan cost, longest first, so the longest
@@ -1523,10 +1520,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         HIPCHK(cp, hipMemcpy(c->d_lord_off, c->lord_off.data(), c->lord_off.size() * sizeof(int), hipMemcpyHostToDevice));
     }
     if (g_hi > g_lo) {
-        HIPCHK(cp, hipMalloc(&c->d_wq, 3 * wpl * sizeof(int)));
-        HIPCHK(cp, hipMalloc(&c->d_wp, 3 * wpl * sizeof(int)));
-        HIPCHK(cp, hipMemset(c->d_wq, 0, 3 * wpl * sizeof(int)));
-        HIPCHK(cp, hipMemset(c->d_wp, 0, 3 * wpl * sizeof(int)));
         if (hipMalloc(&c->d_acc, (size_t)SHARE_R * SHARE_NACC * accC * sizeof(uint4)) != hipSuccess)
             return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for split-sharing records failed",
                            SHARE_R * SHARE_NACC * accC * 16e-9);
@@ -1763,10 +1756,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.split_target = c->split_target;
     T.g_lo = g_lo;
     T.g_hi = g_hi;
-    T.ws = ws;
-    T.wpl = wpl;
-    T.wq = c->d_wq;
-    T.wp = c->d_wp;
     T.acc = c->d_acc;
     T.lord = c->d_lord;
     T.lord_off = c->d_lord_off;
@@ -2360,8 +2349,6 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_ld);
     hipFree(c->d4x);
     hipFree(c->d_rec);
-    hipFree(c->d_wq);
-    hipFree(c->d_wp);
     hipFree(c->d_acc);
     hipFree(c->d_wterm);
     hipFree(c->d_lord);

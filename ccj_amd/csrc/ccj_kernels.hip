@@ -291,12 +291,6 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
             if (m < INF / 2) { wpp = m; T.WPP[cell] = m; }
             T.WP[cell] = imin(pe.PUP * (sigma + 1), wpp);
             T.WBW[cell] = make_int2(wbp, T.WP[cell]);  // the pair the level loops load
-            if (T.wq) {  // transposed copies for the split-point-sharing leaders of k_level4d
-                const long long q0 = (long long)l * T.ws + i + WQ_OFF, p0 = (long long)i * T.ws + l;
-                const int wb = imin(pe.cp * (sigma + 1), wbp), wp = imin(pe.PUP * (sigma + 1), wpp);
-                T.wq[q0] = wb; T.wq[T.wpl + q0] = wbp; T.wq[2 * T.wpl + q0] = wp;
-                T.wp[p0] = wb; T.wp[T.wpl + p0] = wbp; T.wp[2 * T.wpl + p0] = wp;
-            }
         }
     }
 
@@ -689,13 +683,8 @@ __device__ __forceinline__ int hi16(unsigned w) { return (int)w >> 16; }
 // ints per lane a leader's split wave hands to part 0: the follower slices of one side
 constexpr int LEAD_RED = 15 * (SHARE_R - 1);
 
-// split-point sharing (ccj_engine.h): SHARE_R consecutive W values of one transposed-copy row
+// split-point sharing (ccj_engine.h): the SHARE_R W values of one split step, one per follower
 typedef int wv_t __attribute__((ext_vector_type(SHARE_R)));
-__device__ __forceinline__ wv_t ldw(const int *p) {
-    wv_t v;
-    __builtin_memcpy(&v, p, sizeof(v));  // 4-byte aligned: one dwordx4 (R = 4) in unaligned-access mode
-    return v;
-}
 // partial record: up to 7 int16 fields (min-clamped like a store), slot 7 = 32767
 __device__ __forceinline__ uint4 pack_acc(const int *f, int nf) {
     int c[8];
@@ -829,8 +818,6 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     if (grp && LEAD != (arole != 2 || brole != 2)) return;
     const int a_stop = arole == 2 ? ra : a;  // last split step this cell scans itself
     const int b_stop = brole == 2 ? rb : b;
-    const int ws = T.ws;
-    const long long wpl = T.wpl;
 
     // ---- fused a-loop: split point d inside [i, j] ----
     int pLm00 = INTERN_INF + bp, pLm01 = INF, pLm10 = INF, pMm00 = INTERN_INF + bp, pMm10 = INF;
@@ -904,12 +891,6 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             CHKR(L.lr + (unsigned)Uj + L0);
             v.wi = rp[(unsigned)Ui + lh];
             v.wj = rp[(unsigned)Uj + L0];
-#ifdef CCJ_SHARE_WVEC
-            const int *q = T.wq + (i + s - 1) * ws + (i - SHARE_R + 1 + WQ_OFF);  // W(i-r, i+s-1), r = R-1..0
-            const int *p = T.wp + (j - s + 1) * ws + j;                          // W(j-s+1, j+r), r = 0..R-1
-            v.qb = ldw(q); v.qbp = ldw(q + wpl); v.qp = ldw(q + 2 * wpl);
-            v.pb = ldw(p); v.pbp = ldw(p + wpl); v.pp = ldw(p + 2 * wpl);
-#else
             // span-major rows: W(i-r, i+s-1) and W(j-s+1, j+r) have span s-1+r, coalesced along the lanes
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
@@ -920,7 +901,6 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 v.qb[SHARE_R - 1 - r] = WBD(v.qbp[SHARE_R - 1 - r], s + r, o + i - r);
                 v.pb[r] = WBD(v.pbp[r], s + r, o + j - s + 1);
             }
-#endif
             return v;
         };
         auto st = [&](const LA &v, int mask) {
@@ -1126,12 +1106,6 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             CHKR(L.lr + 2 * L.C + (unsigned)Ul + lh);
             v.wk = rp[(unsigned)(L.C + Uk) + L0];
             v.wl = rp[(unsigned)(2 * L.C + Ul) + lh];
-#ifdef CCJ_SHARE_WVEC
-            const int *q = T.wq + (k + s - 1) * ws + (k - SHARE_R + 1 + WQ_OFF);  // W(k-r, k+s-1), r = R-1..0
-            const int *p = T.wp + (l - s + 1) * ws + l;                          // W(l-s+1, l+r), r = 0..R-1
-            v.qb = ldw(q); v.qbp = ldw(q + wpl); v.qp = ldw(q + 2 * wpl);
-            v.pb = ldw(p); v.pbp = ldw(p + wpl); v.pp = ldw(p + 2 * wpl);
-#else
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
@@ -1141,7 +1115,6 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 v.qb[SHARE_R - 1 - r] = WBD(v.qbp[SHARE_R - 1 - r], s + r, o + k - r);
                 v.pb[r] = WBD(v.pbp[r], s + r, o + l - s + 1);
             }
-#endif
             return v;
         };
         auto st = [&](const LB &v, int mask) {
