@@ -574,6 +574,99 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
     return b1;
 }
 
+// The same minimum for a wave whose row has at most 32 cells: the wave is G groups of 64/G lanes,
+// each group holding the whole row and walking every G-th list entry (entry e0+g+G*u), so the list
+// takes 1/G of the iterations; the groups are min-reduced at the end (lanes l, l+64/G, ...).  The
+// entry is per lane here, so the A/B tables are read with ds_bpermute instead of readlane.  All 64
+// lanes run the scan (bpermute sources must be live).
+__device__ __forceinline__ int bperm(int v, int l) { return __builtin_amdgcn_ds_bpermute(l << 2, v); }
+
+#ifndef CCJ_ILG_B
+#define CCJ_ILG_B 4
+#endif
+constexpr int ILG_B = CCJ_ILG_B;  // entries per lane per batch in the grouped walk (registers: 8 waves/SIMD)
+template <bool CROSS, bool PMWIN>
+__device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__restrict__ ent, int cnt, unsigned long long Atab, int Btab,
+                                         unsigned lofs2, int as, int bs, int G, int g) {
+    int b1 = INF;
+    if (cnt <= 0) return b1;
+    const int alo = (int)(unsigned)Atab, ahi = (int)(unsigned)(Atab >> 32);
+    // only the packed word is loaded (the cross term 2*u1*dt is recomputed): half the registers
+    const uint32_t nul = (63u << 21) | (uint32_t)INTERN_INF;
+    auto fetch = [&](int e0, uint32_t *E) {
+#pragma unroll
+        for (int u = 0; u < ILG_B; ++u) {
+            const int e = e0 + g + G * u;
+            E[u] = ent[imin(e, cnt - 1)].x;
+            if (e >= cnt) E[u] = nul;
+        }
+    };
+    auto issue = [&](const uint32_t *E, int *v) {
+#pragma unroll
+        for (int u = 0; u < ILG_B; ++u) {
+            const int dt = il_dt(E[u]), u1 = il_u1(E[u]);
+            unsigned off = (unsigned)bperm(Btab, u1);
+            if (CROSS) off += (unsigned)(2 * u1 * dt);
+            const unsigned long long A = ((unsigned long long)(unsigned)bperm(ahi, dt) << 32) | (unsigned)bperm(alo, dt);
+#ifdef CCJ_DEBUG_BOUNDS
+            {
+                const int16_t *q = (const int16_t *)((const char *)(A + off) + lofs2);
+                const bool in = (q >= T.d4x && q < T.d4x + T.nx) || (q >= T.pmx && q < T.pmx + T.npm) ||
+                                (q >= T.dummy && q < T.dummy + T.n + 64);
+                if (!in || (dt != 63 && (dt < 2 || dt > 2 * MAXLOOP - 2))) {
+                    if (atomicOr(T.err, 64) == 0) printf("k_iloop (grouped, G %d) OOB: dt %d u1 %d\n", G, dt, u1);
+                    v[u] = 0;
+                    continue;
+                }
+            }
+#endif
+            v[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)(A + off) + lofs2);
+        }
+    };
+    auto reduce = [&](const uint32_t *E, const int *v) {
+#pragma unroll
+        for (int u = 0; u < ILG_B; ++u) {
+            const int c = il_e(E[u]) + v[u];
+            if (PMWIN) {
+                const int u1 = il_u1(E[u]), u2 = il_dt(E[u]) - 2 - u1;
+                b1 = imin(b1, (u1 <= as - 2 && u2 <= bs - 2) ? c : INF);
+            } else {
+                b1 = imin(b1, c);
+            }
+        }
+    };
+    uint32_t E[ILG_B];
+    int v[ILG_B];
+    const int stepE = G * ILG_B;
+    fetch(0, E);
+    issue(E, v);
+#pragma unroll 1
+    for (int e0 = stepE; e0 < cnt; e0 += stepE) {
+        uint32_t En[ILG_B];
+        int vn[ILG_B];
+        fetch(e0, En);
+        issue(En, vn);
+        reduce(E, v);
+#pragma unroll
+        for (int u = 0; u < ILG_B; ++u) {
+            E[u] = En[u];
+            v[u] = vn[u];
+        }
+    }
+    reduce(E, v);
+    for (int off = 64 / G; off < 64; off <<= 1) b1 = imin(b1, __shfl_xor(b1, off));
+    return b1;
+}
+
+// lanes per group for a row of nact cells: 64 (one group, scalar list walk) above 32 cells
+__device__ __forceinline__ int il_groups(int nact) {
+#ifdef CCJ_IL_NOPACK
+    return 1;
+#else
+    return nact <= 8 ? 8 : nact <= 16 ? 4 : nact <= 32 ? 2 : 1;
+#endif
+}
+
 // one wave per work item (host-built list for level t: closing pairs that can pair, heaviest first)
 __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long first, int nitems, int a_lo, int a_end) {
     const int n = T.n, rs = T.rs, m = n - t - 2;
@@ -590,7 +683,8 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
     if (role == 0) {
         // PL: wave = (a, i, h-chunk), lanes h; closing pair (i, j)
         const int a = f1, i = f2;
-        const int h = zc * 64 + lane;
+        const int G = il_groups(imin(64, m - i - zc * 64 + 1)), gq = lane / (64 / G);
+        const int h = zc * 64 + (lane & (64 / G - 1));
         const bool act = h <= m - i;
         const unsigned lofs2 = 2u * (unsigned)(act ? h : m - i);  // idle lanes re-read a valid cell
         const size_t pidx = (size_t)a * rs + i;
@@ -605,20 +699,24 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
         if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
         const int e0 = (int)T.ilseg[pidx * IL_SEG + 3];
-        const int b1 = il_scan<true, false>(T, T.il + pidx * IL_CAP + e0, (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0, Atab, Btab, lofs2, 0, 0);
+        const uint2 *le = T.il + pidx * IL_CAP + e0;
+        const int lc = (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0;
+        const int b1 = G == 1 ? il_scan<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0)
+                              : il_scan_g<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, gq);
 #ifdef CCJ_DEBUG_BOUNDS
         if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
             atomicOr(T.err, 128);
             return;
         }
 #endif
-        if (act) T.d4[Lt.lb + (long long)PL * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
+        if (act && gq == 0) T.d4[Lt.lb + (long long)PL * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
     } else if (role == 1) {
         // PR: wave = (a, q, i-chunk), lanes i; closing pair (k, l), q = i+h-1 = k-a-3
         const int a = f1, q = f2;
         const int b = t - a;
         const int k = q + a + 3;
-        const int i = zc * 64 + lane + 1;
+        const int G = il_groups(imin(64, q + 1 - zc * 64)), gq = lane / (64 / G);
+        const int i = zc * 64 + (lane & (64 / G - 1)) + 1;
         const bool act = i <= q + 1;
         const unsigned lofs2 = 2u * (unsigned)((act ? i : q + 1) - 1);
         const int h = q + 1 - i;
@@ -631,20 +729,24 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
         if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
         const int e0 = (int)T.ilseg[pidx * IL_SEG + 3];
-        const int b1 = il_scan<false, false>(T, T.il + pidx * IL_CAP + e0, (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0, Atab, Btab, lofs2, 0, 0);
+        const uint2 *le = T.il + pidx * IL_CAP + e0;
+        const int lc = (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0;
+        const int b1 = G == 1 ? il_scan<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0)
+                              : il_scan_g<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, gq);
 #ifdef CCJ_DEBUG_BOUNDS
         if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
             atomicOr(T.err, 128);
             return;
         }
 #endif
-        if (act) T.d4[Lt.lb + (long long)PR * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
+        if (act && gq == 0) T.d4[Lt.lb + (long long)PR * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
     } else {
         // PM: wave = (h, j, a-chunk), lanes a; pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
         const int h = f1, j = f2;
         const int g = h + 2, k = j + g;
         const int alo = imax(imax(2, t - (n - k)), a_lo), ahi = imin(imin(t - 2, j - 1), a_end - 1);
-        const int a = alo + zc * 64 + lane;
+        const int G = il_groups(imin(64, ahi - alo - zc * 64 + 1)), gq = lane / (64 / G);
+        const int a = alo + zc * 64 + (lane & (64 / G - 1));
         const bool act = a <= ahi;
         const int as = act ? a : ahi;
         const unsigned lofs2 = 2u * (unsigned)as;
@@ -663,14 +765,16 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         // entries with dt > t-2 fit no cell of this level
         const int cnt = (int)T.ilmseg[pidx * IL_SEG + imin(t - 1, IL_SEG - 1)];
         const int e0 = (int)T.ilmseg[pidx * IL_SEG + 3];
-        const int b1 = il_scan<true, true>(T, T.ilm + pidx * IL_CAP + e0, cnt - e0, Atab, Btab, lofs2, as, t - as);
+        const uint2 *le = T.ilm + pidx * IL_CAP + e0;
+        const int b1 = G == 1 ? il_scan<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as)
+                              : il_scan_g<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, G, gq);
 #ifdef CCJ_DEBUG_BOUNDS
         if (act && (a < 0 || a > t || h < 0 || h >= m || (j - a) < 1 || (j - a) > m - h)) {
             atomicOr(T.err, 128);
             return;
         }
 #endif
-        if (act) T.d4[Lt.lb + (long long)PM * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + (j - a) - 1] = (int16_t)clamp_store(b1);
+        if (act && gq == 0) T.d4[Lt.lb + (long long)PM * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + (j - a) - 1] = (int16_t)clamp_store(b1);
     }
 }
 
