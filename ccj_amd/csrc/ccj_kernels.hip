@@ -574,9 +574,10 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
     return b1;
 }
 
-// The same minimum for a wave whose row has at most 32 cells: the wave is G groups of 64/G lanes,
-// each group holding the whole row and walking every G-th list entry (entry e0+g+G*u), so the list
-// takes 1/G of the iterations; the groups are min-reduced at the end (lanes l, l+64/G, ...).  The
+// The same minimum for a wave whose row has at most 32 cells: the wave is G groups of W lanes
+// (il_groups), each group holding the whole row and walking every G-th list entry (entry
+// e0+g+G*u), so the list takes 1/G of the iterations; the groups are min-reduced at the end
+// (lanes rl, rl+W, ..., rl+(G-1)W; rl unused with power-of-two W).  The
 // entry is per lane here, so the A/B tables are read with ds_bpermute instead of readlane.  All 64
 // lanes run the scan (bpermute sources must be live).
 __device__ __forceinline__ int bperm(int v, int l) { return __builtin_amdgcn_ds_bpermute(l << 2, v); }
@@ -587,7 +588,7 @@ __device__ __forceinline__ int bperm(int v, int l) { return __builtin_amdgcn_ds_
 constexpr int ILG_B = CCJ_ILG_B;  // entries per lane per batch in the grouped walk (registers: 8 waves/SIMD)
 template <bool CROSS, bool PMWIN>
 __device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__restrict__ ent, int cnt, unsigned long long Atab, int Btab,
-                                         unsigned lofs2, int as, int bs, int G, int g) {
+                                         unsigned lofs2, int as, int bs, int G, int W, int g, int rl) {
     int b1 = INF;
     if (cnt <= 0) return b1;
     const int alo = (int)(unsigned)Atab, ahi = (int)(unsigned)(Atab >> 32);
@@ -654,17 +655,21 @@ __device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__rest
         }
     }
     reduce(E, v);
-    for (int off = 64 / G; off < 64; off <<= 1) b1 = imin(b1, __shfl_xor(b1, off));
+    for (int off = W; off < 64; off <<= 1) b1 = imin(b1, __shfl_xor(b1, off));
     return b1;
 }
 
-// lanes per group for a row of nact cells: 64 (one group, scalar list walk) above 32 cells
-__device__ __forceinline__ int il_groups(int nact) {
+// Lane groups for a row of nact cells: W lanes per group (one per cell, W >= nact, a power of two
+// >= 8), G = 64/W groups; lane = gq*W + rl.  Rows above 32 cells keep one group (the scalar list
+// walk).  (Groups of exactly nact lanes, W not a power of two, measured the same.)
+struct ILGroups { int G, W, gq, rl; };
+__device__ __forceinline__ ILGroups il_groups(int nact, int lane) {
 #ifdef CCJ_IL_NOPACK
-    return 1;
+    const int W = 64;
 #else
-    return nact <= 8 ? 8 : nact <= 16 ? 4 : nact <= 32 ? 2 : 1;
+    const int W = nact > 32 ? 64 : nact > 16 ? 32 : nact > 8 ? 16 : 8;
 #endif
+    return {64 / W, W, lane / W, lane & (W - 1)};
 }
 
 // one wave per work item (host-built list for level t: closing pairs that can pair, heaviest first)
@@ -683,8 +688,9 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
     if (role == 0) {
         // PL: wave = (a, i, h-chunk), lanes h; closing pair (i, j)
         const int a = f1, i = f2;
-        const int G = il_groups(imin(64, m - i - zc * 64 + 1)), gq = lane / (64 / G);
-        const int h = zc * 64 + (lane & (64 / G - 1));
+        const ILGroups lg = il_groups(imin(64, m - i - zc * 64 + 1), lane);
+        const int G = lg.G, gq = lg.gq;
+        const int h = zc * 64 + lg.rl;
         const bool act = h <= m - i;
         const unsigned lofs2 = 2u * (unsigned)(act ? h : m - i);  // idle lanes re-read a valid cell
         const size_t pidx = (size_t)a * rs + i;
@@ -702,7 +708,7 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         const uint2 *le = T.il + pidx * IL_CAP + e0;
         const int lc = (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0;
         const int b1 = G == 1 ? il_scan<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0)
-                              : il_scan_g<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, gq);
+                              : il_scan_g<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl);
 #ifdef CCJ_DEBUG_BOUNDS
         if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
             atomicOr(T.err, 128);
@@ -715,8 +721,9 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         const int a = f1, q = f2;
         const int b = t - a;
         const int k = q + a + 3;
-        const int G = il_groups(imin(64, q + 1 - zc * 64)), gq = lane / (64 / G);
-        const int i = zc * 64 + (lane & (64 / G - 1)) + 1;
+        const ILGroups lg = il_groups(imin(64, q + 1 - zc * 64), lane);
+        const int G = lg.G, gq = lg.gq;
+        const int i = zc * 64 + lg.rl + 1;
         const bool act = i <= q + 1;
         const unsigned lofs2 = 2u * (unsigned)((act ? i : q + 1) - 1);
         const int h = q + 1 - i;
@@ -732,7 +739,7 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         const uint2 *le = T.il + pidx * IL_CAP + e0;
         const int lc = (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0;
         const int b1 = G == 1 ? il_scan<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0)
-                              : il_scan_g<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, gq);
+                              : il_scan_g<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl);
 #ifdef CCJ_DEBUG_BOUNDS
         if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
             atomicOr(T.err, 128);
@@ -745,8 +752,9 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         const int h = f1, j = f2;
         const int g = h + 2, k = j + g;
         const int alo = imax(imax(2, t - (n - k)), a_lo), ahi = imin(imin(t - 2, j - 1), a_end - 1);
-        const int G = il_groups(imin(64, ahi - alo - zc * 64 + 1)), gq = lane / (64 / G);
-        const int a = alo + zc * 64 + (lane & (64 / G - 1));
+        const ILGroups lg = il_groups(imin(64, ahi - alo - zc * 64 + 1), lane);
+        const int G = lg.G, gq = lg.gq;
+        const int a = alo + zc * 64 + lg.rl;
         const bool act = a <= ahi;
         const int as = act ? a : ahi;
         const unsigned lofs2 = 2u * (unsigned)as;
@@ -767,7 +775,7 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         const int e0 = (int)T.ilmseg[pidx * IL_SEG + 3];
         const uint2 *le = T.ilm + pidx * IL_CAP + e0;
         const int b1 = G == 1 ? il_scan<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as)
-                              : il_scan_g<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, G, gq);
+                              : il_scan_g<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl);
 #ifdef CCJ_DEBUG_BOUNDS
         if (act && (a < 0 || a > t || h < 0 || h >= m || (j - a) < 1 || (j - a) > m - h)) {
             atomicOr(T.err, 128);
