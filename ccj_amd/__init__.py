@@ -118,6 +118,8 @@ def lib() -> ctypes.CDLL:
     L.ccj_host_timing.restype = ip
     L.ccj_iloop_ms.argtypes = [vp]
     L.ccj_iloop_ms.restype = ctypes.c_double
+    L.ccj_set_timing.argtypes = [vp, ip]
+    L.ccj_set_timing.restype = ip
     L.ccj_comm_unique_id.argtypes = [cp]
     L.ccj_comm_unique_id.restype = ip
     L.ccj_comm_init.argtypes = [vp, cp]
@@ -305,6 +307,11 @@ class W_final:
         out = (ctypes.c_uint64 * len(HASH_NAMES))()
         self._check(lib().ccj_hashes(self._h, out))
         return {name: "%016x" % out[x] for x, name in enumerate(HASH_NAMES)}
+
+    def set_timing(self, mode: int) -> None:
+        """What later ccj() calls time: 0 = the fill; 1 (default) = + level durations; 2 = + per-kernel
+        family times (k_diag2d, k_iloop) from extra marker events, which slow the fill down."""
+        self._check(lib().ccj_set_timing(self._h, mode))
 
     def timing(self) -> dict:
         f = ctypes.c_double()

@@ -71,7 +71,12 @@ struct ccj_ctx {
     bool host_tb = false;                   // W + traceback on the host over the mirror (else on the GPU)
     int split_target = 6144;                // k_level4d split heuristic (0: never split)
     bool share = true;                      // split-point sharing
-    bool lead_same_stream = false;          // CCJ_LEAD_SAME_STREAM=1: leaders serialized after the plain launch
+    // fill timing (ccj_set_timing, CCJ_LEVEL_TIMING): 0 = fill only; 1 = + level durations from the
+    // lev_done events the fill records anyway (no extra packets); 2 = + a marker pair around every
+    // kernel family launch (k_diag2d, k_iloop, the level span).  The markers of mode 2 are barrier
+    // packets on the streams and cost ~3 ms per n=200 fill, so the default is 1.
+    int level_timing = 1;
+    bool lead_same_stream = true;           // leaders after the plain launch on st (CCJ_LEAD_SAME_STREAM=0: own stream)
     ncclComm_t comm = nullptr;
 
     // layout
@@ -1375,7 +1380,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         c->split_target = e ? atoi(e) : 6144;
         if (opts && opts->split_target) c->split_target = opts->split_target < 0 ? 0 : opts->split_target;
         const char *ls = getenv("CCJ_LEAD_SAME_STREAM");
-        c->lead_same_stream = ls && atoi(ls) == 1;
+        c->lead_same_stream = !(ls && atoi(ls) == 0);
+        const char *lt = getenv("CCJ_LEVEL_TIMING");
+        if (lt) c->level_timing = std::max(0, std::min(2, atoi(lt)));
         const char *g = getenv("CCJ_SHARE_SPLITS");
         c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
     }
@@ -1454,7 +1461,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipEventCreate(&c->ev_end));
     HIPCHK(cp, hipEventCreate(&c->ev_pre));
     c->lev_done.resize(n + 1);
-    for (auto &e : c->lev_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto &e : c->lev_done) HIPCHK(cp, hipEventCreate(&e));  // timed: the level durations (mode 1)
     c->p_done.resize(n + 1);
     for (auto &e : c->p_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->tev.resize(7 * (size_t)n + 7);
@@ -1809,14 +1816,16 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     HIPCHK(c, hipStreamWaitEvent(c->st_p, c->ev_pre, 0));
     for (int s = 0; s < n; ++s) {
         hipEvent_t *ev = &c->tev[7 * (size_t)s];
+        // timing markers (ev[0..6]) only when per-kernel timing is on
+        auto trec = [&](int x, hipStream_t q) { return c->level_timing == 2 ? hipEventRecord(ev[x], q) : hipSuccess; };
         if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_d, c->p_done[s], 0));
-        HIPCHK(c, hipEventRecord(ev[0], c->st_d));
+        HIPCHK(c, trec(0, c->st_d));
         HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, s, c->st_d));
-        HIPCHK(c, hipEventRecord(ev[1], c->st_d));
+        HIPCHK(c, trec(1, c->st_d));
         HIPCHK(c, hipEventRecord(c->dg_done[s], c->st_d));
         if (s < c->nlev) {
             if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 3], 0));
-            HIPCHK(c, hipEventRecord(ev[2], c->st_il));
+            HIPCHK(c, trec(2, c->st_il));
             const int G = c->world;
             for (int r = 0; r < G; ++r) {
                 if (!c->simulate && r != c->rank) continue;
@@ -1826,23 +1835,25 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
                 HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[tr], (int)(c->it_off[tr + 1] - c->it_off[tr]), lo, hi,
                                                  c->st_il));
             }
-            HIPCHK(c, hipEventRecord(ev[3], c->st_il));
+            HIPCHK(c, trec(3, c->st_il));
             HIPCHK(c, hipEventRecord(c->il_done[s], c->st_il));
             HIPCHK(c, hipStreamWaitEvent(st, c->il_done[s], 0));
             if (s >= 1) HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s - 1], 0));
-            HIPCHK(c, hipEventRecord(ev[4], st));
+            HIPCHK(c, trec(4, st));
             for (int r = 0; r < G; ++r) {
                 if (!c->simulate && r != c->rank) continue;
                 int lo = 0, hi = 0;
                 ccj_shard_range(n, s, G, r, &lo, &hi);
                 HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, lo, hi, G == 1 ? 1 : 0, st));
             }
-            HIPCHK(c, hipEventRecord(c->pl_done[s], st));
+            if (!c->lead_same_stream) HIPCHK(c, hipEventRecord(c->pl_done[s], st));
             if (s >= c->T.g_lo && s < c->T.g_hi && c->lead_same_stream) {
-                HIPCHK(c, hipEventRecord(ev[6], st));  // timing experiment: leaders after the plain launch
+                // leaders right after the plain launch on the same stream: no cross-stream hop
+                // between the two launches of a level or between levels (measured faster than
+                // running them concurrently on st_lead)
                 HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, st));
             } else if (s >= c->T.g_lo && s < c->T.g_hi) {
-                // leaders on their own stream, same inputs as the level kernel (level s-1 complete,
+                // CCJ_LEAD_SAME_STREAM=0: leaders on their own stream, same inputs as the level kernel (level s-1 complete,
                 // k_iloop(s), k_diag2d(s-1)); the level is done when both launches are.  Level s-1
                 // is waited for as its plain launch (pl_done) plus, in stream order, its leaders
                 // (st_lead), not as the joined lev_done, which would put a second cross-stream hop
@@ -1854,7 +1865,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
                     if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->lev_done[s - 1], 0));
                     else HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->ev_pre, 0));
                 }
-                HIPCHK(c, hipEventRecord(ev[6], c->st_lead));
+                HIPCHK(c, trec(6, c->st_lead));
                 HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, c->st_lead));
                 HIPCHK(c, hipEventRecord(c->ld_done[s], c->st_lead));
                 HIPCHK(c, hipStreamWaitEvent(st, c->ld_done[s], 0));
@@ -1876,7 +1887,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
                 }
                 HIPCHK(c, (hipError_t)ccjk_copies(&c->T, s, 0, s + 1, st));
             }
-            HIPCHK(c, hipEventRecord(ev[5], st));
+            HIPCHK(c, trec(5, st));
             HIPCHK(c, hipEventRecord(c->lev_done[s], st));
             if (c->overlap && c->h4) {
                 // stream the finished level to the pinned host mirror while later levels run
@@ -1919,7 +1930,16 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     c->lev_ms_v.assign(n, 0.0);
     c->diag_ms_v.assign(n, 0.0);
     c->il_ms_v.assign(n, 0.0);
-    for (int s = 0; s < n; ++s) {
+    if (c->level_timing == 1) {
+        // level s = from the end of level s-1 (ev_pre for s = 0) to its lev_done on st: the waits for
+        // k_iloop(s) / k_diag2d(s-1), the plain launch and the leaders
+        for (int s = 0; s < c->nlev && s < n; ++s) {
+            HIPCHK(c, hipEventElapsedTime(&ms, s == 0 ? c->ev_pre : c->lev_done[s - 1], c->lev_done[s]));
+            lsum += ms;
+            c->lev_ms_v[s] = ms;
+        }
+    }
+    for (int s = 0; s < n && c->level_timing == 2; ++s) {
         const hipEvent_t *ev = &c->tev[7 * (size_t)s];
         HIPCHK(c, hipEventElapsedTime(&ms, ev[0], ev[1]));
         dsum += ms;
@@ -1932,7 +1952,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
             float t4 = 0, t5 = 0, t6 = 0;
             HIPCHK(c, hipEventElapsedTime(&t4, c->ev_start, ev[4]));
             HIPCHK(c, hipEventElapsedTime(&t5, c->ev_start, ev[5]));
-            if (s >= c->T.g_lo && s < c->T.g_hi) {
+            if (s >= c->T.g_lo && s < c->T.g_hi && !c->lead_same_stream) {
                 HIPCHK(c, hipEventElapsedTime(&t6, c->ev_start, ev[6]));
                 t4 = std::min(t4, t6);
             }
@@ -2279,6 +2299,12 @@ extern "C" int ccj_iloop_times(const ccj_ctx *c, double *iloop_ms, int cap) {
 }
 
 extern "C" double ccj_iloop_ms(const ccj_ctx *c) { return c ? c->il_ms : 0.0; }
+
+extern "C" int ccj_set_timing(ccj_ctx *c, int mode) {
+    if (!c || mode < 0 || mode > 2) return CCJ_E_ARG;
+    c->level_timing = mode;
+    return CCJ_OK;
+}
 
 extern "C" int ccj_shard_range(int n, int t, int world, int rank, int *a_lo, int *a_end) {
     if (!a_lo || !a_end || world < 1 || rank < 0 || rank >= world || t < 0) return CCJ_E_ARG;

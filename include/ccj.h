@@ -123,6 +123,10 @@ int  ccj_host_timing(const ccj_ctx *ctx, double *out3);
  * (k_diag2d, span s); ccj_iloop_times: iloop_ms[t] (k_iloop, level t). */
 int  ccj_level_times(const ccj_ctx *ctx, double *level_ms, double *diag_ms, int cap);
 int  ccj_iloop_times(const ccj_ctx *ctx, double *iloop_ms, int cap);
+/* What the next fills time (HIP events): 0 = the fill only; 1 (default) = + per-level durations
+ * (level_ms, from events the fill records anyway); 2 = + k_diag2d / k_iloop times and level spans
+ * from extra marker events around every launch (they slow the fill down by a few percent). */
+int  ccj_set_timing(ccj_ctx *ctx, int mode);
 
 /* ---- band sharding (one sequence over several GPUs) ---- */
 #define CCJ_COMM_ID_BYTES 128

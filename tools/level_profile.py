@@ -17,6 +17,10 @@ fills = []
 for _ in range(int(os.environ.get("CCJ_PROFILE_REPS", "5"))):
     wf.ccj()
     fills.append(wf.timing()["fill_ms"])
+lev1 = wf.timing()["level4d_ms"]
+# one more fold with a marker pair around every launch for the per-kernel breakdown (slower fill)
+wf.set_timing(2)
+wf.ccj()
 L = lib()
 L.ccj_level_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int]
 lv = (ctypes.c_double * n)()
@@ -28,6 +32,8 @@ L.ccj_iloop_times(wf._h, il, n)
 tm = wf.timing()
 tm["fill_ms_median"] = sorted(fills)[len(fills) // 2]
 tm["fill_ms_min"] = min(fills)
+tm["fill_ms_instrumented"] = tm.pop("fill_ms")
+tm["level4d_ms_uninstrumented"] = lev1
 print(json.dumps(tm))
 for t in range(0, n, max(1, n // 25)):
     print(f"t={t:4d} level4d {lv[t]*1e3:9.1f} us   iloop {il[t]*1e3:8.1f} us   diag2d {dg[t]*1e3:8.1f} us")
