@@ -35,6 +35,23 @@ def rseq(seed, n):
     return "".join(r.choice("ACGU") for _ in range(n))
 
 
+def max_over_ranks(elapsed, dist):
+    """The job's time: the slowest rank's wall clock over the timed steps (gloo all-reduce MAX)."""
+    if dist is None:
+        return elapsed
+    import torch
+    tt = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
+
+
+def job_value(cells, steps, elapsed, world, shard):
+    """Whole-job DP-cells/s: batch mode folds one sequence per rank per step, band sharding one
+    sequence per step over all ranks."""
+    seqs_per_step = 1 if shard else world
+    return seqs_per_step * steps * cells / elapsed
+
+
 def cpu_baseline(n_sample=100, seed=3, params="Turner04"):
     """Reference CPU CCJ (oracle/_ref/ref_driver, compiled from the reference sources) on a bounded
     sample of the same workload; falls back to our C restatement (oracle/ccj_oracle.c)."""
@@ -118,11 +135,7 @@ def main():
     wf.ccj()
     tmi = wf.timing()
     il_ms, diag_ms = tmi["iloop_ms"], tmi["diag2d_ms"]
-    if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(elapsed, dist)
 
     cells = num_cells(a.n)
     wm = (ctypes.c_double * 4)()
@@ -156,7 +169,7 @@ def main():
         return
     sec_per_seq = elapsed / a.steps
     seqs_per_step = 1 if shard else world  # sharded: the whole job folds one sequence per step
-    value = seqs_per_step * a.steps * cells / elapsed
+    value = job_value(cells, a.steps, elapsed, world, shard)
     out = {
         "metric": METRIC,
         "value": value,
