@@ -96,6 +96,8 @@ def lib() -> ctypes.CDLL:
     for fn in ("ccj_fill", "ccj_fill_device", "ccj_sync_host", "ccj_n"):
         getattr(L, fn).argtypes = [vp]
         getattr(L, fn).restype = ip
+    L.ccj_reset.argtypes = [vp, cp]
+    L.ccj_reset.restype = ip
     L.ccj_result.argtypes = [vp, cp, ctypes.POINTER(ctypes.c_double), cp, ip]
     L.ccj_result.restype = ip
     L.ccj_get4.argtypes = [vp, ip, ip, ip, ip, ip]
@@ -255,6 +257,18 @@ class W_final:
             self._check(L.ccj_comm_init(h, comm_id))
         self.structure: Optional[str] = None
         self.energy: Optional[float] = None
+        self.stdout_msgs = ""
+
+    def reset(self, seq: str) -> None:
+        """Rebind this context to another sequence of the same length (include/ccj.h ccj_reset):
+        the allocations are reused, only the sequence tables and work lists are rebuilt."""
+        if len(seq) != self.n:
+            raise CCJError(CCJ_E_ARG, f"reset: length {len(seq)} differs from n={self.n}")
+        self._check(lib().ccj_reset(self._h, seq.encode()))
+        self.seq = seq
+        self._seq_buf = ctypes.create_string_buffer(seq.encode())
+        self.structure = None
+        self.energy = None
         self.stdout_msgs = ""
 
     def _check(self, rc: int):

@@ -32,8 +32,8 @@
 #include <string>
 #include <vector>
 
+#include "W_final.hh"
 #include "ccj.h"
-#include "ccj_parfile.h"
 
 static const char kHelp[] =
     "Usage: CCJ [options] [sequence]\n"
@@ -82,25 +82,9 @@ static bool read_blob(const std::string &path, std::vector<char> &out) {
 
 static std::string bundled(const char *name) { return exe_dir() + "/../params/" + name + ".ccjp"; }
 
-// vrna_params_load on top of the compiled-in defaults; 0 ok, 1 = reference would exit(1).
-static int load_par_file(const std::string &path, std::vector<char> &blob) {
-    std::vector<char> base;
-    if (!read_blob(bundled("default"), base)) {
-        std::cerr << "CCJ: missing " << bundled("default") << std::endl;
-        return 1;
-    }
-    blob.assign(sizeof(ccj_energy_params), 0);
-    std::vector<char> log(1 << 22);
-    int rc = ccj_params_load_par(path.c_str(), reinterpret_cast<const ccj_energy_params *>(base.data()),
-                                 reinterpret_cast<ccj_energy_params *>(blob.data()), log.data(), (int)log.size());
-    std::cerr << log.data();
-    if (rc == CCJ_E_PARFILE) return 1;
-    return 0;
-}
-
 struct Args {
     int dangles = 2;
-    bool input_given = false, noConv = false, noGU = false, paramFile_given = false;
+    bool input_given = false, noConv = false, noGU = false, paramFile_given = false, compat_abort = false;
     std::string paramFile;
     std::vector<std::string> inputs;
 };
@@ -164,11 +148,24 @@ static int parse(int argc, char *argv[], Args &a) {
 
 int main(int argc, char *argv[]) {
     Args a;
+    // --ref-compat-abort (exact spelling, anywhere before `--`): reproduce the stock build's n >= 214
+    // assert abort (matrices.hh:160).  It is taken out before the reference's option table sees
+    // argv, so getopt's messages (prefix ambiguity lists) stay the reference's.
+    std::vector<char *> av;
+    for (int k = 0; k < argc; ++k) {
+        if (k > 0 && !strcmp(argv[k], "--")) {
+            for (; k < argc; ++k) av.push_back(argv[k]);
+            break;
+        }
+        if (k > 0 && !strcmp(argv[k], "--ref-compat-abort")) a.compat_abort = true;
+        else av.push_back(argv[k]);
+    }
+    av.push_back(nullptr);
+    argc = (int)av.size() - 1;
+    argv = av.data();
     int pr = parse(argc, argv, a);
     if (pr < 0) return EXIT_SUCCESS;
     if (pr > 0) return 1;
-    const char *dev_env = getenv("CCJ_DEVICE");
-    int device = dev_env ? atoi(dev_env) : 0;
 
     std::string seq;
     if (!a.inputs.empty()) seq = a.inputs[0];
@@ -177,7 +174,6 @@ int main(int argc, char *argv[]) {
     if (!a.noConv)
         for (char &c : seq)
             if (c == 'T') c = 'U';
-    int noGU = a.noGU;
     if (seq.empty()) {
         std::cout << "sequence is missing" << std::endl;
         return EXIT_FAILURE;
@@ -187,65 +183,48 @@ int main(int argc, char *argv[]) {
             std::cout << "Sequence contains character " << c << " that is not G,C,A,U, or T." << std::endl;
             return EXIT_FAILURE;
         }
-    std::vector<char> blob;
+    noGU = a.noGU;  // CCJ.cc:77
     if (a.paramFile_given) {
         if (!exists(a.paramFile)) {
             std::cerr << "Not a valid parameter file!" << std::endl;
             return EXIT_FAILURE;
         }
         size_t L = a.paramFile.size();
-        if (L > 5 && a.paramFile.compare(L - 5, 5, ".ccjp") == 0) {
+        if (L > 5 && a.paramFile.compare(L - 5, 5, ".ccjp") == 0) {  // one of our table blobs
+            std::vector<char> blob;
             if (!read_blob(a.paramFile, blob)) {
                 std::cerr << "Not a valid parameter file!" << std::endl;
                 return EXIT_FAILURE;
             }
-        } else if (load_par_file(a.paramFile, blob)) {
-            return EXIT_FAILURE;
+            ccj_wfinal_use_tables(*reinterpret_cast<const ccj_energy_params *>(blob.data()));
+        } else {
+            vrna_params_load(a.paramFile.c_str(), VRNA_PARAMETER_FORMAT_DEFAULT);  // exits 1 on a syntax error
         }
     } else if (seq.find('T') != std::string::npos) {
         noGU = 1;
-        read_blob(bundled("DNA_Mathews2004"), blob);
-        // vrna_params_load_DNA_Mathews2004 ends in check_symmetry (io.c:1126); the built-in DNA
-        // set has two asymmetric stack-enthalpy pairs, so the reference always prints this
-        for (int w = 0; w < 4; ++w) std::cerr << "WARNING: stacking enthalpies not symmetric" << std::endl;
+        vrna_params_load_DNA_Mathews2004();
     } else if (exists("params/rna_DirksPierce09.par")) {
-        if (load_par_file("params/rna_DirksPierce09.par", blob)) return EXIT_FAILURE;
+        vrna_params_load("params/rna_DirksPierce09.par", VRNA_PARAMETER_FORMAT_DEFAULT);
     } else {
-        read_blob(bundled("DirksPierce09"), blob);
+        std::vector<char> blob;
+        if (!read_blob(bundled("DirksPierce09"), blob)) {
+            std::cerr << "CCJ: bundled parameter tables missing next to " << exe_dir() << std::endl;
+            return 2;
+        }
+        ccj_wfinal_use_tables(*reinterpret_cast<const ccj_energy_params *>(blob.data()));
     }
-    if (blob.size() != sizeof(ccj_energy_params)) {
-        std::cerr << "CCJ: bundled parameter tables missing next to " << exe_dir() << std::endl;
-        return 2;
-    }
-    ccj_problem prob{seq.c_str(), a.dangles, noGU, reinterpret_cast<const ccj_energy_params *>(blob.data()), nullptr};
-    ccj_options o{device, 0, 0, 0, 0, 0, 0, 0};  // fill + traceback on the GPU
-    ccj_ctx *ctx = nullptr;
-    int rc = ccj_create(&prob, &o, &ctx);
-    if (rc != CCJ_OK) {
-        std::cerr << "CCJ: engine error " << rc << ": " << ccj_last_error(ctx) << std::endl;
-        return 2;
-    }
-    rc = ccj_fill(ctx);
-    if (rc != CCJ_OK) {
-        std::cerr << "CCJ: engine error " << rc << ": " << ccj_last_error(ctx) << std::endl;
-        ccj_destroy(ctx);
-        return 2;
-    }
-    std::string structure(seq.size() + 1, '\0');
-    std::vector<char> msgs(1 << 16);
+    if (a.compat_abort) setenv("CCJ_REF_COMPAT_ABORT", "1", 1);
     double energy = 0;
-    rc = ccj_result(ctx, &structure[0], &energy, msgs.data(), (int)msgs.size());
-    std::cout << msgs.data();
-    if (rc == CCJ_E_BACKTRACK || rc == CCJ_E_INTER_EXIT) {
-        std::string err = ccj_last_error(ctx);
-        std::cout.flush();
-        std::cerr << err;
-        ccj_destroy(ctx);
-        return rc == CCJ_E_INTER_EXIT ? 0 : (err.find("Assertion") != std::string::npos ? 134 : EXIT_FAILURE);
+    std::string structure;
+    try {
+        W_final wf(seq, a.dangles);  // CCJ.cc:44-49
+        energy = wf.ccj();
+        structure = wf.structure;
+    } catch (const std::exception &e) {
+        std::cerr << "CCJ: " << e.what() << std::endl;
+        return 2;
     }
-    structure.resize(seq.size());
     std::cout << seq << std::endl;
     std::cout << structure << " (" << energy << ")" << std::endl;
-    ccj_destroy(ctx);
     return 0;
 }

@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -23,6 +24,7 @@
 #include <memory>
 #include <stack>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ccj.h"
@@ -108,6 +110,7 @@ struct ccj_ctx {
     uint2 *d_il = nullptr, *d_ilm = nullptr;
     int16_t *d_dummy = nullptr;
     uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
+    size_t items_cap = 0;
     std::vector<long long> it_off;        // first item of (level t, shard r) at t*world + r
     uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
@@ -1364,6 +1367,178 @@ extern "C" uint64_t ccj_num_cells(int n) {
 
 static thread_local std::string g_create_err;
 
+// Everything that depends on the sequence itself (not only on n): the encoding, the pair-type,
+// hairpin and e_stP tables, and the k_iloop work items.  ccj_create runs it once, ccj_reset for
+// each new sequence of the same length (the allocations are reused).
+static int seq_setup(ccj_ctx *c) {
+    ccj_ctx *cp = c;
+    const int n = c->n;
+    const bool trace = getenv("CCJ_TRACE_SETUP") != nullptr;
+    auto tp0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!trace) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "seq_setup %-10s %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tp0).count());
+        tp0 = now;
+    };
+    const size_t plane = (size_t)(n + 1) * c->rs;
+    // pair_mat.h:159-183 encode_sequence
+    c->S.assign(n + 2, 0);
+    c->S1.assign(n + 2, 0);
+    for (int i = 1; i <= n; ++i) c->S[i] = c->S1[i] = (short)encode_base(c->seq[i - 1]);
+    c->S[n + 1] = c->S[1];
+    c->S[0] = (short)n;
+    c->S1[n + 1] = c->S1[1];
+    c->S1[0] = c->S1[n];
+    // ---- host-side sequence tables: pair types, hairpins, e_stP
+    std::vector<int8_t> pt(plane, 0);
+    std::vector<int> hp(plane, INF);
+    std::vector<int16_t> est(plane, (int16_t)INTERN_INF);
+    c->hpt_h.assign(plane, 0);
+    for (int w = 0; w < n; ++w)
+        for (int p = 1; p + w <= n; ++p) {
+            const int q = p + w;
+            const size_t x = (size_t)w * c->rs + p;
+            const int tc = c->pair[c->S[p]][c->S[q]];
+            pt[x] = (int8_t)tc;
+            c->hpt_h[x] = tc;
+            // HairpinE, s_energy_matrix.cc:275-282
+            hp[x] = (tc == 0) ? INF
+                              : E_Hairpin_host(&c->prm, c->lx.data(), w - 1, tc, c->S1[p + 1], c->S1[q - 1],
+                                               c->seq.c_str() + p - 1);
+            // get_e_stP, pseudo_loop.cc:828-834 (saturated, see k_precompute_ie)
+            if (q - p >= 2 && p + 1 != q - 1) {
+                const int t2 = c->pair[c->S[p + 1]][c->S[q - 1]];
+                const int e = E_IntLoop(&c->prm, c->lx.data(), 0, 0, tc, c->rtype[t2], c->S1[p + 1], c->S1[q - 1],
+                                        c->S1[p], c->S1[q]);
+                const long v = lrint(c->e_stP * e);
+                if (v < -32768) return set_err(cp, CCJ_E_PARAMS, "e_stP below int16 range");
+                if (tc > 0 && t2 > 0 && v >= INTERN_INF) return set_err(cp, CCJ_E_PARAMS, "e_stP of a canonical stack >= 32767");
+                est[x] = (int16_t)(v >= INTERN_INF ? INTERN_INF : v);
+            }
+        }
+    lap("tables");
+    HIPCHK(cp, hipMemcpy(c->d_pt, pt.data(), plane, hipMemcpyHostToDevice));
+    // ---- k_iloop work items (one per wave): the closing pairs that can pair, per level, heaviest
+    // first.  item = role << 30 | f1 << 20 | f2 << 10 | chunk (DESIGN.md §4.2)
+    {
+        const int rs = c->rs;
+        auto ptp = [&](int p, int q) { return (int)pt[(size_t)(q - p) * rs + p]; };
+        // candidate-list lengths (as k_build_il builds them), used to order the waves.  With row
+        // prefix counts R[x][y] = #{y' <= y : (x, y') can pair}, each (u1) row of a pair's window is
+        // one difference, O(IE_U) per pair instead of O(IE_U^2).
+        const int W1 = n + 2;
+        std::vector<int> R((size_t)W1 * W1, 0);
+        for (int x = 1; x <= n; ++x)
+            for (int y = 1; y <= n + 1; ++y)
+                R[(size_t)x * W1 + y] = R[(size_t)x * W1 + y - 1] + (y > x && y <= n && ptp(x, y) > 0 ? 1 : 0);
+        auto rcount = [&](int x, int ylo, int yhi) {  // pairable (x, y), ylo <= y <= yhi
+            if (yhi < ylo) return 0;
+            return R[(size_t)x * W1 + yhi] - R[(size_t)x * W1 + ylo - 1];
+        };
+        std::vector<int> cl((size_t)(n + 1) * rs, 0), cm((size_t)(n + 1) * rs, 0);
+        for (int w = 0; w < n; ++w)
+            for (int p = 1; p + w <= n; ++p) {
+                const int q = p + w;
+                int x = 0, y = 0;
+                for (int u1 = 0; u1 < IE_U; ++u1) {
+                    // closed loops: u1 <= min(w, MAXLOOP) - 2, u2 <= min(w - u1 - 6, MAXLOOP - 2, IE_U - 1)
+                    const int u2hi = std::min({w - u1 - 6, MAXLOOP - 2, IE_U - 1});
+                    if (u1 <= std::min(w, MAXLOOP) - 2 && u2hi >= 0) x += rcount(p + 1 + u1, q - 1 - u2hi, q - 1);
+                    // enclosing loops: d = p-1-u1 >= 1, q+1 <= dp = q+1+u2 <= n
+                    const int d = p - 1 - u1;
+                    if (d >= 1) y += rcount(d, q + 1, std::min(n, q + IE_U));
+                }
+                cl[(size_t)w * rs + p] = x;
+                cm[(size_t)w * rs + p] = y;
+            }
+        lap("listlen");
+        if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
+        constexpr int KMAX = IE_U * IE_U;
+        const int G = c->world;
+        // one item list per (level, shard), built on host threads (levels are independent)
+        std::vector<std::vector<uint32_t>> per((size_t)n * G);
+        auto build_level = [&](int tr, std::vector<std::pair<int, uint32_t>> &lvl, std::vector<int> &hist) {
+            const int t = tr / G, r = tr % G;
+            const int m = n - t - 2;
+            lvl.clear();
+            int a_lo = 0, a_end = 0;
+            ccj_shard_range(n, t, G, r, &a_lo, &a_end);
+            const bool mine = c->simulate || r == c->rank;
+            if (!(mine && t < c->nlev && t >= 4)) return;
+            for (int a = std::max(6, a_lo); a < a_end; ++a)  // PL: (a, i, h-chunk)
+                for (int i = 1; i <= m; ++i)
+                    if (ptp(i, i + a) > 0)
+                        for (int hc = 0; hc * 64 <= m - i; ++hc)
+                            lvl.push_back({cl[(size_t)a * rs + i], (0u << 30) | ((uint32_t)a << 20) | ((uint32_t)i << 10) | (uint32_t)hc});
+            for (int a = a_lo; a <= std::min(t - 6, a_end - 1); ++a)  // PR: (a, q, i-chunk), closing pair (q+a+3, q+t+3)
+                for (int q = 0; q < m; ++q) {
+                    const int k = q + a + 3, b = t - a;
+                    if (ptp(k, k + b) > 0)
+                        for (int ic = 0; ic * 64 <= q; ++ic)
+                            lvl.push_back({cl[(size_t)b * rs + k], (1u << 30) | ((uint32_t)a << 20) | ((uint32_t)q << 10) | (uint32_t)ic});
+                }
+            for (int h = 2; h <= m - 1; ++h)  // PM: (h, j, a-chunk)
+                for (int j = 1; j + h + 2 <= n; ++j) {
+                    const int k = j + h + 2;
+                    const int alo = std::max({2, t - (n - k), a_lo}), ahi = std::min({t - 2, j - 1, a_end - 1});
+                    if (alo > ahi || ptp(j, k) <= 0) continue;
+                    for (int ac = 0; alo + ac * 64 <= ahi; ++ac)
+                        lvl.push_back({cm[(size_t)(h + 2) * rs + j], (2u << 30) | ((uint32_t)h << 20) | ((uint32_t)j << 10) | (uint32_t)ac});
+                }
+            // heaviest list first: a stable counting sort on the list length (keys <= IE_U^2),
+            // the same order as a stable sort by descending key
+            std::fill(hist.begin(), hist.end(), 0);
+            for (auto &e : lvl) ++hist[KMAX - e.first];
+            int pos = 0;
+            for (int k = 0; k <= KMAX; ++k) {
+                const int cnt = hist[k];
+                hist[k] = pos;
+                pos += cnt;
+            }
+            std::vector<uint32_t> &out = per[tr];
+            out.resize(pos);
+            for (auto &e : lvl) out[hist[KMAX - e.first]++] = e.second;
+        };
+        {
+            std::atomic<int> next{0};
+            auto worker = [&]() {
+                std::vector<std::pair<int, uint32_t>> lvl;
+                std::vector<int> hist(KMAX + 1);
+                for (int tr; (tr = next.fetch_add(1)) < n * G;) build_level(tr, lvl, hist);
+            };
+            const int nth = std::max(1, std::min<int>(8, (int)std::thread::hardware_concurrency()));
+            std::vector<std::thread> pool;
+            for (int x = 1; x < nth; ++x) pool.emplace_back(worker);
+            worker();
+            for (auto &th : pool) th.join();
+        }
+        c->it_off.assign((size_t)n * G + 1, 0);
+        for (int tr = 0; tr < n * G; ++tr) c->it_off[tr + 1] = c->it_off[tr] + (long long)per[tr].size();
+        std::vector<uint32_t> items((size_t)c->it_off[(size_t)n * G]);
+        for (int tr = 0; tr < n * G; ++tr)
+            if (!per[tr].empty()) memcpy(items.data() + c->it_off[tr], per[tr].data(), per[tr].size() * sizeof(uint32_t));
+        c->it_off[(size_t)n * G] = (long long)items.size();
+        lap("items");
+        if (items.size() > c->items_cap || !c->d_items) {  // ccj_reset: grow only
+            if (c->d_items) HIPCHK(cp, hipFree(c->d_items));
+            c->d_items = nullptr;
+            c->items_cap = std::max<size_t>(items.size(), 1);
+            HIPCHK(cp, hipMalloc(&c->d_items, c->items_cap * sizeof(uint32_t)));
+        }
+        c->T.items = c->d_items;
+        if (!items.empty())
+            HIPCHK(cp, hipMemcpy(c->d_items, items.data(), items.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    HIPCHK(cp, hipMemcpy(c->d_hp, hp.data(), plane * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_est, est.data(), plane * sizeof(int16_t), hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_S, c->S.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
+    HIPCHK(cp, hipMemcpy(c->d_S1, c->S1.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
+    lap("upload");
+    c->filled = c->mirrored = false;
+    return CCJ_OK;
+}
+
 static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::unique_ptr<ccj_ctx> &c, ccj_ctx **out) {
     c->seq = prob->seq;
     c->n = (int)c->seq.size();
@@ -1408,13 +1583,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     if (c->noGU) c->pair[3][4] = c->pair[4][3] = 0;
     for (int x = 0; x < 8; ++x)
         for (int y = 0; y < 8; ++y) c->rtype[c->pair[x][y]] = c->pair[y][x];
-    c->S.assign(n + 2, 0);
-    c->S1.assign(n + 2, 0);
-    for (int i = 1; i <= n; ++i) c->S[i] = c->S1[i] = (short)encode_base(c->seq[i - 1]);
-    c->S[n + 1] = c->S[1];
-    c->S[0] = (short)n;
-    c->S1[n + 1] = c->S1[1];
-    c->S1[0] = c->S1[n];
     // (int)(lxc*log(x/30.)) with the host libm, as ViennaRNA computes it
     c->lx.assign(2 * n + 128, 0);
     for (size_t x = 31; x < c->lx.size(); ++x) c->lx[x] = (int)(c->prm.lxc * log((double)x / 30.));
@@ -1593,111 +1761,15 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
 
     for (int t = 0; t < n; ++t) c->lv_host[t].base = c->d4 ? c->d4 + c->lv_off[t] : nullptr;
 
-    // ---- host-side sequence tables: pair types, hairpins, e_stP
-    std::vector<int8_t> pt(plane, 0);
-    std::vector<int> hp(plane, INF);
-    std::vector<int16_t> est(plane, (int16_t)INTERN_INF);
-    c->hpt_h.assign(plane, 0);
-    for (int w = 0; w < n; ++w)
-        for (int p = 1; p + w <= n; ++p) {
-            const int q = p + w;
-            const size_t x = (size_t)w * c->rs + p;
-            const int tc = c->pair[c->S[p]][c->S[q]];
-            pt[x] = (int8_t)tc;
-            c->hpt_h[x] = tc;
-            // HairpinE, s_energy_matrix.cc:275-282
-            hp[x] = (tc == 0) ? INF
-                              : E_Hairpin_host(&c->prm, c->lx.data(), w - 1, tc, c->S1[p + 1], c->S1[q - 1],
-                                               c->seq.c_str() + p - 1);
-            // get_e_stP, pseudo_loop.cc:828-834 (saturated, see k_precompute_ie)
-            if (q - p >= 2 && p + 1 != q - 1) {
-                const int t2 = c->pair[c->S[p + 1]][c->S[q - 1]];
-                const int e = E_IntLoop(&c->prm, c->lx.data(), 0, 0, tc, c->rtype[t2], c->S1[p + 1], c->S1[q - 1],
-                                        c->S1[p], c->S1[q]);
-                const long v = lrint(c->e_stP * e);
-                if (v < -32768) return set_err(cp, CCJ_E_PARAMS, "e_stP below int16 range");
-                if (tc > 0 && t2 > 0 && v >= INTERN_INF) return set_err(cp, CCJ_E_PARAMS, "e_stP of a canonical stack >= 32767");
-                est[x] = (int16_t)(v >= INTERN_INF ? INTERN_INF : v);
-            }
-        }
+    if (const int rc = seq_setup(cp)) return rc;
     int8_t pair8[64], rt8[8];
     for (int x = 0; x < 8; ++x) {
         rt8[x] = (int8_t)c->rtype[x];
         for (int y = 0; y < 8; ++y) pair8[x * 8 + y] = (int8_t)c->pair[x][y];
     }
-    HIPCHK(cp, hipMemcpy(c->d_pt, pt.data(), plane, hipMemcpyHostToDevice));
-    // ---- k_iloop work items (one per wave): the closing pairs that can pair, per level, heaviest
-    // first.  item = role << 30 | f1 << 20 | f2 << 10 | chunk (DESIGN.md §4.2)
-    {
-        const int rs = c->rs;
-        auto ptp = [&](int p, int q) { return (int)pt[(size_t)(q - p) * rs + p]; };
-        // candidate-list lengths (as k_build_il builds them), used to order the waves
-        std::vector<int> cl((size_t)(n + 1) * rs, 0), cm((size_t)(n + 1) * rs, 0);
-        for (int w = 0; w < n; ++w)
-            for (int p = 1; p + w <= n; ++p) {
-                const int q = p + w;
-                int x = 0, y = 0;
-                for (int u1 = 0; u1 < IE_U; ++u1)
-                    for (int u2 = 0; u2 < IE_U; ++u2) {
-                        if (u1 <= std::min(w, MAXLOOP) - 2 && u2 <= std::min(w - u1 - 6, MAXLOOP - 2) &&
-                            ptp(p + 1 + u1, q - 1 - u2) > 0)
-                            ++x;
-                        const int d = p - 1 - u1, dp = q + 1 + u2;
-                        if (d >= 1 && dp <= n && ptp(d, dp) > 0) ++y;
-                    }
-                cl[(size_t)w * rs + p] = x;
-                cm[(size_t)w * rs + p] = y;
-            }
-        if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
-        std::vector<uint32_t> items;
-        std::vector<std::pair<int, uint32_t>> lvl;
-        const int G = c->world;
-        c->it_off.assign((size_t)n * G + 1, 0);
-        for (int tr = 0; tr < n * G; ++tr) {
-            const int t = tr / G, r = tr % G;
-            c->it_off[tr] = (long long)items.size();
-            const int m = n - t - 2;
-            lvl.clear();
-            int a_lo = 0, a_end = 0;
-            ccj_shard_range(n, t, G, r, &a_lo, &a_end);
-            const bool mine = c->simulate || r == c->rank;
-            if (mine && t < c->nlev && t >= 4) {
-                for (int a = std::max(6, a_lo); a < a_end; ++a)  // PL: (a, i, h-chunk)
-                    for (int i = 1; i <= m; ++i)
-                        if (ptp(i, i + a) > 0)
-                            for (int hc = 0; hc * 64 <= m - i; ++hc)
-                                lvl.push_back({cl[(size_t)a * rs + i], (0u << 30) | ((uint32_t)a << 20) | ((uint32_t)i << 10) | (uint32_t)hc});
-                for (int a = a_lo; a <= std::min(t - 6, a_end - 1); ++a)  // PR: (a, q, i-chunk), closing pair (q+a+3, q+t+3)
-                    for (int q = 0; q < m; ++q) {
-                        const int k = q + a + 3, b = t - a;
-                        if (ptp(k, k + b) > 0)
-                            for (int ic = 0; ic * 64 <= q; ++ic)
-                                lvl.push_back({cl[(size_t)b * rs + k], (1u << 30) | ((uint32_t)a << 20) | ((uint32_t)q << 10) | (uint32_t)ic});
-                    }
-                for (int h = 2; h <= m - 1; ++h)  // PM: (h, j, a-chunk)
-                    for (int j = 1; j + h + 2 <= n; ++j) {
-                        const int k = j + h + 2;
-                        const int alo = std::max({2, t - (n - k), a_lo}), ahi = std::min({t - 2, j - 1, a_end - 1});
-                        if (alo > ahi || ptp(j, k) <= 0) continue;
-                        for (int ac = 0; alo + ac * 64 <= ahi; ++ac)
-                            lvl.push_back({cm[(size_t)(h + 2) * rs + j], (2u << 30) | ((uint32_t)h << 20) | ((uint32_t)j << 10) | (uint32_t)ac});
-                    }
-                std::stable_sort(lvl.begin(), lvl.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
-                for (auto &e : lvl) items.push_back(e.second);
-            }
-        }
-        c->it_off[(size_t)n * G] = (long long)items.size();
-        HIPCHK(cp, hipMalloc(&c->d_items, std::max<size_t>(items.size(), 1) * sizeof(uint32_t)));
-        if (!items.empty())
-            HIPCHK(cp, hipMemcpy(c->d_items, items.data(), items.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    }
-    HIPCHK(cp, hipMemcpy(c->d_hp, hp.data(), plane * sizeof(int), hipMemcpyHostToDevice));
-    HIPCHK(cp, hipMemcpy(c->d_est, est.data(), plane * sizeof(int16_t), hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_pair, pair8, 64, hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_rtype, rt8, 8, hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_lx, c->lx.data(), c->lx.size() * sizeof(int), hipMemcpyHostToDevice));
-    HIPCHK(cp, hipMemcpy(c->d_S, c->S.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
-    HIPCHK(cp, hipMemcpy(c->d_S1, c->S1.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_prm, &c->prm, sizeof(ccj_energy_params), hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_lv, c->lv_host.data(), c->lv_host.size() * sizeof(LevelDesc), hipMemcpyHostToDevice));
     {
@@ -1788,6 +1860,21 @@ extern "C" int ccj_create(const ccj_problem *prob, const ccj_options *opts, ccj_
         if (c) ccj_destroy(c.release());
     }
     return rc;
+}
+
+extern "C" int ccj_reset(ccj_ctx *c, const char *seq) {
+    if (!c || !seq) return CCJ_E_ARG;
+    const std::string s(seq);
+    if ((int)s.size() != c->n) return set_err(c, CCJ_E_ARG, "ccj_reset: length %zu differs from the context's n=%d", s.size(), c->n);
+    for (char ch : s)
+        if (!(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'U' || ch == 'T'))
+            return set_err(c, CCJ_E_ARG, "ccj_reset: invalid character in sequence");
+    HIPCHK(c, hipSetDevice(c->device));
+    // the previous fold's streams may still read the sequence tables
+    for (hipStream_t q : {c->st, c->st_copy, c->st_p, c->st_il, c->st_d, c->st_lead}) HIPCHK(c, hipStreamSynchronize(q));
+    c->seq = s;
+    c->W.clear();
+    return seq_setup(c);
 }
 
 extern "C" int ccj_fill_device(ccj_ctx *c) {

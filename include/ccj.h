@@ -88,6 +88,13 @@ typedef struct ccj_options {
  * (reference W_final.cc:20-56).  opts may be NULL. */
 int  ccj_create(const ccj_problem *prob, const ccj_options *opts, ccj_ctx **out);
 
+/* Rebind a context to another sequence of the same length n (same tables, dangles, noGU,
+ * options): rebuilds only the sequence tables and the interior-loop work lists and reuses every
+ * allocation, so a batch of equal-length sequences pays ccj_create's multi-GB allocation once.
+ * The reference has no equivalent (each fold constructs a new W_final, W_final.cc:20-56).
+ * CCJ_E_ARG if the length differs or the sequence has characters other than ACGUT. */
+int  ccj_reset(ccj_ctx *ctx, const char *seq);
+
 /* Run the whole DP fill on the GPU (replaces W_final.cc:60-67), then make the host mirror
  * valid (ccj_sync_host is implied). */
 int  ccj_fill(ccj_ctx *ctx);

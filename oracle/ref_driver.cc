@@ -161,7 +161,7 @@ struct Opts {
     int dangles = 2;
     bool noGU = false;
     std::string parfile, blob, dump, out;
-    bool dna = false, timing = false;
+    bool dna = false, timing = false, hash = false;
     std::string seq;
 };
 
@@ -214,50 +214,10 @@ struct Hasher {
     }
 };
 
-static int cmd_fold(const Opts &o) {
-    noGU = o.noGU ? 1 : 0;
-    if (load_params(o)) return 1;
-    std::string seq = o.seq;
-    auto t0 = std::chrono::steady_clock::now();
-    W_final wf(seq, o.dangles);
-    double energy = wf.ccj();
-    auto t1 = std::chrono::steady_clock::now();
-    std::cout << seq << std::endl;
-    std::cout << wf.structure << " (" << energy << ")" << std::endl;
-    if (o.timing)
-        fprintf(stderr, "TIME %.6f\n", std::chrono::duration<double>(t1 - t0).count());
-    return 0;
-}
-
-// Fill only, by calling the reference's own member functions in the order of
-// W_final.cc:60-77 (no backtrack, so reference backtrack exits cannot hide the matrices), then
-// print one FNV-1a hash per matrix in canonical order.
-static int cmd_hash(const Opts &o) {
-    noGU = o.noGU ? 1 : 0;
-    if (load_params(o)) return 1;
-    std::string seq = o.seq;
-    W_final wf(seq, o.dangles);
-    int n = (int)seq.size();
+// One FNV-1a hash per DP matrix in canonical (i,j,k,l) order, printed as HASH lines.
+static void hash_all(const Opts &o, W_final &wf, int n) {
     pseudo_loop *P = wf.P;
     s_energy_matrix *V = wf.V;
-    for (int i = n; i >= 1; --i)
-        for (int j = i; j <= n; ++j) {
-            V->compute_energy(i, j);
-            P->compute_energies(i, j);
-            V->compute_WMv_WMp(i, j, P->get_energy(i, j));
-            V->compute_energy_WM(i, j, P->P);
-        }
-    for (int j = TURN + 1; j <= n; j++) {
-        energy_t m1 = wf.W[j - 1], m2 = INF, m3 = INF;
-        for (int k = 1; k <= j - TURN - 1; ++k) {
-            energy_t acc = (k > 1) ? wf.W[k - 1] : 0;
-            m2 = std::min(m2, acc + wf.E_ext_Stem(V->get_energy(k, j), V->get_energy(k + 1, j), V->get_energy(k, j - 1),
-                                                   V->get_energy(k + 1, j - 1), wf.S_, wf.params_, k, j, n));
-            m3 = std::min(m3, acc + std::min({P->get_energy(k, j), P->get_energy(k + 1, j), P->get_energy(k, j - 1),
-                                              P->get_energy(k + 1, j - 1)}) + PS_penalty);
-        }
-        wf.W[j] = std::min({m1, m2, m3});
-    }
     Hasher H;
     if (!o.dump.empty()) H.dump = fopen(o.dump.c_str(), "wb");
     H.add4("PK", P->PK, n);
@@ -301,6 +261,58 @@ static int cmd_hash(const Opts &o) {
     }
     if (H.dump) fclose(H.dump);
     for (auto &kv : H.hashes) printf("HASH %s %016llx\n", kv.first.c_str(), (unsigned long long)kv.second);
+}
+
+static int cmd_fold(const Opts &o) {
+    noGU = o.noGU ? 1 : 0;
+    if (load_params(o)) return 1;
+    std::string seq = o.seq;
+    auto t0 = std::chrono::steady_clock::now();
+    W_final wf(seq, o.dangles);
+    double energy = wf.ccj();
+    auto t1 = std::chrono::steady_clock::now();
+    std::cout << seq << std::endl;
+    std::cout << wf.structure << " (" << energy << ")" << std::endl;
+    if (o.timing)
+        fprintf(stderr, "TIME %.6f\n", std::chrono::duration<double>(t1 - t0).count());
+    if (o.hash) {  // the matrices and W survive ccj(); hash them after the fold's own output
+        fflush(stdout);
+        hash_all(o, wf, (int)seq.size());
+        printf("MFE %d\n", (int)wf.W[seq.size()]);
+    }
+    return 0;
+}
+
+// Fill only, by calling the reference's own member functions in the order of
+// W_final.cc:60-77 (no backtrack, so reference backtrack exits cannot hide the matrices), then
+// print one FNV-1a hash per matrix in canonical order.
+static int cmd_hash(const Opts &o) {
+    noGU = o.noGU ? 1 : 0;
+    if (load_params(o)) return 1;
+    std::string seq = o.seq;
+    W_final wf(seq, o.dangles);
+    int n = (int)seq.size();
+    pseudo_loop *P = wf.P;
+    s_energy_matrix *V = wf.V;
+    for (int i = n; i >= 1; --i)
+        for (int j = i; j <= n; ++j) {
+            V->compute_energy(i, j);
+            P->compute_energies(i, j);
+            V->compute_WMv_WMp(i, j, P->get_energy(i, j));
+            V->compute_energy_WM(i, j, P->P);
+        }
+    for (int j = TURN + 1; j <= n; j++) {
+        energy_t m1 = wf.W[j - 1], m2 = INF, m3 = INF;
+        for (int k = 1; k <= j - TURN - 1; ++k) {
+            energy_t acc = (k > 1) ? wf.W[k - 1] : 0;
+            m2 = std::min(m2, acc + wf.E_ext_Stem(V->get_energy(k, j), V->get_energy(k + 1, j), V->get_energy(k, j - 1),
+                                                   V->get_energy(k + 1, j - 1), wf.S_, wf.params_, k, j, n));
+            m3 = std::min(m3, acc + std::min({P->get_energy(k, j), P->get_energy(k + 1, j), P->get_energy(k, j - 1),
+                                              P->get_energy(k + 1, j - 1)}) + PS_penalty);
+        }
+        wf.W[j] = std::min({m1, m2, m3});
+    }
+    hash_all(o, wf, n);
     printf("MFE %d\n", (int)wf.W[n]);
     return 0;
 }
@@ -333,6 +345,7 @@ int main(int argc, char **argv) {
         else if (s == "--blob" && a + 1 < argc) o.blob = argv[++a];
         else if (s == "--dna") o.dna = true;
         else if (s == "--time") o.timing = true;
+        else if (s == "--hash") o.hash = true;
         else if (s == "--dump" && a + 1 < argc) o.dump = argv[++a];
         else if (s == "-o" && a + 1 < argc) o.out = argv[++a];
         else o.seq = s;

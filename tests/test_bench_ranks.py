@@ -5,6 +5,8 @@ import os
 import socket
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
@@ -17,16 +19,20 @@ def _free_port():
 
 
 def _rank(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, bench.max_over_ranks(1.0 + 2.5 * rank, dist)))
-    finally:
-        dist.destroy_process_group()
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            q.put((rank, bench.max_over_ranks(1.0 + 2.5 * rank, dist)))
+        finally:
+            dist.destroy_process_group()
+    except Exception as e:  # report to the parent instead of leaving it blocked on the queue
+        q.put((rank, repr(e)))
 
 
 def test_max_over_ranks_gloo():
+    pytest.importorskip("torch")
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -49,3 +55,33 @@ def test_job_value():
     assert bench.job_value(cells, 5, 0.25, 1, False) == 5 * cells / 0.25
     assert bench.job_value(cells, 5, 0.25, 8, False) == 8 * 5 * cells / 0.25   # batch: weak scaling
     assert bench.job_value(cells, 5, 0.25, 8, True) == 5 * cells / 0.25        # band-sharded: one fold
+
+
+def test_rank_seeds():
+    # batch: rank r folds seed + r (config 5: --seed 6 --gpus 8 -> seeds 6..13); --distinct: new every step
+    assert [bench.rank_seed(6, r, 8, 0, False) for r in range(8)] == list(range(6, 14))
+    assert bench.rank_seed(6, 3, 8, 5, False) == 9
+    assert [bench.rank_seed(5, 1, 2, k, True) for k in range(3)] == [6, 8, 10]
+
+
+def test_gpus_flag_spawns_ranks():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts two rank processes itself (gloo, no GPU in
+    --dry-run) and rank 0 reports n_gpus 2 with both ranks present."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--dry-run",
+                        "--seed", "6"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["ranks_reported"] == 2 and out["seeds"] == [6, 7]
+
+
+def test_gpus_mismatch_fails():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0

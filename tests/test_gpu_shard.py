@@ -57,3 +57,17 @@ def test_sharded_fold_equals_unsharded(n, world):
         assert wf.hashes() == h0
     finally:
         wf.close()
+
+
+@pytest.mark.parametrize("world", [4])
+@pytest.mark.parametrize("case", [c for c in golden("e2e_large.json") if c["n"] == 200], ids=lambda c: c["tag"])
+def test_sharded_fold_matches_reference_stdout(case, world):
+    """BASELINE config 4 (DirksPierce09, n=200, 4 GPUs) and the headline sequence, band-sharded
+    (shard_simulate), against the reference's own output for the same input."""
+    from ccj_amd import W_final
+    wf = W_final(case["seq"], case["dangles"], params=case["params"], shard_world=world, shard_simulate=True)
+    try:
+        e = wf.ccj()
+        assert wf.stdout_msgs + case["seq"] + "\n" + f"{wf.structure} ({e:g})\n" == case["stdout"]
+    finally:
+        wf.close()
