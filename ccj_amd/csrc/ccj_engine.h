@@ -164,4 +164,6 @@ int ccjk_level_split(int n, int t, int a_lo, int a_end, int split_target);
 int ccjk_level4d_lead(const ccj::DevTables *T, int t, void *stream);
 int ccjk_copies(const ccj::DevTables *T, int t, int a_lo, int a_end, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
+int ccjk_items(const ccj::DevTables *T, const int2 *range, int G, int rank, int simulate, long long *counts,
+               const long long *offs, uint32_t *items, int pass, void *stream);
 }

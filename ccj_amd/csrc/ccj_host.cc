@@ -111,6 +111,8 @@ struct ccj_ctx {
     int16_t *d_dummy = nullptr;
     uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
     size_t items_cap = 0;
+    int2 *d_irange = nullptr;             // [t*world + r]: the a-blocks shard r computes at level t
+    long long *d_icount = nullptr, *d_ioff = nullptr;  // k_items: items per (t, r), first item
     std::vector<long long> it_off;        // first item of (level t, shard r) at t*world + r
     uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
@@ -1419,116 +1421,31 @@ static int seq_setup(ccj_ctx *c) {
         }
     lap("tables");
     HIPCHK(cp, hipMemcpy(c->d_pt, pt.data(), plane, hipMemcpyHostToDevice));
-    // ---- k_iloop work items (one per wave): the closing pairs that can pair, per level, heaviest
-    // first.  item = role << 30 | f1 << 20 | f2 << 10 | chunk
+    // ---- k_iloop work items (one per wave), built on the GPU by k_items: count per (level, shard),
+    // offsets on the host, then write
     {
-        const int rs = c->rs;
-        auto ptp = [&](int p, int q) { return (int)pt[(size_t)(q - p) * rs + p]; };
-        // candidate-list lengths (as k_build_il builds them), used to order the waves.  With row
-        // prefix counts R[x][y] = #{y' <= y : (x, y') can pair}, each (u1) row of a pair's window is
-        // one difference, O(IE_U) per pair instead of O(IE_U^2).
-        const int W1 = n + 2;
-        std::vector<int> R((size_t)W1 * W1, 0);
-        for (int x = 1; x <= n; ++x)
-            for (int y = 1; y <= n + 1; ++y)
-                R[(size_t)x * W1 + y] = R[(size_t)x * W1 + y - 1] + (y > x && y <= n && ptp(x, y) > 0 ? 1 : 0);
-        auto rcount = [&](int x, int ylo, int yhi) {  // pairable (x, y), ylo <= y <= yhi
-            if (yhi < ylo) return 0;
-            return R[(size_t)x * W1 + yhi] - R[(size_t)x * W1 + ylo - 1];
-        };
-        std::vector<int> cl((size_t)(n + 1) * rs, 0), cm((size_t)(n + 1) * rs, 0);
-        for (int w = 0; w < n; ++w)
-            for (int p = 1; p + w <= n; ++p) {
-                const int q = p + w;
-                int x = 0, y = 0;
-                for (int u1 = 0; u1 < IE_U; ++u1) {
-                    // closed loops: u1 <= min(w, MAXLOOP) - 2, u2 <= min(w - u1 - 6, MAXLOOP - 2, IE_U - 1)
-                    const int u2hi = std::min({w - u1 - 6, MAXLOOP - 2, IE_U - 1});
-                    if (u1 <= std::min(w, MAXLOOP) - 2 && u2hi >= 0) x += rcount(p + 1 + u1, q - 1 - u2hi, q - 1);
-                    // enclosing loops: d = p-1-u1 >= 1, q+1 <= dp = q+1+u2 <= n
-                    const int d = p - 1 - u1;
-                    if (d >= 1) y += rcount(d, q + 1, std::min(n, q + IE_U));
-                }
-                cl[(size_t)w * rs + p] = x;
-                cm[(size_t)w * rs + p] = y;
-            }
-        lap("listlen");
         if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
-        constexpr int KMAX = IE_U * IE_U;
         const int G = c->world;
-        // one item list per (level, shard), built on host threads (levels are independent)
-        std::vector<std::vector<uint32_t>> per((size_t)n * G);
-        auto build_level = [&](int tr, std::vector<std::pair<int, uint32_t>> &lvl, std::vector<int> &hist) {
-            const int t = tr / G, r = tr % G;
-            const int m = n - t - 2;
-            lvl.clear();
-            int a_lo = 0, a_end = 0;
-            ccj_shard_range(n, t, G, r, &a_lo, &a_end);
-            const bool mine = c->simulate || r == c->rank;
-            if (!(mine && t < c->nlev && t >= 4)) return;
-            for (int a = std::max(6, a_lo); a < a_end; ++a)  // PL: (a, i, h-chunk)
-                for (int i = 1; i <= m; ++i)
-                    if (ptp(i, i + a) > 0)
-                        for (int hc = 0; hc * 64 <= m - i; ++hc)
-                            lvl.push_back({cl[(size_t)a * rs + i], (0u << 30) | ((uint32_t)a << 20) | ((uint32_t)i << 10) | (uint32_t)hc});
-            for (int a = a_lo; a <= std::min(t - 6, a_end - 1); ++a)  // PR: (a, q, i-chunk), closing pair (q+a+3, q+t+3)
-                for (int q = 0; q < m; ++q) {
-                    const int k = q + a + 3, b = t - a;
-                    if (ptp(k, k + b) > 0)
-                        for (int ic = 0; ic * 64 <= q; ++ic)
-                            lvl.push_back({cl[(size_t)b * rs + k], (1u << 30) | ((uint32_t)a << 20) | ((uint32_t)q << 10) | (uint32_t)ic});
-                }
-            for (int h = 2; h <= m - 1; ++h)  // PM: (h, j, a-chunk)
-                for (int j = 1; j + h + 2 <= n; ++j) {
-                    const int k = j + h + 2;
-                    const int alo = std::max({2, t - (n - k), a_lo}), ahi = std::min({t - 2, j - 1, a_end - 1});
-                    if (alo > ahi || ptp(j, k) <= 0) continue;
-                    for (int ac = 0; alo + ac * 64 <= ahi; ++ac)
-                        lvl.push_back({cm[(size_t)(h + 2) * rs + j], (2u << 30) | ((uint32_t)h << 20) | ((uint32_t)j << 10) | (uint32_t)ac});
-                }
-            // heaviest list first: a stable counting sort on the list length (keys <= IE_U^2),
-            // the same order as a stable sort by descending key
-            std::fill(hist.begin(), hist.end(), 0);
-            for (auto &e : lvl) ++hist[KMAX - e.first];
-            int pos = 0;
-            for (int k = 0; k <= KMAX; ++k) {
-                const int cnt = hist[k];
-                hist[k] = pos;
-                pos += cnt;
-            }
-            std::vector<uint32_t> &out = per[tr];
-            out.resize(pos);
-            for (auto &e : lvl) out[hist[KMAX - e.first]++] = e.second;
-        };
-        {
-            std::atomic<int> next{0};
-            auto worker = [&]() {
-                std::vector<std::pair<int, uint32_t>> lvl;
-                std::vector<int> hist(KMAX + 1);
-                for (int tr; (tr = next.fetch_add(1)) < n * G;) build_level(tr, lvl, hist);
-            };
-            const int nth = std::max(1, std::min<int>(8, (int)std::thread::hardware_concurrency()));
-            std::vector<std::thread> pool;
-            for (int x = 1; x < nth; ++x) pool.emplace_back(worker);
-            worker();
-            for (auto &th : pool) th.join();
-        }
-        c->it_off.assign((size_t)n * G + 1, 0);
-        for (int tr = 0; tr < n * G; ++tr) c->it_off[tr + 1] = c->it_off[tr] + (long long)per[tr].size();
-        std::vector<uint32_t> items((size_t)c->it_off[(size_t)n * G]);
-        for (int tr = 0; tr < n * G; ++tr)
-            if (!per[tr].empty()) memcpy(items.data() + c->it_off[tr], per[tr].data(), per[tr].size() * sizeof(uint32_t));
-        c->it_off[(size_t)n * G] = (long long)items.size();
-        lap("items");
-        if (items.size() > c->items_cap || !c->d_items) {  // ccj_reset: grow only
+        const int nb = n * G;
+        HIPCHK(cp, (hipError_t)ccjk_items(&c->T, c->d_irange, G, c->rank, c->simulate, c->d_icount, nullptr, nullptr, 0, c->st));
+        std::vector<long long> cnt((size_t)nb);
+        HIPCHK(cp, hipMemcpyAsync(cnt.data(), c->d_icount, nb * sizeof(long long), hipMemcpyDeviceToHost, c->st));
+        HIPCHK(cp, hipStreamSynchronize(c->st));
+        c->it_off.assign((size_t)nb + 1, 0);
+        for (int x = 0; x < nb; ++x) c->it_off[x + 1] = c->it_off[x] + cnt[x];
+        const size_t total = (size_t)c->it_off[nb];
+        lap("count");
+        if (total > c->items_cap || !c->d_items) {  // ccj_reset: grow only
             if (c->d_items) HIPCHK(cp, hipFree(c->d_items));
             c->d_items = nullptr;
-            c->items_cap = std::max<size_t>(items.size(), 1);
+            c->items_cap = std::max<size_t>(total, 1);
             HIPCHK(cp, hipMalloc(&c->d_items, c->items_cap * sizeof(uint32_t)));
         }
         c->T.items = c->d_items;
-        if (!items.empty())
-            HIPCHK(cp, hipMemcpy(c->d_items, items.data(), items.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        HIPCHK(cp, hipMemcpyAsync(c->d_ioff, c->it_off.data(), (nb + 1) * sizeof(long long), hipMemcpyHostToDevice, c->st));
+        HIPCHK(cp, (hipError_t)ccjk_items(&c->T, c->d_irange, G, c->rank, c->simulate, c->d_icount, c->d_ioff, c->d_items, 1,
+                                          c->st));
+        // the fill's first launches are on st too (k_iloop waits for ev_pre, recorded on st)
     }
     HIPCHK(cp, hipMemcpy(c->d_hp, hp.data(), plane * sizeof(int), hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_est, est.data(), plane * sizeof(int16_t), hipMemcpyHostToDevice));
@@ -1761,7 +1678,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
 
     for (int t = 0; t < n; ++t) c->lv_host[t].base = c->d4 ? c->d4 + c->lv_off[t] : nullptr;
 
-    if (const int rc = seq_setup(cp)) return rc;
     int8_t pair8[64], rt8[8];
     for (int x = 0; x < 8; ++x) {
         rt8[x] = (int8_t)c->rtype[x];
@@ -1840,6 +1756,22 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.lord_off = c->d_lord_off;
     T.lord_off_h = c->lord_off.empty() ? nullptr : c->lord_off.data();
     T.accC = accC;
+    {
+        // shard ranges of the k_iloop work items, [t*world + r] (sequence-independent)
+        const int G = c->world;
+        std::vector<int2> rg((size_t)n * G);
+        for (int t = 0; t < n; ++t)
+            for (int r = 0; r < G; ++r) {
+                int lo = 0, hi = 0;
+                ccj_shard_range(n, t, G, r, &lo, &hi);
+                rg[(size_t)t * G + r] = make_int2(lo, hi);
+            }
+        HIPCHK(cp, hipMalloc(&c->d_irange, rg.size() * sizeof(int2)));
+        HIPCHK(cp, hipMemcpy(c->d_irange, rg.data(), rg.size() * sizeof(int2), hipMemcpyHostToDevice));
+        HIPCHK(cp, hipMalloc(&c->d_icount, rg.size() * sizeof(long long)));
+        HIPCHK(cp, hipMalloc(&c->d_ioff, (rg.size() + 1) * sizeof(long long)));
+    }
+    if (const int rc = seq_setup(cp)) return rc;
     *out = c.release();
     return CCJ_OK;
 }
@@ -2473,6 +2405,9 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_ilm);
     hipFree(c->d_dummy);
     hipFree(c->d_items);
+    hipFree(c->d_irange);
+    hipFree(c->d_icount);
+    hipFree(c->d_ioff);
     hipFree(c->d_ilseg);
     hipFree(c->d_ilmseg);
     hipFree(c->d2i);

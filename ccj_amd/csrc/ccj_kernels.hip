@@ -338,14 +338,25 @@ __device__ __forceinline__ unsigned long long rdl64(unsigned long long v, int l)
 
 constexpr int PT_WAVES = 4;  // waves per k_pterm workgroup = consecutive do values sharing jo
 
-__global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngroups) {
+// Grid: one workgroup per (jo, ddc, grp), linear id L = jo*gx + ddc*ngroups + grp.  With xcd = C > 0
+// (CCJ_PTERM_XCD) the dispatch order is remapped so that each XCD (workgroups are dealt round-robin
+// to the 8 XCDs) runs runs of C consecutive L: workgroups of one jo and neighbouring ddc / grp,
+// which read neighbouring rows and straddle the same 128-B lines, share one L2.
+__global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngroups, int gx, int total, int xcd) {
     __shared__ unsigned long long red[PT_WAVES][64];
     const int n = T.n;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int jo = blockIdx.y;
-    const int ddc = blockIdx.x / ngroups;
-    const int grp = blockIdx.x - ddc * ngroups;
+    int L = (int)blockIdx.x;
+    if (xcd) {  // runs of xcd consecutive workgroups per XCD, runs interleaved over the XCDs
+        const int q = L >> 3;
+        L = ((q / xcd) * 8 + (L & 7)) * xcd + q % xcd;
+    }
+    if (L >= total) return;  // whole workgroup
+    const int jo = L / gx;
+    const int bx = L - jo * gx;
+    const int ddc = bx / ngroups;
+    const int grp = bx - ddc * ngroups;
     const int dd0 = jo + 1 + ddc * PT_WAVES;
     if (dd0 > sigma - 2) return;  // whole workgroup
     const int dd = dd0 + w;
@@ -474,6 +485,112 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
     }
     // null tail: dt 63 addresses T.dummy (32767), energy 32767 -> 65534, never below a clamped result
     if (lane < IL_B) ent[cnt + lane] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0u);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_iloop work items, built on the GPU once per sequence (ccj_create / ccj_reset).  One wave of
+// k_iloop per item; an item is a closing pair that can pair plus a 64-lane chunk of the cells that
+// share it (role << 30 | f1 << 20 | f2 << 10 | chunk):
+//   PL (role 0): for a in [max(6,a_lo), a_end), i in [1, m]:   pair (i, i+a),  chunks over h <= m-i
+//   PR (role 1): for a in [a_lo, min(t-6, a_end-1)], q < m:    pair (k, k+t-a), k = q+a+3, chunks over i <= q+1
+//   PM (role 2): for h in [2, m-1], j in [1, n]:               pair (j, k = j+h+2), chunks over a in [alo, ahi]
+// in this enumeration order (measured no slower than heaviest-list-first).  One workgroup per
+// (level t, shard r) walks its "rows" (one closing pair each) 256 at a time; pass 0 counts the
+// items, pass 1 writes them at offs[t*G+r] + an exclusive scan of the row counts.
+// ------------------------------------------------------------------------------------------
+struct ItemRows {
+    int m, aPL0, nPLa, aPR0, nPRa, nPL, nPR, nPM;
+};
+__device__ __forceinline__ ItemRows item_rows(int n, int t, int a_lo, int a_end) {
+    ItemRows R;
+    R.m = n - t - 2;
+    R.aPL0 = imax(6, a_lo);
+    R.nPLa = imax(0, a_end - R.aPL0);
+    R.aPR0 = a_lo;
+    R.nPRa = imax(0, imin(t - 6, a_end - 1) - a_lo + 1);
+    R.nPL = R.nPLa * R.m;
+    R.nPR = R.nPRa * R.m;
+    R.nPM = imax(0, R.m - 2) * n;
+    return R;
+}
+// items of row x and the first of them (chunk 0); 0 when the pair cannot pair
+__device__ __forceinline__ int item_row(const DevTables &T, int t, const ItemRows &R, int x, int a_lo, int a_end,
+                                        uint32_t &it0) {
+    const int n = T.n, m = R.m;
+    if (x < R.nPL) {
+        const int a = R.aPL0 + x / m, i = 1 + x % m;
+        it0 = (0u << 30) | ((uint32_t)a << 20) | ((uint32_t)i << 10);
+        return ptype(T, i, i + a) > 0 ? (m - i) / 64 + 1 : 0;
+    }
+    x -= R.nPL;
+    if (x < R.nPR) {
+        const int a = R.aPR0 + x / m, q = x % m;
+        const int k = q + a + 3, b = t - a;
+        it0 = (1u << 30) | ((uint32_t)a << 20) | ((uint32_t)q << 10);
+        return ptype(T, k, k + b) > 0 ? q / 64 + 1 : 0;
+    }
+    x -= R.nPR;
+    const int h = 2 + x / n, j = 1 + x % n;
+    const int k = j + h + 2;
+    if (k > n) return 0;
+    const int alo = imax(imax(2, t - (n - k)), a_lo), ahi = imin(imin(t - 2, j - 1), a_end - 1);
+    if (alo > ahi || ptype(T, j, k) <= 0) return 0;
+    it0 = (2u << 30) | ((uint32_t)h << 20) | ((uint32_t)j << 10);
+    return (ahi - alo) / 64 + 1;
+}
+
+__global__ __launch_bounds__(256) void k_items(DevTables T, const int2 *__restrict__ range, int G, int rank, int simulate,
+                                               long long *counts, const long long *__restrict__ offs, uint32_t *items,
+                                               int pass) {
+    __shared__ int wsum[4];
+    __shared__ long long tot;
+    const int b = blockIdx.x, t = b / G, r = b - t * G;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const bool mine = simulate || r == rank;
+    if (!mine || t < 4 || t >= T.nlev) {
+        if (pass == 0 && tid == 0) counts[b] = 0;
+        return;  // whole workgroup
+    }
+    const int2 ar = range[b];
+    const ItemRows R = item_rows(T.n, t, ar.x, ar.y);
+    const int nrows = R.nPL + R.nPR + R.nPM;
+    long long base = pass ? offs[b] : 0;
+    for (int c0 = 0; c0 < nrows; c0 += 256) {
+        const int x = c0 + tid;
+        uint32_t it0 = 0;
+        const int cnt = x < nrows ? item_row(T, t, R, x, ar.x, ar.y, it0) : 0;
+        // exclusive scan of cnt over the workgroup: wave scan, then the wave totals
+        int inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        int before = 0;
+        for (int v = 0; v < w; ++v) before += wsum[v];
+        const int chunk_total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (pass) {
+            const long long pos = base + before + inc - cnt;
+            for (int c = 0; c < cnt; ++c) items[pos + c] = it0 | (uint32_t)c;
+        }
+        base += chunk_total;
+        __syncthreads();  // wsum is rewritten by the next chunk
+    }
+    if (pass == 0 && tid == 0) {
+        tot = base;
+        counts[b] = tot;
+    }
+}
+
+extern "C" int ccjk_items(const DevTables *T, const int2 *range, int G, int rank, int simulate, long long *counts,
+                          const long long *offs, uint32_t *items, int pass, void *stream) {
+    const int blocks = T->n * G;
+    if (blocks <= 0) return 0;
+    hipLaunchKernelGGL(k_items, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *T, range, G, rank, simulate,
+                       counts, offs, items, pass);
+    return (int)hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1580,8 +1697,14 @@ extern "C" int ccjk_pterm(const DevTables *T, int sigma, void *stream) {
     if (nint <= 0) return 0;
     const int ngroups = (nint + 63) / 64;
     const int nddc = (sigma - 2 + PT_WAVES - 1) / PT_WAVES;
-    dim3 grid(nddc * ngroups, sigma - 2);
-    hipLaunchKernelGGL(k_pterm, grid, dim3(64 * PT_WAVES), 0, (hipStream_t)stream, *T, sigma, ngroups);
+    static const int xcd = [] {
+        const char *e = getenv("CCJ_PTERM_XCD");
+        return e ? atoi(e) : 4;  // measured: 15% less traffic than plain dispatch order, same time
+    }();
+    const int gx = nddc * ngroups, total = gx * (sigma - 2);
+    const int blocks = xcd ? 8 * xcd * ((total + 8 * xcd - 1) / (8 * xcd)) : total;
+    hipLaunchKernelGGL(k_pterm, dim3((unsigned)blocks), dim3(64 * PT_WAVES), 0, (hipStream_t)stream, *T, sigma, ngroups, gx,
+                       total, xcd);
     return (int)hipGetLastError();
 }
 

@@ -66,7 +66,7 @@ def test_ref_compat_abort_reproduces_stock_n214_abort(tmp_path):
     import random
     r = random.Random(1)
     seq = "".join(r.choice("ACGU") for _ in range(214))
-    par = [c for c in G["cases"] if c["files"]][0]
+    par = [c for c in G["cases"] if c["files"] and c["fold"] and c["rc"] == 0][0]
     name, text = next(iter(par["files"].items()))
     (tmp_path / name).write_text(text)
     env = dict(os.environ, CCJ_REF_COMPAT_ABORT="1")
