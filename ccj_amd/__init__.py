@@ -18,7 +18,7 @@ from typing import Optional
 
 __all__ = [
     "W_final", "ccj", "load_params", "load_par", "ParFileError", "param_path", "CCJError", "BacktrackExit", "lib", "MAT4", "MAT2",
-    "num_cells", "comm_unique_id", "shard_range", "level_layout",
+    "num_cells", "comm_unique_id", "shard_blocks", "level_layout", "LocalGroup",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -126,8 +126,14 @@ def lib() -> ctypes.CDLL:
     L.ccj_comm_unique_id.restype = ip
     L.ccj_comm_init.argtypes = [vp, cp]
     L.ccj_comm_init.restype = ip
-    L.ccj_shard_range.argtypes = [ip, ip, ip, ip, ctypes.POINTER(ip), ctypes.POINTER(ip)]
-    L.ccj_shard_range.restype = ip
+    L.ccj_shard_blocks.argtypes = [ip, ip, ip, ip, ctypes.POINTER(ip), ip]
+    L.ccj_shard_blocks.restype = ip
+    L.ccj_group_create.argtypes = [ip, ctypes.POINTER(vp)]
+    L.ccj_group_create.restype = ip
+    L.ccj_group_destroy.argtypes = [vp]
+    L.ccj_group_destroy.restype = None
+    L.ccj_comm_init_local.argtypes = [vp, vp]
+    L.ccj_comm_init_local.restype = ip
     L.ccj_level_layout.argtypes = [ip, ip, ip, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ip)]
     L.ccj_level_layout.restype = ip
     L.ccj_params_load_par.argtypes = [cp, cp, cp, cp, ip]
@@ -227,10 +233,12 @@ class W_final:
     def __init__(self, seq: str, dangle: int = 2, params: str | bytes = "DirksPierce09",
                  noGU: bool = False, device: int = 0, overlap_d2h: bool = False, shard_world: int = 1,
                  shard_rank: int = 0, shard_simulate: bool = False, comm_id: Optional[bytes] = None,
-                 host_traceback: bool = False, split_target: int = 0, share_splits: int = 0):
+                 host_traceback: bool = False, split_target: int = 0, share_splits: int = 0,
+                 local_group: Optional["LocalGroup"] = None):
         """shard_world > 1: band-shard this one sequence over shard_world processes (one per GPU),
         exchanging each level over RCCL; every rank passes the same comm_id (from comm_unique_id()
-        on one rank).  shard_simulate runs all shards in this process without an exchange.
+        on one rank), or the same local_group when the ranks are contexts of this process.
+        shard_simulate runs all shards in this one context without an exchange.
         host_traceback: run W and the traceback on the host over a mirror of every matrix (the
         reference restatement; overlap_d2h streams that mirror during the fill) instead of on the GPU.
         split_target / share_splits: level-kernel tuning (include/ccj.h ccj_options; 0 = default,
@@ -251,7 +259,10 @@ class W_final:
         if rc != CCJ_OK:
             raise CCJError(rc, L.ccj_last_error(None).decode())
         self._h = h
-        if shard_world > 1 and not shard_simulate:
+        if shard_world > 1 and not shard_simulate and local_group is not None:
+            self._group = local_group  # keeps the group alive as long as this context
+            self._check(L.ccj_comm_init_local(h, local_group._h))
+        elif shard_world > 1 and not shard_simulate:
             if comm_id is None or len(comm_id) != COMM_ID_BYTES:
                 raise CCJError(CCJ_E_ARG, "sharded context needs the 128-byte comm_id of rank 0")
             self._check(L.ccj_comm_init(h, comm_id))
@@ -358,13 +369,40 @@ def comm_unique_id() -> bytes:
     return buf.raw
 
 
-def shard_range(n: int, t: int, world: int, rank: int):
-    """a-blocks [lo, end) of 4-D level t that rank computes in a band-sharded fold (no GPU needed)."""
-    lo, end = ctypes.c_int(), ctypes.c_int()
-    rc = lib().ccj_shard_range(n, t, world, rank, ctypes.byref(lo), ctypes.byref(end))
-    if rc != CCJ_OK:
-        raise CCJError(rc, "bad shard arguments")
-    return lo.value, end.value
+def shard_blocks(n: int, t: int, world: int, rank: int):
+    """a-blocks of 4-D level t that rank computes in a band-sharded fold, ascending (no GPU needed):
+    block a belongs to rank (a // 4) % world on every level (DESIGN.md §7)."""
+    cap = t + 1
+    buf = (ctypes.c_int * max(cap, 1))()
+    cnt = lib().ccj_shard_blocks(n, t, world, rank, buf, cap)
+    if cnt < 0:
+        raise CCJError(-cnt, "bad shard arguments")
+    return list(buf[:cnt])
+
+
+class LocalGroup:
+    """In-process exchange group for a band-sharded fold whose ranks are contexts of this process
+    (include/ccj.h ccj_group): pass it as W_final(..., shard_world=N, shard_rank=r, local_group=g)
+    and drive each rank's fill from its own thread."""
+
+    def __init__(self, world: int):
+        h = ctypes.c_void_p()
+        rc = lib().ccj_group_create(world, ctypes.byref(h))
+        if rc != CCJ_OK:
+            raise CCJError(rc, "ccj_group_create failed")
+        self._h = h
+        self.world = world
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().ccj_group_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def level_layout(n: int, t: int, world: int):

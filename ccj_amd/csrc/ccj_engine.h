@@ -82,6 +82,32 @@ constexpr int SHARE_R = CCJ_SHARE_R;
 constexpr int SHARE_NACC = 4;
 enum AccRec { AI = 0, AJ = 1, AK = 2, AL = 3 };
 
+// Band sharding: a-block a of every level belongs to rank (a / SHARD_GRP) % world,
+// the same rank on every level, so a split-sharing leader (a % SHARE_R == 0) and its followers
+// (a+1 .. a+SHARE_R-1, later levels) always live on one rank.  A rank's blocks are numbered by
+// their "own index" o = 0, 1, ...: a = shard_a(o) ascending.  world = 1: a = o.
+constexpr int SHARD_GRP = SHARE_R;
+__host__ __device__ __forceinline__ int shard_owner(int a, int G) { return (a / SHARD_GRP) % G; }
+__host__ __device__ __forceinline__ int shard_a(int o, int G, int r) {
+    return ((o / SHARD_GRP) * G + r) * SHARD_GRP + o % SHARD_GRP;
+}
+// number of a in [0, x] owned by rank r (x >= -1)
+__host__ __device__ __forceinline__ int shard_count(int x, int G, int r) {
+    const int nb = x + 1, qf = nb / SHARD_GRP, rem = nb % SHARD_GRP;
+    const int full = qf / G + (qf % G > r ? 1 : 0);
+    return full * SHARD_GRP + (qf % G == r ? rem : 0);
+}
+// own index of the first a >= x owned by rank r
+__host__ __device__ __forceinline__ int shard_ceil(int x, int G, int r) {
+    if (x < 0) x = 0;
+    int q = x / SHARD_GRP, off = x % SHARD_GRP;
+    if (q % G != r) {
+        q += ((r - q % G) + G) % G;
+        off = 0;
+    }
+    return (q / G) * SHARD_GRP + off;
+}
+
 struct LvlX {        // per-level bases of the interior-loop copies
     long long lbx;  // element offset of level t in d4x: PLx (C_t elements) then PRx (C_t)
     long long pmb;  // element offset of level t in pmx: m_t * n * (t+1) elements
@@ -137,7 +163,8 @@ struct DevTables {
     int split_target;              // k_level4d: narrow levels split loops so ~this many waves run (0: never)
     int g_lo, g_hi;
     // k_level4d_lead walks only the long-scan a-blocks of a sharing level, longest scan first:
-    // lord[lord_off[t] .. lord_off[t+1]) (device), lord_off_h = the same offsets on the host
+    // rank r's list lord[lord_off[t*G+r] .. lord_off[t*G+r+1]) (device), lord_off_h = the same
+    // offsets on the host
     const int16_t *lord;
     const int *lord_off;
     const int *lord_off_h;
@@ -157,13 +184,15 @@ extern "C" {
 int ccjk_init2d(const ccj::DevTables *T, void *stream);
 int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
 int ccjk_build_il(const ccj::DevTables *T, void *stream);
-int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, int a_lo, int a_end, void *stream);
+int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, int G, int rank, void *stream);
 int ccjk_diag2d(const ccj::DevTables *T, int sigma, void *stream);
-int ccjk_level4d(const ccj::DevTables *T, int t, int a_lo, int a_end, int copies, void *stream);
-int ccjk_level_split(int n, int t, int a_lo, int a_end, int split_target);
-int ccjk_level4d_lead(const ccj::DevTables *T, int t, void *stream);
-int ccjk_copies(const ccj::DevTables *T, int t, int a_lo, int a_end, void *stream);
+int ccjk_level4d(const ccj::DevTables *T, int t, int G, int rank, int copies, void *stream);
+int ccjk_level_split(int n, int t, int nblk, int split_target);
+int ccjk_level4d_lead(const ccj::DevTables *T, int t, int G, int rank, void *stream);
+int ccjk_pack(const ccj::DevTables *T, int t, int G, int r, int nmax, int16_t *send, void *stream);
+int ccjk_unpack(const ccj::DevTables *T, int t, int G, int r, int nmax, const int16_t *recv, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
-int ccjk_items(const ccj::DevTables *T, const int2 *range, int G, int rank, int simulate, long long *counts,
-               const long long *offs, uint32_t *items, int pass, void *stream);
+int ccjk_canon(const ccj::DevTables *T, int x, const long long *offij, int16_t *out, void *stream);
+int ccjk_items(const ccj::DevTables *T, int G, int rank, int simulate, long long *counts, const long long *offs,
+               uint32_t *items, int pass, void *stream);
 }

@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -53,6 +55,36 @@ struct DevBuf {
 
 }  // namespace
 
+// In-process stand-in for the RCCL communicator (tests): world contexts, one host
+// thread each, exchange through device-to-device copies with a host barrier around every level.
+struct ccj_group {
+    int world = 1;
+    std::vector<ccj_ctx *> members;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    long gen = 0;
+    bool broken = false;
+    // false when a member gave up (error or 120 s without the others)
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (broken) return false;
+        const long g = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; }) || broken) {
+            broken = true;
+            cv.notify_all();
+            return false;
+        }
+        return true;
+    }
+};
+
 struct ccj_ctx {
     // problem
     int n = 0;
@@ -78,7 +110,6 @@ struct ccj_ctx {
     // kernel family launch (k_diag2d, k_iloop, the level span).  The markers of mode 2 are barrier
     // packets on the streams and cost ~3 ms per n=200 fill, so the default is 1.
     int level_timing = 1;
-    bool lead_same_stream = true;           // leaders after the plain launch on st (CCJ_LEAD_SAME_STREAM=0: own stream)
     ncclComm_t comm = nullptr;
 
     // layout
@@ -111,7 +142,9 @@ struct ccj_ctx {
     int16_t *d_dummy = nullptr;
     uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
     size_t items_cap = 0;
-    int2 *d_irange = nullptr;             // [t*world + r]: the a-blocks shard r computes at level t
+    int16_t *d_send = nullptr, *d_recv = nullptr;  // band-sharded exchange: own slice, world slices
+    std::vector<int> xnmax;               // per level: the largest rank's block count (slice = 22 x nmax x M)
+    ccj_group *lgroup = nullptr;          // in-process exchange between contexts (tests), else RCCL
     long long *d_icount = nullptr, *d_ioff = nullptr;  // k_items: items per (t, r), first item
     std::vector<long long> it_off;        // first item of (level t, shard r) at t*world + r
     uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
@@ -124,8 +157,6 @@ struct ccj_ctx {
     std::vector<unsigned long long> h_pk;
     int8_t *d_vt = nullptr;
     hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr, st_il = nullptr, st_d = nullptr;
-    hipStream_t st_lead = nullptr;   // k_level4d_lead: split-point-sharing leaders of the level
-    std::vector<hipEvent_t> ld_done, pl_done;  // k_level4d_lead(t) / k_level4d(t) finished
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<double> lev_ms_v, diag_ms_v, il_ms_v;
     std::vector<hipEvent_t> il_done, dg_done;  // k_iloop(t) / k_diag2d(sigma) finished
@@ -139,7 +170,7 @@ struct ccj_ctx {
     std::vector<int> h2i;     // same 9 arrays
     std::vector<int8_t> hvt;
     std::vector<int> hpt_h;   // pair type table [w][p] host copy (int)
-    bool filled = false, mirrored = false;
+    bool filled = false, mirrored = false, mirrored2d = false;
     std::vector<int> W;
 
     double fill_ms = 0, level_ms = 0, diag_ms = 0, pre_ms = 0, il_ms = 0;
@@ -1369,6 +1400,21 @@ extern "C" uint64_t ccj_num_cells(int n) {
 
 static thread_local std::string g_create_err;
 
+// The exchange of one level through the in-process group: every member pulls each member's
+// packed slice into its own receive buffer (same device), between two barriers, so no slice is
+// overwritten by the next level's pack before every member has read it.
+static int local_allgather(ccj_ctx *c, size_t slice) {
+    ccj_group *g = c->lgroup;
+    HIPCHK(c, hipStreamSynchronize(c->st));  // own slice packed
+    if (!g->barrier()) return set_err(c, CCJ_E_STATE, "local exchange: a group member failed");
+    for (int r = 0; r < g->world; ++r)
+        HIPCHK(c, hipMemcpyAsync(c->d_recv + (size_t)r * slice, g->members[r]->d_send, slice * sizeof(int16_t),
+                                 hipMemcpyDeviceToDevice, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    if (!g->barrier()) return set_err(c, CCJ_E_STATE, "local exchange: a group member failed");
+    return CCJ_OK;
+}
+
 // Everything that depends on the sequence itself (not only on n): the encoding, the pair-type,
 // hairpin and e_stP tables, and the k_iloop work items.  ccj_create runs it once, ccj_reset for
 // each new sequence of the same length (the allocations are reused).
@@ -1427,7 +1473,7 @@ static int seq_setup(ccj_ctx *c) {
         if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
         const int G = c->world;
         const int nb = n * G;
-        HIPCHK(cp, (hipError_t)ccjk_items(&c->T, c->d_irange, G, c->rank, c->simulate, c->d_icount, nullptr, nullptr, 0, c->st));
+        HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, nullptr, nullptr, 0, c->st));
         std::vector<long long> cnt((size_t)nb);
         HIPCHK(cp, hipMemcpyAsync(cnt.data(), c->d_icount, nb * sizeof(long long), hipMemcpyDeviceToHost, c->st));
         HIPCHK(cp, hipStreamSynchronize(c->st));
@@ -1443,8 +1489,7 @@ static int seq_setup(ccj_ctx *c) {
         }
         c->T.items = c->d_items;
         HIPCHK(cp, hipMemcpyAsync(c->d_ioff, c->it_off.data(), (nb + 1) * sizeof(long long), hipMemcpyHostToDevice, c->st));
-        HIPCHK(cp, (hipError_t)ccjk_items(&c->T, c->d_irange, G, c->rank, c->simulate, c->d_icount, c->d_ioff, c->d_items, 1,
-                                          c->st));
+        HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, c->d_ioff, c->d_items, 1, c->st));
         // the fill's first launches are on st too (k_iloop waits for ev_pre, recorded on st)
     }
     HIPCHK(cp, hipMemcpy(c->d_hp, hp.data(), plane * sizeof(int), hipMemcpyHostToDevice));
@@ -1452,7 +1497,7 @@ static int seq_setup(ccj_ctx *c) {
     HIPCHK(cp, hipMemcpy(c->d_S, c->S.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
     HIPCHK(cp, hipMemcpy(c->d_S1, c->S1.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
     lap("upload");
-    c->filled = c->mirrored = false;
+    c->filled = c->mirrored = c->mirrored2d = false;
     return CCJ_OK;
 }
 
@@ -1471,8 +1516,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         const char *e = getenv("CCJ_SPLIT_TARGET");
         c->split_target = e ? atoi(e) : 6144;
         if (opts && opts->split_target) c->split_target = opts->split_target < 0 ? 0 : opts->split_target;
-        const char *ls = getenv("CCJ_LEAD_SAME_STREAM");
-        c->lead_same_stream = !(ls && atoi(ls) == 0);
         const char *lt = getenv("CCJ_LEVEL_TIMING");
         if (lt) c->level_timing = std::max(0, std::min(2, atoi(lt)));
         const char *g = getenv("CCJ_SHARE_SPLITS");
@@ -1515,7 +1558,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         if (m > 0) {
             long long C = 0;
             ccj_level_layout(n, t, c->world, &C, &L.M);
-            L.C = (int)C;  // padded to world equal a-chunks when sharded
+            L.C = (int)C;
             c->nlev = t + 1;
         }
         c->lv_off[t] = off;
@@ -1523,7 +1566,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         off += (int64_t)NMAT4 * L.C;
     }
     c->total4 = off;
-    if (c->world == 1 && (uint64_t)off != (uint64_t)NMAT4 * ccj_num_cells(n))
+    if ((uint64_t)off != (uint64_t)NMAT4 * ccj_num_cells(n))
         return set_err(c.get(), CCJ_E_ARG, "layout size mismatch");
 
     ccj_ctx *cp = c.get();
@@ -1533,11 +1576,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_p, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_il, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_d, hipStreamNonBlocking));
-    HIPCHK(cp, hipStreamCreateWithFlags(&c->st_lead, hipStreamNonBlocking));
-    c->ld_done.resize(n + 1);
-    for (auto &e : c->ld_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    c->pl_done.resize(n + 1);
-    for (auto &e : c->pl_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->il_done.resize(n + 1);
     for (auto &e : c->il_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->dg_done.resize(n + 1);
@@ -1564,18 +1602,18 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     // and its followers run one cell per lane) and the partial-record ring
     int g_lo = 0, g_hi = 0;
     long long accC = 0;
-    if (c->share && c->world == 1) {
+    if (c->share) {
         // from the first level that runs unsplit to the last level: the narrow early levels keep
         // their split loops (short scans); on the narrow late levels k_level4d_lead splits the long
         // scans like the level heuristic would (ccjk_level4d_lead).  CCJ_SHARE_LATE=0 limits
         // sharing to the unsplit middle levels (measured 0.6 ms slower at n=200).
         g_lo = -1;
         for (int t = 0; t < c->nlev && g_lo < 0; ++t)
-            if (ccjk_level_split(n, t, 0, t + 1, c->split_target) == 1) g_lo = t;
+            if (ccjk_level_split(n, t, t + 1, c->split_target) == 1) g_lo = t;
         if (g_lo < 0 || (getenv("CCJ_SHARE_LATE") && atoi(getenv("CCJ_SHARE_LATE")) == 0)) {
             g_hi = g_lo < 0 ? 0 : g_lo;
             for (int t = std::max(g_lo, 0); g_lo >= 0 && t < c->nlev; ++t)
-                if (ccjk_level_split(n, t, 0, t + 1, c->split_target) == 1 && g_hi == t) g_hi = t + 1;
+                if (ccjk_level_split(n, t, t + 1, c->split_target) == 1 && g_hi == t) g_hi = t + 1;
             if (g_lo < 0) g_lo = 0;
         } else {
             g_hi = c->nlev;
@@ -1585,15 +1623,19 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     if (g_hi > g_lo && !(getenv("CCJ_LEAD_ORDER") && atoi(getenv("CCJ_LEAD_ORDER")) == 0)) {
         // the a-blocks k_level4d_lead runs on each sharing level (a leader or a full scan on either
         // side; the roles of level4d_body), ordered by scan cost, longest first, so the longest
-        // waves do not start last.  A leader step costs about 2.5 plain steps.
+        // waves do not start last.  A leader step costs about 2.5 plain steps.  One list per
+        // (level t, rank r) at t*world + r: the rank's own blocks (ccj_engine.h shard_owner).
         std::vector<int16_t> lord;
-        c->lord_off.assign((size_t)n + 1, 0);
+        const int G = c->world;
+        c->lord_off.assign((size_t)n * G + 1, 0);
         std::vector<std::pair<double, int>> blk;
-        for (int t = 0; t < n; ++t) {
-            c->lord_off[t] = (int)lord.size();
+        for (int tr = 0; tr < n * G; ++tr) {
+            const int t = tr / G, r = tr % G;
+            c->lord_off[tr] = (int)lord.size();
             if (t < g_lo || t >= g_hi) continue;
             blk.clear();
             for (int a = 0; a <= t; ++a) {
+                if (shard_owner(a, G) != r) continue;
                 const int b = t - a, ra = a % SHARE_R, rb = b % SHARE_R;
                 const int ar = b >= SHARE_R - 1 ? (ra == 0 ? 1 : (t - ra >= g_lo ? 2 : 0)) : 0;
                 const int br = a >= SHARE_R - 1 ? (rb == 0 ? 1 : (t - rb >= g_lo ? 2 : 0)) : 0;
@@ -1604,7 +1646,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
             std::stable_sort(blk.begin(), blk.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
             for (auto &e : blk) lord.push_back((int16_t)e.second);
         }
-        c->lord_off[n] = (int)lord.size();
+        c->lord_off[(size_t)n * G] = (int)lord.size();
         HIPCHK(cp, hipMalloc(&c->d_lord, std::max<size_t>(lord.size(), 1) * sizeof(int16_t)));
         HIPCHK(cp, hipMalloc(&c->d_lord_off, c->lord_off.size() * sizeof(int)));
         if (!lord.empty())
@@ -1757,19 +1799,24 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.lord_off_h = c->lord_off.empty() ? nullptr : c->lord_off.data();
     T.accC = accC;
     {
-        // shard ranges of the k_iloop work items, [t*world + r] (sequence-independent)
         const int G = c->world;
-        std::vector<int2> rg((size_t)n * G);
-        for (int t = 0; t < n; ++t)
-            for (int r = 0; r < G; ++r) {
-                int lo = 0, hi = 0;
-                ccj_shard_range(n, t, G, r, &lo, &hi);
-                rg[(size_t)t * G + r] = make_int2(lo, hi);
+        HIPCHK(cp, hipMalloc(&c->d_icount, (size_t)n * G * sizeof(long long)));
+        HIPCHK(cp, hipMalloc(&c->d_ioff, ((size_t)n * G + 1) * sizeof(long long)));
+        if (G > 1 && !c->simulate) {
+            // exchange slices: per level, 22 matrices x the largest rank's blocks x M
+            c->xnmax.assign(n, 0);
+            size_t slice = 0;
+            for (int t = 0; t < c->nlev; ++t) {
+                int nm = 0;
+                for (int r = 0; r < G; ++r) nm = std::max(nm, shard_count(t, G, r));
+                c->xnmax[t] = nm;
+                slice = std::max(slice, (size_t)NMAT4 * nm * c->lv_host[t].M);
             }
-        HIPCHK(cp, hipMalloc(&c->d_irange, rg.size() * sizeof(int2)));
-        HIPCHK(cp, hipMemcpy(c->d_irange, rg.data(), rg.size() * sizeof(int2), hipMemcpyHostToDevice));
-        HIPCHK(cp, hipMalloc(&c->d_icount, rg.size() * sizeof(long long)));
-        HIPCHK(cp, hipMalloc(&c->d_ioff, (rg.size() + 1) * sizeof(long long)));
+            if (hipMalloc(&c->d_send, std::max<size_t>(slice, 1) * sizeof(int16_t)) != hipSuccess ||
+                hipMalloc(&c->d_recv, std::max<size_t>(slice * G, 1) * sizeof(int16_t)) != hipSuccess)
+                return set_err(cp, CCJ_E_OOM, "device allocation of the exchange buffers (%.2f GB) failed",
+                               slice * (G + 1) * 2e-9);
+        }
     }
     if (const int rc = seq_setup(cp)) return rc;
     *out = c.release();
@@ -1803,7 +1850,7 @@ extern "C" int ccj_reset(ccj_ctx *c, const char *seq) {
             return set_err(c, CCJ_E_ARG, "ccj_reset: invalid character in sequence");
     HIPCHK(c, hipSetDevice(c->device));
     // the previous fold's streams may still read the sequence tables
-    for (hipStream_t q : {c->st, c->st_copy, c->st_p, c->st_il, c->st_d, c->st_lead}) HIPCHK(c, hipStreamSynchronize(q));
+    for (hipStream_t q : {c->st, c->st_copy, c->st_p, c->st_il, c->st_d}) HIPCHK(c, hipStreamSynchronize(q));
     c->seq = s;
     c->W.clear();
     return seq_setup(c);
@@ -1816,7 +1863,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     hipStream_t st = c->st;
     const auto enq0 = std::chrono::steady_clock::now();
     const size_t plane = (size_t)(n + 1) * c->rs;
-    c->filled = c->mirrored = false;
+    c->filled = c->mirrored = c->mirrored2d = false;
     HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), st));
     HIPCHK(c, hipEventRecord(c->ev_start, st));
     HIPCHK(c, (hipError_t)ccjk_init2d(&c->T, st));
@@ -1846,12 +1893,10 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
             if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 3], 0));
             HIPCHK(c, trec(2, c->st_il));
             const int G = c->world;
-            for (int r = 0; r < G; ++r) {
+            for (int r = 0; r < G; ++r) {  // every rank's launches in simulation, else this rank's
                 if (!c->simulate && r != c->rank) continue;
-                int lo = 0, hi = 0;
-                ccj_shard_range(n, s, G, r, &lo, &hi);
                 const size_t tr = (size_t)s * G + r;
-                HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[tr], (int)(c->it_off[tr + 1] - c->it_off[tr]), lo, hi,
+                HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[tr], (int)(c->it_off[tr + 1] - c->it_off[tr]), G, r,
                                                  c->st_il));
             }
             HIPCHK(c, trec(3, c->st_il));
@@ -1859,52 +1904,31 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
             HIPCHK(c, hipStreamWaitEvent(st, c->il_done[s], 0));
             if (s >= 1) HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s - 1], 0));
             HIPCHK(c, trec(4, st));
+            // the level: its plain launch, then (sharing levels) the leaders on the same stream, no
+            // cross-stream hop between the two launches or between levels
             for (int r = 0; r < G; ++r) {
                 if (!c->simulate && r != c->rank) continue;
-                int lo = 0, hi = 0;
-                ccj_shard_range(n, s, G, r, &lo, &hi);
-                HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, lo, hi, G == 1 ? 1 : 0, st));
+                HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, G, r, 1, st));
             }
-            if (!c->lead_same_stream) HIPCHK(c, hipEventRecord(c->pl_done[s], st));
-            if (s >= c->T.g_lo && s < c->T.g_hi && c->lead_same_stream) {
-                // leaders right after the plain launch on the same stream: no cross-stream hop
-                // between the two launches of a level or between levels (measured faster than
-                // running them concurrently on st_lead)
-                HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, st));
-            } else if (s >= c->T.g_lo && s < c->T.g_hi) {
-                // CCJ_LEAD_SAME_STREAM=0: leaders on their own stream, same inputs as the level kernel (level s-1 complete,
-                // k_iloop(s), k_diag2d(s-1)); the level is done when both launches are.  Level s-1
-                // is waited for as its plain launch (pl_done) plus, in stream order, its leaders
-                // (st_lead), not as the joined lev_done, which would put a second cross-stream hop
-                // between two leader launches.
-                HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->il_done[s], 0));
-                if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->dg_done[s - 1], 0));
-                if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->pl_done[s - 1], 0));
-                if (s - 1 >= c->T.g_hi || s - 1 < c->T.g_lo) {  // level s-1 had no leader launch on st_lead
-                    if (s >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->lev_done[s - 1], 0));
-                    else HIPCHK(c, hipStreamWaitEvent(c->st_lead, c->ev_pre, 0));
-                }
-                HIPCHK(c, trec(6, c->st_lead));
-                HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, c->st_lead));
-                HIPCHK(c, hipEventRecord(c->ld_done[s], c->st_lead));
-                HIPCHK(c, hipStreamWaitEvent(st, c->ld_done[s], 0));
+            for (int r = 0; r < G; ++r) {
+                if (!c->simulate && r != c->rank) continue;
+                HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, G, r, st));
             }
-            if (G > 1) {
-                if (!c->simulate) {
-                    // in-place all-gather of the level: per matrix, rank r owns chunk r of C_t
+            if (G > 1 && !c->simulate) {
+                // band-sharded exchange: this rank's cells of the level, all 22
+                // matrices, packed into one slice; ONE all-gather of equal slices; the other ranks'
+                // cells unpacked with their loop records and interior-loop copies
+                const int nmax = c->xnmax[s];
+                const size_t slice = (size_t)NMAT4 * nmax * c->lv_host[s].M;
+                HIPCHK(c, (hipError_t)ccjk_pack(&c->T, s, G, c->rank, nmax, c->d_send, st));
+                if (c->lgroup) {
+                    if (const int rc = local_allgather(c, slice)) return rc;
+                } else {
                     if (!c->comm) return set_err(c, CCJ_E_STATE, "sharded context without ccj_comm_init");
-                    const LevelDesc &L = c->lv_host[s];
-                    const size_t chunk = (size_t)L.C / G;
-                    if (ncclGroupStart() != ncclSuccess) return set_err(c, CCJ_E_HIP, "ncclGroupStart failed");
-                    for (int x = 0; x < NMAT4; ++x) {
-                        int16_t *base = c->d4 + c->lv_off[s] + (size_t)x * L.C;
-                        if (ncclAllGather(base + chunk * c->rank, base, chunk * sizeof(int16_t), ncclInt8, c->comm, st) !=
-                            ncclSuccess)
-                            return set_err(c, CCJ_E_HIP, "ncclAllGather failed at level %d", s);
-                    }
-                    if (ncclGroupEnd() != ncclSuccess) return set_err(c, CCJ_E_HIP, "ncclGroupEnd failed");
+                    if (ncclAllGather(c->d_send, c->d_recv, slice * sizeof(int16_t), ncclInt8, c->comm, st) != ncclSuccess)
+                        return set_err(c, CCJ_E_HIP, "ncclAllGather failed at level %d", s);
                 }
-                HIPCHK(c, (hipError_t)ccjk_copies(&c->T, s, 0, s + 1, st));
+                HIPCHK(c, (hipError_t)ccjk_unpack(&c->T, s, G, c->rank, nmax, c->d_recv, st));
             }
             HIPCHK(c, trec(5, st));
             HIPCHK(c, hipEventRecord(c->lev_done[s], st));
@@ -1967,15 +1991,8 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
             HIPCHK(c, hipEventElapsedTime(&ms, ev[2], ev[3]));
             isum += ms;
             c->il_ms_v[s] = ms;
-            // the level's span: from the first of its two launches to the join (ev[6] = leaders)
-            float t4 = 0, t5 = 0, t6 = 0;
-            HIPCHK(c, hipEventElapsedTime(&t4, c->ev_start, ev[4]));
-            HIPCHK(c, hipEventElapsedTime(&t5, c->ev_start, ev[5]));
-            if (s >= c->T.g_lo && s < c->T.g_hi && !c->lead_same_stream) {
-                HIPCHK(c, hipEventElapsedTime(&t6, c->ev_start, ev[6]));
-                t4 = std::min(t4, t6);
-            }
-            ms = t5 - t4;
+            // the level's span: from its first launch to its last (exchange included when sharded)
+            HIPCHK(c, hipEventElapsedTime(&ms, ev[4], ev[5]));
             lsum += ms;
             c->lev_ms_v[s] = ms;
         }
@@ -2024,6 +2041,18 @@ namespace {
 int ensure_mirror(const ccj_ctx *cc) {
     ccj_ctx *c = const_cast<ccj_ctx *>(cc);
     return c->mirrored ? CCJ_OK : ccj_sync_host(c);
+}
+
+// only the 2-D arrays (no 4-D copy): what ccj_get2 needs
+int ensure_mirror_2d(const ccj_ctx *cc) {
+    ccj_ctx *c = const_cast<ccj_ctx *>(cc);
+    if (c->mirrored || c->mirrored2d) return CCJ_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t plane = (size_t)(c->n + 1) * c->rs;
+    HIPCHK(c, hipMemcpy(c->h2i.data(), c->d2i, A2_N * plane * sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(c->hvt.data(), c->d_vt, plane, hipMemcpyDeviceToHost));
+    c->mirrored2d = true;
+    return CCJ_OK;
 }
 
 // W + traceback on the GPU (ccj_backtrack.hip); brackets on the host
@@ -2126,7 +2155,7 @@ extern "C" int ccj_get4(const ccj_ctx *c, int mat, int i, int j, int k, int l) {
 }
 
 extern "C" int ccj_get2(const ccj_ctx *c, int mat, int i, int j) {
-    if (!c || !c->filled || ensure_mirror(c) || i < 1 || j > c->n || i > j) return INF;
+    if (!c || !c->filled || ensure_mirror_2d(c) || i < 1 || j > c->n || i > j) return INF;
     switch (mat) {
         case CCJ_M2_P: return c->raw2(A2_P, i, j);
         case CCJ_M2_WBP: return c->raw2(A2_WBP, i, j);
@@ -2145,20 +2174,65 @@ extern "C" int ccj_getW(const ccj_ctx *c, int j) {
     return c->W[j];
 }
 
-extern "C" int ccj_hashes(const ccj_ctx *c, uint64_t *out) {
-    if (!c || !c->filled || !out || ensure_mirror(c)) return CCJ_E_STATE;
+extern "C" int ccj_hashes(const ccj_ctx *cc, uint64_t *out) {
+    if (!cc || !cc->filled || !out) return CCJ_E_STATE;
+    ccj_ctx *c = const_cast<ccj_ctx *>(cc);
     const int n = c->n;
     const uint64_t H0 = 1469598103934665603ull;
-    for (int m = 0; m < NMAT4; ++m) {
-        uint64_t h = H0;
+    // 4-D: each matrix is rewritten in canonical (i,j,k,l) order on the GPU (k_canon), copied back,
+    // and FNV-hashed on host threads (one chain per matrix)
+    const size_t cells = (size_t)ccj_num_cells(n);
+    if (cells > 0) {
+        HIPCHK(c, hipSetDevice(c->device));
+        std::vector<long long> offij((size_t)(n + 1) * (n + 1), 0);
+        long long pos = 0;
         for (int i = 1; i <= n; ++i)
-            for (int j = i; j <= n; ++j)
-                for (int k = j + 2; k <= n; ++k)
-                    for (int l = k; l <= n; ++l) {
-                        const int16_t v = (int16_t)ccj_get4(c, m, i, j, k, l);
-                        h = fnv(h, &v, 2);
-                    }
-        out[m] = h;
+            for (int j = i; j <= n; ++j) {
+                offij[(size_t)i * (n + 1) + j] = pos;
+                for (int k = j + 2; k <= n; ++k) pos += n - k + 1;
+            }
+        long long *d_off = nullptr;
+        int16_t *d_canon = nullptr;
+        HIPCHK(c, hipMalloc(&d_off, offij.size() * sizeof(long long)));
+        if (hipMalloc(&d_canon, cells * sizeof(int16_t)) != hipSuccess) {
+            hipFree(d_off);
+            return set_err(c, CCJ_E_OOM, "ccj_hashes: device scratch of %.2f GB", cells * 2e-9);
+        }
+        HIPCHK(c, hipMemcpy(d_off, offij.data(), offij.size() * sizeof(long long), hipMemcpyHostToDevice));
+        std::vector<std::vector<int16_t>> host(NMAT4);
+        std::vector<std::thread> th;
+        int rc = CCJ_OK;
+        for (int m = 0; m < NMAT4 && rc == CCJ_OK; ++m) {
+            host[m].resize(cells);
+            if (ccjk_canon(&c->T, m, d_off, d_canon, c->st) != 0 ||
+                hipMemcpyAsync(host[m].data(), d_canon, cells * sizeof(int16_t), hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+                hipStreamSynchronize(c->st) != hipSuccess) {
+                rc = set_err(c, CCJ_E_HIP, "ccj_hashes: canonical copy of matrix %d failed", m);
+                break;
+            }
+            th.emplace_back([&host, out, m, H0] {
+                out[m] = fnv(H0, host[m].data(), host[m].size() * sizeof(int16_t));
+                std::vector<int16_t>().swap(host[m]);
+            });
+        }
+        for (auto &x : th) x.join();
+        hipFree(d_off);
+        hipFree(d_canon);
+        if (rc != CCJ_OK) return rc;
+        if (ensure_mirror_2d(c)) return CCJ_E_STATE;
+    } else {
+        if (ensure_mirror(c)) return CCJ_E_STATE;
+        for (int m = 0; m < NMAT4; ++m) {
+            uint64_t h = H0;
+            for (int i = 1; i <= n; ++i)
+                for (int j = i; j <= n; ++j)
+                    for (int k = j + 2; k <= n; ++k)
+                        for (int l = k; l <= n; ++l) {
+                            const int16_t v = (int16_t)ccj_get4(c, m, i, j, k, l);
+                            h = fnv(h, &v, 2);
+                        }
+            out[m] = h;
+        }
     }
     for (int m = 0; m < CCJ_NMAT2; ++m) {
         uint64_t h = H0;
@@ -2325,21 +2399,19 @@ extern "C" int ccj_set_timing(ccj_ctx *c, int mode) {
     return CCJ_OK;
 }
 
-extern "C" int ccj_shard_range(int n, int t, int world, int rank, int *a_lo, int *a_end) {
-    if (!a_lo || !a_end || world < 1 || rank < 0 || rank >= world || t < 0) return CCJ_E_ARG;
+extern "C" int ccj_shard_blocks(int n, int t, int world, int rank, int *a_out, int cap) {
+    if (world < 1 || rank < 0 || rank >= world || t < 0 || (cap > 0 && !a_out)) return -CCJ_E_ARG;
     (void)n;
-    const int B = (t + 1 + world - 1) / world;  // a-blocks per shard (the last one may be short)
-    *a_lo = std::min(rank * B, t + 1);
-    *a_end = std::min((rank + 1) * B, t + 1);
-    return CCJ_OK;
+    const int cnt = shard_count(t, world, rank);
+    for (int o = 0; o < cnt && o < cap; ++o) a_out[o] = shard_a(o, world, rank);
+    return cnt;
 }
 
 extern "C" int ccj_level_layout(int n, int t, int world, long long *C, int *M) {
     if (!C || !M || world < 1 || t < 0) return CCJ_E_ARG;
     const int m = n - t - 2;
     *M = m > 0 ? m * (m + 1) / 2 : 0;
-    const long long B = world == 1 ? t + 1 : (long long)((t + 1 + world - 1) / world) * world;
-    *C = B * *M;
+    *C = (long long)(t + 1) * *M;  // unpadded for every world (the exchange packs slices)
     return CCJ_OK;
 }
 
@@ -2365,6 +2437,24 @@ extern "C" int ccj_comm_init(ccj_ctx *c, const char *id_in) {
     return CCJ_OK;
 }
 
+extern "C" int ccj_group_create(int world, ccj_group **out) {
+    if (!out || world < 1) return CCJ_E_ARG;
+    *out = new ccj_group();
+    (*out)->world = world;
+    (*out)->members.assign(world, nullptr);
+    return CCJ_OK;
+}
+
+extern "C" void ccj_group_destroy(ccj_group *g) { delete g; }
+
+extern "C" int ccj_comm_init_local(ccj_ctx *c, ccj_group *g) {
+    if (!c || !g || g->world != c->world || c->world < 2 || c->simulate) return CCJ_E_ARG;
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->members[c->rank] = c;
+    c->lgroup = g;
+    return CCJ_OK;
+}
+
 extern "C" int ccj_n(const ccj_ctx *c) { return c ? c->n : 0; }
 extern "C" const char *ccj_last_error(const ccj_ctx *c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
@@ -2376,7 +2466,6 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->st_p) hipStreamSynchronize(c->st_p);
     if (c->st_il) hipStreamSynchronize(c->st_il);
     if (c->st_d) hipStreamSynchronize(c->st_d);
-    if (c->st_lead) hipStreamSynchronize(c->st_lead);
     hipFree(c->d4);
     hipFree(c->d_ie);
     hipFree(c->d_est);
@@ -2405,7 +2494,8 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_ilm);
     hipFree(c->d_dummy);
     hipFree(c->d_items);
-    hipFree(c->d_irange);
+    hipFree(c->d_send);
+    hipFree(c->d_recv);
     hipFree(c->d_icount);
     hipFree(c->d_ioff);
     hipFree(c->d_ilseg);
@@ -2424,9 +2514,6 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->st_il) hipStreamDestroy(c->st_il);
     if (c->st_d) hipStreamDestroy(c->st_d);
-    if (c->st_lead) hipStreamDestroy(c->st_lead);
-    for (auto e : c->ld_done) hipEventDestroy(e);
-    for (auto e : c->pl_done) hipEventDestroy(e);
     for (auto e : c->il_done) hipEventDestroy(e);
     for (auto e : c->dg_done) hipEventDestroy(e);
     for (auto e : c->tev) hipEventDestroy(e);

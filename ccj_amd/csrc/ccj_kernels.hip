@@ -491,40 +491,46 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
 // k_iloop work items, built on the GPU once per sequence (ccj_create / ccj_reset).  One wave of
 // k_iloop per item; an item is a closing pair that can pair plus a 64-lane chunk of the cells that
 // share it (role << 30 | f1 << 20 | f2 << 10 | chunk):
-//   PL (role 0): for a in [max(6,a_lo), a_end), i in [1, m]:   pair (i, i+a),  chunks over h <= m-i
-//   PR (role 1): for a in [a_lo, min(t-6, a_end-1)], q < m:    pair (k, k+t-a), k = q+a+3, chunks over i <= q+1
-//   PM (role 2): for h in [2, m-1], j in [1, n]:               pair (j, k = j+h+2), chunks over a in [alo, ahi]
+//   PL (role 0): for own a in [6, t], i in [1, m]:   pair (i, i+a),  chunks over h <= m-i
+//   PR (role 1): for own a in [0, t-6], q < m:        pair (k, k+t-a), k = q+a+3, chunks over i <= q+1
+//   PM (role 2): for h in [2, m-1], j in [1, n]:      pair (j, k = j+h+2), chunks over the own a in [alo, ahi]
+// ("own": the rank's a-blocks, ccj_engine.h shard_a; every a when unsharded)
 // in this enumeration order (measured no slower than heaviest-list-first).  One workgroup per
 // (level t, shard r) walks its "rows" (one closing pair each) 256 at a time; pass 0 counts the
 // items, pass 1 writes them at offs[t*G+r] + an exclusive scan of the row counts.
 // ------------------------------------------------------------------------------------------
 struct ItemRows {
-    int m, aPL0, nPLa, aPR0, nPRa, nPL, nPR, nPM;
+    int m, oPL0, nPLa, nPRa, nPL, nPR, nPM;
 };
-__device__ __forceinline__ ItemRows item_rows(int n, int t, int a_lo, int a_end) {
+// rows of level t for rank r of G (its own a-blocks, ccj_engine.h shard_a)
+__device__ __forceinline__ ItemRows item_rows(int n, int t, int G, int r) {
     ItemRows R;
     R.m = n - t - 2;
-    R.aPL0 = imax(6, a_lo);
-    R.nPLa = imax(0, a_end - R.aPL0);
-    R.aPR0 = a_lo;
-    R.nPRa = imax(0, imin(t - 6, a_end - 1) - a_lo + 1);
+    R.oPL0 = shard_ceil(6, G, r);
+    R.nPLa = imax(0, shard_count(t, G, r) - R.oPL0);
+    R.nPRa = t >= 6 ? shard_count(t - 6, G, r) : 0;
     R.nPL = R.nPLa * R.m;
     R.nPR = R.nPRa * R.m;
     R.nPM = imax(0, R.m - 2) * n;
     return R;
 }
+// rank r's a-blocks of a PM pair (j, k = j+h+2) at level t: own indices [o0, o1]
+__device__ __forceinline__ void pm_own_range(int n, int t, int j, int k, int G, int r, int &o0, int &o1) {
+    const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, j - 1);
+    o0 = shard_ceil(alo, G, r);
+    o1 = ahi >= alo ? shard_count(ahi, G, r) - 1 : o0 - 1;
+}
 // items of row x and the first of them (chunk 0); 0 when the pair cannot pair
-__device__ __forceinline__ int item_row(const DevTables &T, int t, const ItemRows &R, int x, int a_lo, int a_end,
-                                        uint32_t &it0) {
+__device__ __forceinline__ int item_row(const DevTables &T, int t, const ItemRows &R, int x, int G, int r, uint32_t &it0) {
     const int n = T.n, m = R.m;
     if (x < R.nPL) {
-        const int a = R.aPL0 + x / m, i = 1 + x % m;
+        const int a = shard_a(R.oPL0 + x / m, G, r), i = 1 + x % m;
         it0 = (0u << 30) | ((uint32_t)a << 20) | ((uint32_t)i << 10);
         return ptype(T, i, i + a) > 0 ? (m - i) / 64 + 1 : 0;
     }
     x -= R.nPL;
     if (x < R.nPR) {
-        const int a = R.aPR0 + x / m, q = x % m;
+        const int a = shard_a(x / m, G, r), q = x % m;
         const int k = q + a + 3, b = t - a;
         it0 = (1u << 30) | ((uint32_t)a << 20) | ((uint32_t)q << 10);
         return ptype(T, k, k + b) > 0 ? q / 64 + 1 : 0;
@@ -533,13 +539,14 @@ __device__ __forceinline__ int item_row(const DevTables &T, int t, const ItemRow
     const int h = 2 + x / n, j = 1 + x % n;
     const int k = j + h + 2;
     if (k > n) return 0;
-    const int alo = imax(imax(2, t - (n - k)), a_lo), ahi = imin(imin(t - 2, j - 1), a_end - 1);
-    if (alo > ahi || ptype(T, j, k) <= 0) return 0;
+    int o0, o1;
+    pm_own_range(n, t, j, k, G, r, o0, o1);
+    if (o0 > o1 || ptype(T, j, k) <= 0) return 0;
     it0 = (2u << 30) | ((uint32_t)h << 20) | ((uint32_t)j << 10);
-    return (ahi - alo) / 64 + 1;
+    return (o1 - o0) / 64 + 1;
 }
 
-__global__ __launch_bounds__(256) void k_items(DevTables T, const int2 *__restrict__ range, int G, int rank, int simulate,
+__global__ __launch_bounds__(256) void k_items(DevTables T, int G, int rank, int simulate,
                                                long long *counts, const long long *__restrict__ offs, uint32_t *items,
                                                int pass) {
     __shared__ int wsum[4];
@@ -551,14 +558,13 @@ __global__ __launch_bounds__(256) void k_items(DevTables T, const int2 *__restri
         if (pass == 0 && tid == 0) counts[b] = 0;
         return;  // whole workgroup
     }
-    const int2 ar = range[b];
-    const ItemRows R = item_rows(T.n, t, ar.x, ar.y);
+    const ItemRows R = item_rows(T.n, t, G, r);
     const int nrows = R.nPL + R.nPR + R.nPM;
     long long base = pass ? offs[b] : 0;
     for (int c0 = 0; c0 < nrows; c0 += 256) {
         const int x = c0 + tid;
         uint32_t it0 = 0;
-        const int cnt = x < nrows ? item_row(T, t, R, x, ar.x, ar.y, it0) : 0;
+        const int cnt = x < nrows ? item_row(T, t, R, x, G, r, it0) : 0;
         // exclusive scan of cnt over the workgroup: wave scan, then the wave totals
         int inc = cnt;
 #pragma unroll
@@ -584,12 +590,12 @@ __global__ __launch_bounds__(256) void k_items(DevTables T, const int2 *__restri
     }
 }
 
-extern "C" int ccjk_items(const DevTables *T, const int2 *range, int G, int rank, int simulate, long long *counts,
-                          const long long *offs, uint32_t *items, int pass, void *stream) {
+extern "C" int ccjk_items(const DevTables *T, int G, int rank, int simulate, long long *counts, const long long *offs,
+                          uint32_t *items, int pass, void *stream) {
     const int blocks = T->n * G;
     if (blocks <= 0) return 0;
-    hipLaunchKernelGGL(k_items, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *T, range, G, rank, simulate,
-                       counts, offs, items, pass);
+    hipLaunchKernelGGL(k_items, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *T, G, rank, simulate, counts,
+                       offs, items, pass);
     return (int)hipGetLastError();
 }
 
@@ -790,7 +796,7 @@ __device__ __forceinline__ ILGroups il_groups(int nact, int lane) {
 }
 
 // one wave per work item (host-built list for level t: closing pairs that can pair, heaviest first)
-__global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long first, int nitems, int a_lo, int a_end) {
+__global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long first, int nitems, int G_SH, int rank) {
     const int n = T.n, rs = T.rs, m = n - t - 2;
     const int lane = threadIdx.x & 63;
     const int w = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -868,12 +874,15 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         // PM: wave = (h, j, a-chunk), lanes a; pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
         const int h = f1, j = f2;
         const int g = h + 2, k = j + g;
-        const int alo = imax(imax(2, t - (n - k)), a_lo), ahi = imin(imin(t - 2, j - 1), a_end - 1);
-        const ILGroups lg = il_groups(imin(64, ahi - alo - zc * 64 + 1), lane);
+        // the rank's own a-blocks in the window (all of [alo, ahi] when unsharded): lanes = own index
+        int o0, o1;
+        pm_own_range(n, t, j, k, G_SH, rank, o0, o1);
+        const ILGroups lg = il_groups(imin(64, o1 - o0 - zc * 64 + 1), lane);
         const int G = lg.G, gq = lg.gq;
-        const int a = alo + zc * 64 + lg.rl;
-        const bool act = a <= ahi;
-        const int as = act ? a : ahi;
+        const int o = o0 + zc * 64 + lg.rl;
+        const bool act = o <= o1;
+        const int a = shard_a(imin(o, o1), G_SH, rank);
+        const int as = a;
         const unsigned lofs2 = 2u * (unsigned)as;
         const size_t pidx = (size_t)g * rs + j;
         // PMx(t-dt, a-1-u1, h+dt, j-1-u1) = pmb + (h+dt)*n*(t+1-dt) + (j-2-u1)(t+1-dt) - 1-u1 + a
@@ -949,7 +958,7 @@ __device__ __forceinline__ void write_records(const DevTables &T, long long lr, 
 // windows are walked by source level dt (outer) so the level descriptor is loaded once per dt.
 // ------------------------------------------------------------------------------------------
 template <bool LEAD>
-__device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wavesPerA, int split, int a_lo, int a_end,
+__device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wavesPerA, int split, int G, int rank, int nblk,
                                              int copies) {
 #ifdef CCJ_DEBUG_BOUNDS
     g_dbg_err = T.err;
@@ -970,13 +979,14 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     const int cpb = (int)(blockDim.x >> 6) / split;  // chunks per block
     const int gw = __builtin_amdgcn_readfirstlane(bid * cpb + wib / split);
     const int lane = threadIdx.x & 63;
-    // this launch computes the a-blocks [a_lo, a_end) of level t (a band shard, §7)
+    // this launch computes nblk a-blocks of level t: rank's own blocks shard_a(0 .. nblk-1) (all of
+    // them when unsharded, ccj_engine.h), or on leader launches the rank's list T.lord
     const int a_rel = __builtin_amdgcn_readfirstlane(gw / wavesPerA);
-    const int a_raw = a_lo + a_rel;
-    if (split == 1 && a_raw >= a_end) return;
-    const bool wave_ok = a_raw < a_end;  // grid tail (split > 1 keeps the wave for the barrier)
-    int a = wave_ok ? a_raw : a_end - 1;
-    if (LEAD && T.lord) a = T.lord[T.lord_off[t] + a];  // leader launches: [a_lo, a_end) indexes the list
+    if (split == 1 && a_rel >= nblk) return;
+    const bool wave_ok = a_rel < nblk;  // grid tail (split > 1 keeps the wave for the barrier)
+    const int oi = wave_ok ? a_rel : nblk - 1;
+    int a = shard_a(oi, G, rank);
+    if (LEAD && T.lord) a = T.lord[T.lord_off[t * G + rank] + oi];
     const int chunk = wave_ok ? gw - a_rel * wavesPerA : 0;
     const int m = n - t - 2;
     const int Mt = (m * (m + 1)) >> 1;
@@ -1638,7 +1648,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     dst[POmloop01 * C] = (int16_t)clamp_store(vPOm01);
     dst[POmloop10 * C] = (int16_t)clamp_store(vPOm10);
     // loop records and interior-loop copies (the copies only where a later k_iloop can read them:
-    // its pair can pair); sharded fills write both after the level's all-gather (k_copies)
+    // its pair can pair); in sharded fills the other ranks' cells get both from k_unpack
     if (!copies) return;
     write_records(T, Lt.lr, C, (unsigned)(a * Mt) + L0, clamp_store(vPLm00), clamp_store(vPMm00), clamp_store(vPOm00),
                   clamp_store(vPfromL), clamp_store(vPfromO), clamp_store(vPLm10), clamp_store(vPfromMp),
@@ -1659,12 +1669,12 @@ __global__ __launch_bounds__(512)
 #ifdef CCJ_WAVES_EU
 __attribute__((amdgpu_waves_per_eu(CCJ_WAVES_EU, CCJ_WAVES_EU)))
 #endif
-void k_level4d(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end, int copies) {
-    level4d_body<false>(T, t, wavesPerA, split, a_lo, a_end, copies);
+void k_level4d(DevTables T, int t, int wavesPerA, int split, int G, int rank, int nblk, int copies) {
+    level4d_body<false>(T, t, wavesPerA, split, G, rank, nblk, copies);
 }
-__global__ __launch_bounds__(512) void k_level4d_lead(DevTables T, int t, int wavesPerA, int split, int a_lo, int a_end,
+__global__ __launch_bounds__(512) void k_level4d_lead(DevTables T, int t, int wavesPerA, int split, int G, int rank, int nblk,
                                                       int copies) {
-    level4d_body<true>(T, t, wavesPerA, split, a_lo, a_end, copies);
+    level4d_body<true>(T, t, wavesPerA, split, G, rank, nblk, copies);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1715,28 +1725,44 @@ extern "C" int ccjk_build_il(const DevTables *T, void *stream) {
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int nitems, int a_lo, int a_end,
-                          void *stream) {
+extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int nitems, int G, int rank, void *stream) {
 #ifdef CCJ_ABLATE_ILOOP
     return 0;
 #endif
     if (nitems <= 0) return 0;
     hipLaunchKernelGGL(k_iloop, dim3((unsigned)((nitems + 3) / 4)), dim3(256), 0, (hipStream_t)stream, *T, t, first_item,
-                       nitems, a_lo, a_end);
+                       nitems, G, rank);
     return (int)hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
-// Interior-loop copies of level t for the a-blocks [a_lo, a_end) (sharded fills: after the
-// all-gather the other ranks' cells of level t are present in the main layout but not in the
-// copies).  One lane per cell, main-layout order.
+// Band-sharded exchange of level t.  k_pack: rank r's own cells, all 22 matrices,
+// into one contiguous slice [x][own index][M] of nmax blocks per matrix (nmax = the largest rank's
+// block count at t), so the exchange is ONE all-gather of equal slices.  k_unpack: every cell of the
+// other ranks' blocks from the gathered slices back into the level layout, plus its loop records and
+// interior-loop copies (what k_level4d writes for its own cells).  recv == nullptr: the cells are
+// already in the level layout and only their records and copies are rebuilt.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_copies(DevTables T, int t, int a_lo, int a_end) {
+__global__ __launch_bounds__(256) void k_pack(DevTables T, int t, int G, int r, int nmax, int16_t *send) {
     const int n = T.n, m = n - t - 2, Mt = (m * (m + 1)) >> 1;
     const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const int a = a_lo + (int)(gc / Mt);
-    if (a >= a_end) return;
-    const int c = (int)(gc - (long long)(a - a_lo) * Mt);
+    const int o = (int)(gc / Mt);
+    if (o >= shard_count(t, G, r)) return;
+    const int c = (int)(gc - (long long)o * Mt);
+    const LvlDev Lt = T.ld[t];
+    const int16_t *src = T.d4 + Lt.lb + (long long)shard_a(o, G, r) * Mt + c;
+#pragma unroll 2
+    for (int x = 0; x < NMAT4; ++x) send[((long long)x * nmax + o) * Mt + c] = src[(long long)x * Lt.C];
+}
+
+__global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r, int nmax, const int16_t *recv) {
+    const int n = T.n, m = n - t - 2, Mt = (m * (m + 1)) >> 1;
+    const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int a = (int)(gc / Mt);
+    if (a > t) return;
+    const int ro = shard_owner(a, G);
+    if (ro == r) return;  // own cell: k_level4d wrote it with its records and copies
+    const int c = (int)(gc - (long long)a * Mt);
     const float tm = 2.0f * m + 1.0f;
     int h = (int)((tm - sqrtf(tm * tm - 8.0f * (float)c)) * 0.5f);
     h = imax(0, imin(h, m - 1));
@@ -1747,63 +1773,122 @@ __global__ __launch_bounds__(256) void k_copies(DevTables T, int t, int a_lo, in
     const int j = i + a, k = j + h + 2, l = k + b;
     const LvlDev Lt = T.ld[t];
     const LvlX X = T.ldx[t];
-    const int16_t *src = T.d4 + Lt.lb + (long long)a * Mt + Gh + i - 1;
+    int16_t *dst = T.d4 + Lt.lb + (long long)a * Mt + c;
     const long long C = Lt.C;
-    write_records(T, Lt.lr, Lt.C, (unsigned)(a * Mt + Gh + i - 1), src[PLmloop00 * C], src[PMmloop00 * C],
-                  src[POmloop00 * C], src[PfromL * C], src[PfromO * C], src[PLmloop10 * C], src[PfromMprime * C],
-                  src[PK * C], src[PRmloop00 * C], src[PfromR * C], imin(src[PL * C], src[PR * C]),
-                  src[PMmloop10 * C], src[POmloop10 * C]);
-    if (ptype(T, i, j) > 0) T.d4x[X.lbx + (long long)a * Mt + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = src[PL * (long long)Lt.C];
+    int v[NMAT4];
+    if (recv) {
+        const int o = shard_count(a - 1, G, ro);  // a's own index on its rank
+        const int16_t *sl = recv + (long long)ro * NMAT4 * nmax * Mt + (long long)o * Mt + c;
+#pragma unroll
+        for (int x = 0; x < NMAT4; ++x) {
+            v[x] = sl[(long long)x * nmax * Mt];
+            dst[x * C] = (int16_t)v[x];
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < NMAT4; ++x) v[x] = dst[x * C];
+    }
+    write_records(T, Lt.lr, Lt.C, (unsigned)(a * Mt + c), v[PLmloop00], v[PMmloop00], v[POmloop00], v[PfromL], v[PfromO],
+                  v[PLmloop10], v[PfromMprime], v[PK], v[PRmloop00], v[PfromR], imin(v[PL], v[PR]), v[PMmloop10],
+                  v[POmloop10]);
+    if (ptype(T, i, j) > 0) T.d4x[X.lbx + (long long)a * Mt + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = (int16_t)v[PL];
     if (ptype(T, k, l) > 0) {
         const int q = i + h - 1;
-        T.d4x[X.lbx + Lt.C + (long long)a * Mt + ((q * (q + 1)) >> 1) + i - 1] = src[PR * (long long)Lt.C];
+        T.d4x[X.lbx + Lt.C + (long long)a * Mt + ((q * (q + 1)) >> 1) + i - 1] = (int16_t)v[PR];
     }
-    if (ptype(T, j, k) > 0) T.pmx[X.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = src[PM * (long long)Lt.C];
+    if (ptype(T, j, k) > 0) T.pmx[X.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = (int16_t)v[PM];
 }
 
-extern "C" int ccjk_copies(const DevTables *T, int t, int a_lo, int a_end, void *stream) {
+extern "C" int ccjk_pack(const DevTables *T, int t, int G, int r, int nmax, int16_t *send, void *stream) {
     const int m = T->n - t - 2;
-    if (m <= 0 || a_end <= a_lo) return 0;
-    const long long cells = (long long)(a_end - a_lo) * (m * (m + 1) / 2);
-    hipLaunchKernelGGL(k_copies, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, a_lo, a_end);
+    if (m <= 0) return 0;
+    const long long cells = (long long)shard_count(t, G, r) * (m * (m + 1) / 2);
+    if (cells <= 0) return 0;
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, G, r, nmax, send);
+    return (int)hipGetLastError();
+}
+
+extern "C" int ccjk_unpack(const DevTables *T, int t, int G, int r, int nmax, const int16_t *recv, void *stream) {
+    const int m = T->n - t - 2;
+    if (m <= 0) return 0;
+    const long long cells = (long long)(t + 1) * (m * (m + 1) / 2);
+    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, G, r, nmax, recv);
+    return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Matrix x of every level rewritten in the reference's canonical (i, j, k, l) order (l fastest):
+// the input of ccj_hashes (FNV-1a over that order).  One launch per level t, one thread per cell.
+// Canonical position of (i,j,k,l) = offij[i*(n+1)+j] + sum_{k'=j+2}^{k-1} (n+1-k') + (l-k).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_canon(DevTables T, int x, int t, const long long *__restrict__ offij, int16_t *out) {
+    const int n = T.n, m = n - t - 2;
+    if (m <= 0) return;
+    const LvlDev L = T.ld[t];
+    const int Mt = L.M;
+    const long long cidx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cidx >= (long long)L.C) return;
+    const int a = (int)(cidx / Mt), c = (int)(cidx - (long long)a * Mt);
+    const float tm = 2.0f * m + 1.0f;
+    int h = (int)((tm - sqrtf(tm * tm - 8.0f * (float)c)) * 0.5f);
+    h = imax(0, imin(h, m - 1));
+    while (h > 0 && h * m - ((h * (h - 1)) >> 1) > c) --h;
+    while (h + 1 < m && (h + 1) * m - (((h + 1) * h) >> 1) <= c) ++h;
+    const int Gh = h * m - ((h * (h - 1)) >> 1);
+    const int i = c - Gh + 1, j = i + a, k = j + h + 2, l = k + (t - a);
+    const long long u = k - (j + 2);
+    const long long pos = offij[(long long)i * (n + 1) + j] + u * (n + 1) - u * (2LL * j + 3 + u) / 2 + (l - k);
+    out[pos] = T.d4[L.lb + (long long)x * L.C + cidx];
+}
+
+extern "C" int ccjk_canon(const DevTables *T, int x, const long long *offij, int16_t *out, void *stream) {
+    const int n = T->n;
+    for (int t = 0; t < T->nlev; ++t) {
+        const int m = n - t - 2;
+        const long long C = (long long)(t + 1) * (m * (m + 1) / 2);
+        hipLaunchKernelGGL(k_canon, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, x, t, offij, out);
+    }
     return (int)hipGetLastError();
 }
 
 // narrow levels: split each chunk's a/b loops over up to 8 waves so ~split_target waves run at once
-extern "C" int ccjk_level_split(int n, int t, int a_lo, int a_end, int split_target) {
+extern "C" int ccjk_level_split(int n, int t, int nblk, int split_target) {
     const int m = n - t - 2;
-    if (m <= 0 || a_end <= a_lo) return 1;
-    const long waves = (long)(a_end - a_lo) * ((m * (m + 1) / 2 + 63) / 64);
+    if (m <= 0 || nblk <= 0) return 1;
+    const long waves = (long)nblk * ((m * (m + 1) / 2 + 63) / 64);
     int split = 1;
     while (split_target > 0 && split < 8 && waves * split * 2 <= split_target) split *= 2;
     return split;
 }
 
-extern "C" int ccjk_level4d(const DevTables *T, int t, int a_lo, int a_end, int copies, void *stream) {
+extern "C" int ccjk_level4d(const DevTables *T, int t, int G, int rank, int copies, void *stream) {
     const int m = T->n - t - 2;
     if (m <= 0) return 0;
     const int Mt = m * (m + 1) / 2;
     const int wavesPerA = (Mt + 63) / 64;
-    if (a_end <= a_lo) return 0;
-    const long waves = (long)(a_end - a_lo) * wavesPerA;
+    const int nblk = shard_count(t, G, rank);
+    if (nblk <= 0) return 0;
+    const long waves = (long)nblk * wavesPerA;
     // on the sharing levels this launch only has follower cells (short scans): never split
-    const int split = (t >= T->g_lo && t < T->g_hi) ? 1 : ccjk_level_split(T->n, t, a_lo, a_end, T->split_target);
+    const int split = (t >= T->g_lo && t < T->g_hi) ? 1 : ccjk_level_split(T->n, t, nblk, T->split_target);
     const int threads = split <= 4 ? 256 : 64 * split;
     const int cpb = threads / 64 / split;
     const long blocks = (waves + cpb - 1) / cpb;
     const size_t shmem = split > 1 ? (size_t)cpb * (split - 1) * 22 * 64 * sizeof(int) : 0;
-    hipLaunchKernelGGL(k_level4d, dim3((unsigned)blocks), dim3(threads), shmem, (hipStream_t)stream, *T, t, wavesPerA, split, a_lo, a_end, copies);
+    hipLaunchKernelGGL(k_level4d, dim3((unsigned)blocks), dim3(threads), shmem, (hipStream_t)stream, *T, t, wavesPerA, split,
+                       G, rank, nblk, copies);
     return (int)hipGetLastError();
 }
 
 // the split-point-sharing leader waves of level t (no-op outside the sharing range)
-extern "C" int ccjk_level4d_lead(const DevTables *T, int t, void *stream) {
+extern "C" int ccjk_level4d_lead(const DevTables *T, int t, int G, int rank, void *stream) {
     if (t < T->g_lo || t >= T->g_hi) return 0;
     const int m = T->n - t - 2;
     const int Mt = m * (m + 1) / 2;
     const int wavesPerA = (Mt + 63) / 64;
-    // only the long-scan a-blocks (T->lord, longest first) when the list is there
-    const int nblk = T->lord ? T->lord_off_h[t + 1] - T->lord_off_h[t] : t + 1;
+    // only the rank's long-scan a-blocks (T->lord, longest first) when the list is there
+    const int own = shard_count(t, G, rank);
+    const int nblk = T->lord ? T->lord_off_h[t * G + rank + 1] - T->lord_off_h[t * G + rank] : own;
     if (nblk <= 0) return 0;
     const long waves = (long)nblk * wavesPerA;
     // each leader chunk's scans are split over `split` waves of one workgroup (the barriers inside
@@ -1813,10 +1898,10 @@ extern "C" int ccjk_level4d_lead(const DevTables *T, int t, void *stream) {
         const int v = e ? atoi(e) : 2;
         return v >= 1 && v <= 8 ? v : 2;
     }();
-    // narrow late levels: as many split waves as the plain heuristic would give the whole level
-    const int sp = imax(lsplit, ccjk_level_split(T->n, t, 0, t + 1, T->split_target));
+    // narrow late levels: as many split waves as the plain heuristic would give the rank's blocks
+    const int sp = imax(lsplit, ccjk_level_split(T->n, t, own, T->split_target));
     const size_t shmem = sp > 1 ? (size_t)(sp - 1) * (LEAD_RED > 22 ? LEAD_RED : 22) * 64 * sizeof(int) : 0;
     hipLaunchKernelGGL(k_level4d_lead, dim3((unsigned)waves), dim3(64 * sp), shmem, (hipStream_t)stream, *T, t, wavesPerA,
-                       sp, 0, nblk, 1);
+                       sp, G, rank, nblk, 1);
     return (int)hipGetLastError();
 }

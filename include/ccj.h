@@ -65,8 +65,8 @@ typedef struct ccj_options {
     int device;
     int overlap_d2h;     /* 1: stream finished levels to the host mirror while later levels compute */
     /* Band sharding of one sequence over shard_world processes (one per GPU):
-     * this process computes the a-blocks ccj_shard_range() gives it and the levels are all-gathered
-     * over RCCL (ccj_comm_init before the first fill).  0 or 1 = unsharded. */
+     * this process computes the a-blocks ccj_shard_blocks() gives it and each level is all-gathered
+     * over RCCL (ccj_comm_init, or ccj_comm_init_local, before the first fill).  0 or 1 = unsharded. */
     int shard_world;
     int shard_rank;
     int shard_simulate;  /* 1: run every shard's launches in this one context, no exchange (tests) */
@@ -78,7 +78,7 @@ typedef struct ccj_options {
      *   about this many waves run at once (default 6144); < 0 never splits.
      * share_splits: split-point sharing between the cells of one gap column: a
      *   leader cell scans its whole split range once for itself and the next CCJ_SHARE_R-1 cells of
-     *   its column; < 0 turns it off (every cell scans its own range).  Unsharded fills only. */
+     *   its column; < 0 turns it off (every cell scans its own range). */
     int split_target;
     int share_splits;
 } ccj_options;
@@ -141,10 +141,18 @@ int  ccj_set_timing(ccj_ctx *ctx, int mode);
 int  ccj_comm_unique_id(char *id_out);
 /* Join the sharded context to the RCCL communicator of shard_world ranks. */
 int  ccj_comm_init(ccj_ctx *ctx, const char *id);
-/* The a-blocks [*a_lo, *a_end) of level t that rank computes (host helper, no GPU). */
-int  ccj_shard_range(int n, int t, int world, int rank, int *a_lo, int *a_end);
-/* Per-matrix element stride C_t (padded to world equal chunks) and a-block size M_t of level t. */
+/* The a-blocks of level t that rank computes (host helper, no GPU): writes up to cap of them to
+ * a_out, ascending, and returns how many there are (< 0: bad arguments).  Block a belongs to rank
+ * (a / 4) % world on every level. */
+int  ccj_shard_blocks(int n, int t, int world, int rank, int *a_out, int cap);
+/* Per-matrix element count C_t of level t and the a-block size M_t (the same for every world). */
 int  ccj_level_layout(int n, int t, int world, long long *C, int *M);
+/* In-process exchange group (tests, and several ranks sharing one device): shard_world contexts,
+ * each driven by its own host thread, join one group instead of an RCCL communicator. */
+typedef struct ccj_group ccj_group;
+int  ccj_group_create(int world, ccj_group **out);
+void ccj_group_destroy(ccj_group *g);
+int  ccj_comm_init_local(ccj_ctx *ctx, ccj_group *g);
 
 /* Algorithmic work model of this sequence:
  * out[0] = bytes moved by the 4-D level kernels (2 B per int16 operand read + 44 B of writes per cell),

@@ -71,3 +71,64 @@ def test_sharded_fold_matches_reference_stdout(case, world):
         assert wf.stdout_msgs + case["seq"] + "\n" + f"{wf.structure} ({e:g})\n" == case["stdout"]
     finally:
         wf.close()
+
+
+def _fold_group(seq, params, world):
+    """Every rank of a band-sharded fold as its own context, exchanging through an in-process group
+    (the real sharded path: own blocks only, pack, ONE all-gather per level, unpack with records and
+    interior-loop copies); each rank driven by its own thread."""
+    import threading
+    from ccj_amd import LocalGroup, W_final
+    g = LocalGroup(world)
+    ranks = [W_final(seq, 2, params=params, shard_world=world, shard_rank=r, local_group=g) for r in range(world)]
+    errs = []
+
+    def run(wf):
+        try:
+            wf.fill()
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(wf,)) for wf in ranks]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=300)
+    assert not errs, errs
+    return g, ranks
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", HASHES[:2], ids=lambda c: f"n{len(c['seq'])}-{c['params']}")
+def test_exchange_group_every_rank_holds_the_reference_fold(case, world):
+    g, ranks = _fold_group(case["seq"], case["params"], world)
+    try:
+        for wf in ranks:
+            try:
+                wf.result()
+            except Exception:
+                pass
+            got = wf.hashes()
+            bad = [k for k in case["hashes"] if got[k] != case["hashes"][k]]
+            assert not bad, f"rank {wf.rank if hasattr(wf, 'rank') else '?'}: {bad}"
+    finally:
+        for wf in ranks:
+            wf.close()
+        g.close()
+
+
+def test_exchange_group_config4_dp09_200():
+    """BASELINE config 4 (DirksPierce09, n=200, 4 ranks) through the real exchange path: every rank
+    ends with the reference's matrices and prints the reference's structure."""
+    case = [c for c in golden("hashes_large.json") if c["tag"] == "dp09_200"][0]
+    g, ranks = _fold_group(case["seq"], case["params"], 4)
+    try:
+        for wf in ranks:
+            e = wf.result()
+            assert f"{wf.structure} ({e:g})" == case["stdout"].splitlines()[-1]
+        got = ranks[3].hashes()
+        assert {k: got[k] for k in case["hashes"]} == case["hashes"]
+    finally:
+        for wf in ranks:
+            wf.close()
+        g.close()

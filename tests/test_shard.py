@@ -1,11 +1,13 @@
 """Band sharding of one sequence — host logic, on CPU.
 
-* ccj_shard_range partitions every level's a-blocks into contiguous per-rank ranges, and
-  ccj_level_layout pads each matrix of the level to world equal chunks, so rank r's blocks are
-  exactly chunk r of every matrix: an in-place all-gather per matrix rebuilds the whole level.
-* world-size-2 gloo run: each rank writes only its own blocks of every level (cell values from the
-  C oracle, which is the checker here), the chunks are all-gathered as the RCCL path does on the
-  GPU, and the gathered levels must equal the levels written by one process.
+* Ownership: a-block a of every level belongs to rank (a // 4) % world, the same rank on every
+  level, so a split-sharing leader (a % 4 == 0) and its followers (a+1 .. a+3, on later levels)
+  are on one rank; ccj_shard_blocks lists a rank's blocks, and every level's blocks are partitioned.
+* Exchange: world-size-2 gloo run.  Each rank packs only its own cells of every level (values from
+  the C oracle, which is the checker here) into one slice [matrix][own block][cell] of nmax blocks
+  (nmax = the largest rank's block count), the slices are all-gathered as ONE collective per level
+  (the RCCL path does the same on the GPU), and unpacking the other ranks' slices must rebuild the
+  level exactly as one process writes it.
 """
 import os
 import random
@@ -16,6 +18,7 @@ import pytest
 from tests.oracle_lib import OracleFold, blob
 
 NMAT4 = 22
+GRP = 4
 
 
 def _rseq(seed, n):
@@ -23,80 +26,110 @@ def _rseq(seed, n):
     return "".join(r.choice("ACGU") for _ in range(n))
 
 
+def _owner(a, world):
+    return (a // GRP) % world
+
+
 @pytest.mark.parametrize("n", [7, 33, 200])
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
-def test_shard_ranges_partition_levels(n, world):
-    from ccj_amd import level_layout, shard_range
+def test_shard_blocks_partition_levels(n, world):
+    from ccj_amd import level_layout, shard_blocks
     for t in range(max(n - 2, 1)):
         C, M = level_layout(n, t, world)
-        B = -(-(t + 1) // world)
-        assert C == (t + 1) * M if world == 1 else C == B * world * M
-        nxt = 0
+        assert C == (t + 1) * M  # unpadded for every world
+        seen = []
         for r in range(world):
-            lo, end = shard_range(n, t, world, r)
-            assert lo == min(nxt, t + 1) and lo <= end <= t + 1
-            if world > 1:
-                assert end - lo <= B and lo == min(r * B, t + 1)  # chunk r of C holds blocks [rB, (r+1)B)
-            nxt = end
-        assert nxt == t + 1
+            blocks = shard_blocks(n, t, world, r)
+            assert blocks == sorted(blocks)
+            assert all(_owner(a, world) == r for a in blocks)
+            # a leader's followers a+1..a+3 (the same column on later levels) are on its rank
+            for a in blocks:
+                if a % GRP == 0:
+                    assert all(_owner(a + x, world) == r for x in range(1, GRP))
+            seen += blocks
+        assert sorted(seen) == list(range(t + 1))
+        # balance: ranks differ by at most one group of blocks
+        counts = [len(shard_blocks(n, t, world, r)) for r in range(world)]
+        assert max(counts) - min(counts) <= GRP
 
 
-def _level_buffer(n, t, world, fold, ranks):
-    """22 matrices of level t in the (padded) device layout, cells of the given ranks' blocks only."""
-    from ccj_amd import level_layout, shard_range
-    C, M = level_layout(n, t, world)
+def _cells(n, t, a):
     m = n - t - 2
+    b = t - a
+    for h in range(m):
+        for i in range(1, m - h + 1):
+            j, k = i + a, i + a + h + 2
+            yield h * m - h * (h - 1) // 2 + (i - 1), (i, j, k, k + b)
+
+
+def _level(n, t, fold, blocks):
+    """22 matrices of level t in the device layout, only the given blocks' cells filled."""
+    from ccj_amd import level_layout
+    C, M = level_layout(n, t, 1)
     buf = np.zeros(NMAT4 * C, dtype=np.int16)
-    for r in ranks:
-        lo, end = shard_range(n, t, world, r)
-        for a in range(lo, end):
-            b = t - a
-            for h in range(m):
-                for i in range(1, m - h + 1):
-                    j, k = i + a, i + a + h + 2
-                    l = k + b
-                    off = a * M + h * m - h * (h - 1) // 2 + (i - 1)
-                    for x in range(NMAT4):
-                        buf[x * C + off] = fold.get4(x, i, j, k, l)
-    return buf, C
+    for a in blocks:
+        for off, (i, j, k, l) in _cells(n, t, a):
+            for x in range(NMAT4):
+                buf[x * C + a * M + off] = fold.get4(x, i, j, k, l)
+    return buf, C, M
+
+
+def _pack(level, C, M, blocks, nmax):
+    """k_pack: slice [x][own index][M] of nmax blocks per matrix."""
+    sl = np.zeros(NMAT4 * nmax * M, dtype=np.int16)
+    for o, a in enumerate(blocks):
+        for x in range(NMAT4):
+            sl[(x * nmax + o) * M:(x * nmax + o + 1) * M] = level[x * C + a * M: x * C + (a + 1) * M]
+    return sl
+
+
+def _unpack(level, C, M, slices, world, rank, t, nmax, shard_blocks, n):
+    """k_unpack: the other ranks' blocks from their slices."""
+    for r in range(world):
+        if r == rank:
+            continue
+        for o, a in enumerate(shard_blocks(n, t, world, r)):
+            for x in range(NMAT4):
+                level[x * C + a * M: x * C + (a + 1) * M] = slices[r][(x * nmax + o) * M:(x * nmax + o + 1) * M]
 
 
 def _gloo_rank(rank, world, port, n, seq, q):
-    import torch
-    import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        _gloo_body(rank, world, n, seq, q, torch, dist)
+        import torch
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            q.put((rank, _gloo_body(rank, world, n, seq, torch, dist)))
+        finally:
+            dist.destroy_process_group()
     except Exception as e:  # report instead of leaving the parent waiting
         q.put((rank, repr(e)))
-    finally:
-        dist.destroy_process_group()
 
 
-def _gloo_body(rank, world, n, seq, q, torch, dist):
-    if True:
-        fold = OracleFold(seq, blob("Turner04"), 2, 0)
-        ok = True
-        for t in range(n - 2):
-            mine, C = _level_buffer(n, t, world, fold, [rank])
-            chunk = C // world
-            gathered = np.array(mine)
-            for x in range(NMAT4):
-                # bytes, as the RCCL path sends them: ncclAllGather(base + rank*chunk, base, 2*chunk, ncclInt8)
-                own = torch.from_numpy(mine[x * C + rank * chunk: x * C + (rank + 1) * chunk].copy()).view(torch.uint8)
-                parts = [torch.empty_like(own) for _ in range(world)]
-                dist.all_gather(parts, own)
-                gathered[x * C: (x + 1) * C] = torch.cat(parts).view(torch.int16).numpy()
-            full, _ = _level_buffer(n, t, world, fold, range(world))
-            ok &= bool(np.array_equal(gathered, full))
-        fold.close()
-        q.put((rank, ok))
+def _gloo_body(rank, world, n, seq, torch, dist):
+    from ccj_amd import shard_blocks
+    fold = OracleFold(seq, blob("Turner04"), 2, 0)
+    ok = True
+    for t in range(n - 2):
+        mine = shard_blocks(n, t, world, rank)
+        nmax = max(len(shard_blocks(n, t, world, r)) for r in range(world))
+        level, C, M = _level(n, t, fold, mine)
+        own = torch.from_numpy(_pack(level, C, M, mine, nmax)).view(torch.uint8)  # bytes, like ncclInt8
+        parts = [torch.empty_like(own) for _ in range(world)]
+        dist.all_gather(parts, own)  # ONE collective per level
+        slices = [p.view(torch.int16).numpy() for p in parts]
+        _unpack(level, C, M, slices, world, rank, t, nmax, shard_blocks, n)
+        full, _, _ = _level(n, t, fold, range(t + 1))
+        ok &= bool(np.array_equal(level, full))
+    fold.close()
+    return ok
 
 
 def test_level_allgather_rebuilds_levels_gloo():
+    pytest.importorskip("torch")
     import torch.multiprocessing as mp
-    n, world = 16, 2
+    n, world = 18, 2
     seq = _rseq(11, n)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
