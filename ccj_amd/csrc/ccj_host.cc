@@ -157,6 +157,9 @@ struct ccj_ctx {
     std::vector<unsigned long long> h_pk;
     int8_t *d_vt = nullptr;
     hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr, st_il = nullptr, st_d = nullptr;
+    hipStream_t st_pre = nullptr;        // prepass leader launches (level t beside level t-1)
+    std::vector<hipEvent_t> pre_done;    // prepass launch of level t finished
+    bool prepass = false;                // CCJ_PREPASS=1: leader launch of level t beside level t-1 (measured +0.5 ms at n=200)
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<double> lev_ms_v, diag_ms_v, il_ms_v;
     std::vector<hipEvent_t> il_done, dg_done;  // k_iloop(t) / k_diag2d(sigma) finished
@@ -1518,6 +1521,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         if (opts && opts->split_target) c->split_target = opts->split_target < 0 ? 0 : opts->split_target;
         const char *lt = getenv("CCJ_LEVEL_TIMING");
         if (lt) c->level_timing = std::max(0, std::min(2, atoi(lt)));
+        const char *pp = getenv("CCJ_PREPASS");
+        c->prepass = pp && atoi(pp) != 0;
         const char *g = getenv("CCJ_SHARE_SPLITS");
         c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
     }
@@ -1576,6 +1581,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_p, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_il, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_d, hipStreamNonBlocking));
+    HIPCHK(cp, hipStreamCreateWithFlags(&c->st_pre, hipStreamNonBlocking));
+    c->pre_done.resize(n + 1);
+    for (auto &e : c->pre_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->il_done.resize(n + 1);
     for (auto &e : c->il_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->dg_done.resize(n + 1);
@@ -1654,9 +1662,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         HIPCHK(cp, hipMemcpy(c->d_lord_off, c->lord_off.data(), c->lord_off.size() * sizeof(int), hipMemcpyHostToDevice));
     }
     if (g_hi > g_lo) {
-        if (hipMalloc(&c->d_acc, (size_t)SHARE_R * SHARE_NACC * accC * sizeof(uint4)) != hipSuccess)
+        if (hipMalloc(&c->d_acc, (size_t)SHARE_SLOTS * SHARE_NACC * accC * sizeof(uint4)) != hipSuccess)
             return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for split-sharing records failed",
-                           SHARE_R * SHARE_NACC * accC * 16e-9);
+                           SHARE_SLOTS * SHARE_NACC * accC * 16e-9);
     }
     HIPCHK(cp, hipMalloc(&c->d_ie, ie_elems * sizeof(int16_t)));
     HIPCHK(cp, hipMalloc(&c->d_est, plane * sizeof(int16_t)));
@@ -1798,6 +1806,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.lord_off = c->d_lord_off;
     T.lord_off_h = c->lord_off.empty() ? nullptr : c->lord_off.data();
     T.accC = accC;
+    T.prepass = c->prepass && g_hi > g_lo;
     {
         const int G = c->world;
         HIPCHK(cp, hipMalloc(&c->d_icount, (size_t)n * G * sizeof(long long)));
@@ -1850,7 +1859,7 @@ extern "C" int ccj_reset(ccj_ctx *c, const char *seq) {
             return set_err(c, CCJ_E_ARG, "ccj_reset: invalid character in sequence");
     HIPCHK(c, hipSetDevice(c->device));
     // the previous fold's streams may still read the sequence tables
-    for (hipStream_t q : {c->st, c->st_copy, c->st_p, c->st_il, c->st_d}) HIPCHK(c, hipStreamSynchronize(q));
+    for (hipStream_t q : {c->st, c->st_copy, c->st_p, c->st_il, c->st_d, c->st_pre}) HIPCHK(c, hipStreamSynchronize(q));
     c->seq = s;
     c->W.clear();
     return seq_setup(c);
@@ -1880,6 +1889,21 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     HIPCHK(c, hipStreamWaitEvent(c->st_d, c->ev_pre, 0));
     HIPCHK(c, hipStreamWaitEvent(c->st_il, c->ev_pre, 0));
     HIPCHK(c, hipStreamWaitEvent(c->st_p, c->ev_pre, 0));
+    HIPCHK(c, hipStreamWaitEvent(c->st_pre, c->ev_pre, 0));
+    // prepass leader launch of level t: needs 4-D levels <= t-2 and 2-D spans <= t-1;
+    // enqueued after level t-2, beside level t-1; level t's plain launch waits for it
+    auto enqueue_pre = [&](int t) -> int {
+        if (!c->T.prepass || t < c->T.g_lo || t >= c->T.g_hi || t >= c->nlev) return CCJ_OK;
+        if (t >= 2) HIPCHK(c, hipStreamWaitEvent(c->st_pre, c->lev_done[t - 2], 0));
+        if (t >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_pre, c->dg_done[t - 1], 0));
+        for (int r = 0; r < c->world; ++r) {
+            if (!c->simulate && r != c->rank) continue;
+            HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, t, c->world, r, c->st_pre));
+        }
+        HIPCHK(c, hipEventRecord(c->pre_done[t], c->st_pre));
+        return CCJ_OK;
+    };
+    if (const int rc = enqueue_pre(0)) return rc;
     for (int s = 0; s < n; ++s) {
         hipEvent_t *ev = &c->tev[7 * (size_t)s];
         // timing markers (ev[0..6]) only when per-kernel timing is on
@@ -1889,6 +1913,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
         HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, s, c->st_d));
         HIPCHK(c, trec(1, c->st_d));
         HIPCHK(c, hipEventRecord(c->dg_done[s], c->st_d));
+        if (const int rc = enqueue_pre(s + 1)) return rc;  // its inputs: lev_done[s-1], dg_done[s]
         if (s < c->nlev) {
             if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 3], 0));
             HIPCHK(c, trec(2, c->st_il));
@@ -1903,6 +1928,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
             HIPCHK(c, hipEventRecord(c->il_done[s], c->st_il));
             HIPCHK(c, hipStreamWaitEvent(st, c->il_done[s], 0));
             if (s >= 1) HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s - 1], 0));
+            if (c->T.prepass && s >= c->T.g_lo && s < c->T.g_hi) HIPCHK(c, hipStreamWaitEvent(st, c->pre_done[s], 0));
             HIPCHK(c, trec(4, st));
             // the level: its plain launch, then (sharing levels) the leaders on the same stream, no
             // cross-stream hop between the two launches or between levels
@@ -1910,9 +1936,11 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
                 if (!c->simulate && r != c->rank) continue;
                 HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, G, r, 1, st));
             }
-            for (int r = 0; r < G; ++r) {
-                if (!c->simulate && r != c->rank) continue;
-                HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, G, r, st));
+            if (!c->T.prepass) {
+                for (int r = 0; r < G; ++r) {
+                    if (!c->simulate && r != c->rank) continue;
+                    HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, G, r, st));
+                }
             }
             if (G > 1 && !c->simulate) {
                 // band-sharded exchange: this rank's cells of the level, all 22
@@ -1960,6 +1988,7 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     HIPCHK(c, hipStreamSynchronize(c->st_p));
     HIPCHK(c, hipStreamSynchronize(c->st_il));
     HIPCHK(c, hipStreamSynchronize(c->st_d));
+    HIPCHK(c, hipStreamSynchronize(c->st_pre));
     int herr = 0;
     HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (herr & 1) return set_err(c, CCJ_E_PARAMS, "e_intP table value outside int16 range (flags %d)", herr);
@@ -2466,6 +2495,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->st_p) hipStreamSynchronize(c->st_p);
     if (c->st_il) hipStreamSynchronize(c->st_il);
     if (c->st_d) hipStreamSynchronize(c->st_d);
+    if (c->st_pre) hipStreamSynchronize(c->st_pre);
     hipFree(c->d4);
     hipFree(c->d_ie);
     hipFree(c->d_est);
@@ -2514,6 +2544,8 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->st_il) hipStreamDestroy(c->st_il);
     if (c->st_d) hipStreamDestroy(c->st_d);
+    if (c->st_pre) hipStreamDestroy(c->st_pre);
+    for (auto e : c->pre_done) hipEventDestroy(e);
     for (auto e : c->il_done) hipEventDestroy(e);
     for (auto e : c->dg_done) hipEventDestroy(e);
     for (auto e : c->tev) hipEventDestroy(e);

@@ -918,8 +918,9 @@ __device__ __forceinline__ unsigned pk16(int lo, int hi) { return (unsigned)(uin
 __device__ __forceinline__ int lo16(unsigned w) { return (int)(int16_t)(w & 0xffffu); }
 __device__ __forceinline__ int hi16(unsigned w) { return (int)w >> 16; }
 
-// ints per lane a leader's split wave hands to part 0: the follower slices of one side
-constexpr int LEAD_RED = 15 * (SHARE_R - 1);
+// ints per lane a leader's split wave hands to part 0: the slices r = 0..R-1 of one side (the
+// followers' r >= 1 only, unless the prepass scheme hands r = 0 over too)
+constexpr int LEAD_RED = 15 * SHARE_R;
 
 // split-point sharing (ccj_engine.h): the SHARE_R W values of one split step, one per follower
 typedef int wv_t __attribute__((ext_vector_type(SHARE_R)));
@@ -1052,15 +1053,28 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     const int arole = (grp && b >= SHARE_R - 1) ? (ra == 0 ? 1 : (t - ra >= T.g_lo ? 2 : 0)) : 0;
     const int brole = (grp && a >= SHARE_R - 1) ? (rb == 0 ? 1 : (t - rb >= T.g_lo ? 2 : 0)) : 0;
     // On sharing levels every wave with a long scan (a leader, or a full scan on either side) runs
-    // in its own launch (k_level4d_lead: more registers, scans split over several waves, side
-    // stream); the plain kernel keeps the cells that only follow (short scans, full occupancy).
-    if (grp && LEAD != (arole != 2 || brole != 2)) return;
-    const int a_stop = arole == 2 ? ra : a;  // last split step this cell scans itself
-    const int b_stop = brole == 2 ? rb : b;
+    // in its own launch (k_level4d_lead: more registers, scans split over several waves); the plain
+    // kernel keeps the cells that only follow (short scans, full occupancy).
+    // Prepass scheme (T.prepass): the leader launch of level t runs one level EARLY,
+    // beside level t-1, and scans only the split points s >= 2 (source levels <= t-2), handing
+    // every result — the cell's own (r = 0) and its followers' — over through the partial-record
+    // ring; the plain launch of level t then finishes EVERY cell of the level: split step 1 (level
+    // t-1) for the long-scan sides, steps 1..a%R+1 for the followers (their leader skipped its own
+    // step 1, the followers' step a%R+1), plus the ring records.  Level t's critical path is then
+    // only short scans.
+    const bool prem = T.prepass && grp;
+    if (grp && (prem ? (LEAD && arole == 2 && brole == 2) : (LEAD != (arole != 2 || brole != 2)))) return;
+    // last split step this cell scans itself (in this launch)
+    const int a_stop = prem ? (LEAD ? (arole == 2 ? 0 : a) : (arole == 2 ? imin(ra + 1, a) : imin(1, a)))
+                            : (arole == 2 ? ra : a);
+    const int b_stop = prem ? (LEAD ? (brole == 2 ? 0 : b) : (brole == 2 ? imin(rb + 1, b) : imin(1, b)))
+                            : (brole == 2 ? rb : b);
+    const int s_first = (LEAD && prem) ? 2 : 1;  // first split step this cell scans itself
 
     // ---- fused a-loop: split point d inside [i, j] ----
-    int pLm00 = INTERN_INF + bp, pLm01 = INF, pLm10 = INF, pMm00 = INTERN_INF + bp, pMm10 = INF;
-    int pOm00 = INTERN_INF + bp, pOm10 = INF;
+    const int seed = (LEAD && prem) ? INF : INTERN_INF + bp;  // A-Q3 seeds (the finishing launch adds them)
+    int pLm00 = seed, pLm01 = INF, pLm10 = INF, pMm00 = seed, pMm10 = INF;
+    int pOm00 = seed, pOm10 = INF;
     int fL1 = INF, fL2 = INF, fM = INF, fO1 = INF, pK1 = INF;
     struct AV { int wb_i, wbp_i, wp_i, wb_j, wbp_j, wp_j, Lm00i, Mm00i, Om00i, fLi, fOi, Lm00j, Mm00j, Lm10j, fLj, fMpj, Kj; };
     auto load_a = [&](int s) {
@@ -1168,8 +1182,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 J[6] = imin(J[6], Kj + wpj + mask);      // PK        :184-187
             }
         };
-        if (1 + part <= a) {
-            int s = 1 + part;
+        if (s_first + part <= a) {
+            int s = s_first + part;
             LA cur = ld(s);
             for (;;) {
                 const int sn = s + split;
@@ -1180,29 +1194,35 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 s = sn;
             }
         }
-        if (split > 1) {  // the followers' slices (r >= 1) of the split waves meet in part 0
+        // slices handed over through the ring: the followers' (r >= 1), and in the prepass scheme
+        // the cell's own (r = 0) too; otherwise r = 0 stays in this wave's accumulators
+        const int r0 = prem ? 0 : 1;
+        if (split > 1) {  // the split waves' slices meet in part 0
             int *slot = red + (wib / split) * (split - 1) * LEAD_RED * 64 + lane;
             if (part > 0) {
 #pragma unroll
-                for (int r = 1; r < SHARE_R; ++r)
+                for (int r = 0; r < SHARE_R; ++r)
 #pragma unroll
                     for (int f = 0; f < 7; ++f) {
-                        slot[((part - 1) * LEAD_RED + (r - 1) * 14 + f) * 64] = AI_[r][f];
-                        slot[((part - 1) * LEAD_RED + (r - 1) * 14 + 7 + f) * 64] = AJ_[r][f];
+                        if (r < r0) continue;
+                        slot[((part - 1) * LEAD_RED + r * 14 + f) * 64] = AI_[r][f];
+                        slot[((part - 1) * LEAD_RED + r * 14 + 7 + f) * 64] = AJ_[r][f];
                     }
             }
             __syncthreads();
             if (part == 0)
                 for (int p = 1; p < split; ++p)
 #pragma unroll
-                    for (int r = 1; r < SHARE_R; ++r)
+                    for (int r = 0; r < SHARE_R; ++r)
 #pragma unroll
                         for (int f = 0; f < 7; ++f) {
-                            AI_[r][f] = imin(AI_[r][f], slot[((p - 1) * LEAD_RED + (r - 1) * 14 + f) * 64]);
-                            AJ_[r][f] = imin(AJ_[r][f], slot[((p - 1) * LEAD_RED + (r - 1) * 14 + 7 + f) * 64]);
+                            if (r < r0) continue;
+                            AI_[r][f] = imin(AI_[r][f], slot[((p - 1) * LEAD_RED + r * 14 + f) * 64]);
+                            AJ_[r][f] = imin(AJ_[r][f], slot[((p - 1) * LEAD_RED + r * 14 + 7 + f) * 64]);
                         }
             __syncthreads();
         }
+        if (!prem) {
         pLm00 = imin(pLm00, imin(AI_[0][0], AJ_[0][0]));
         pLm10 = imin(AI_[0][1], AJ_[0][3]);
         pMm10 = AI_[0][2];
@@ -1215,13 +1235,15 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         fL2 = AJ_[0][4];
         fM = AJ_[0][5];
         pK1 = AJ_[0][6];
+        }
         if (!lane_ok || part != 0) return;
 #pragma unroll
-        for (int r = 1; r < SHARE_R; ++r) {
+        for (int r = 0; r < SHARE_R; ++r) {
+            if (r < r0) continue;
             const int tf = t + r;
             if (tf >= T.g_hi) break;
             const int Mf = LD[tf].M, mf = m - r;
-            uint4 *ring = T.acc + (long long)((tf % SHARE_R) * SHARE_NACC) * T.accC;
+            uint4 *ring = T.acc + (long long)((tf % SHARE_SLOTS) * SHARE_NACC) * T.accC;
             if (i - r >= 1) {
                 const unsigned idx = (unsigned)((a + r) * Mf) + L0 - (unsigned)(r * (h + 1));
                 CHKA(idx);
@@ -1238,10 +1260,10 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #ifdef CCJ_ABLATE_LINEAR
     if (a < 0)
 #endif
-    if (arole == 1) {
-        if constexpr (LEAD) lead_a();
-    } else if (1 + part <= a_stop) {
-        int s = 1 + part;
+    if (arole == 1 && LEAD) {
+        lead_a();
+    } else if (s_first + part <= a_stop) {
+        int s = s_first + part;
         AV cur = load_a(s);
         for (;;) {
             const int sn = s + split;
@@ -1252,8 +1274,11 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             s = sn;
         }
     }
-    if (arole == 2) {  // follower: the leader's partial (split points a%R+1 .. a)
-        const uint4 *ring = T.acc + (long long)((t % SHARE_R) * SHARE_NACC) * T.accC;
+    // the ring record of the a-loop: a follower's leader partial (split points a%R+1 .. a, or
+    // a%R+2 .. a in the prepass scheme), and in the prepass scheme the own s >= 2 partial of a
+    // long-scan side
+    if (prem ? !LEAD : arole == 2) {
+        const uint4 *ring = T.acc + (long long)((t % SHARE_SLOTS) * SHARE_NACC) * T.accC;
         const unsigned idx = (unsigned)(a * Mt) + L0;
         CHKA(idx);
         const uint4 pi = ring[(long long)AI * T.accC + idx], pj = ring[(long long)AJ * T.accC + idx];
@@ -1271,7 +1296,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         pK1 = imin(pK1, lo16(pj.w));
     }
     // ---- fused b-loop: split point d inside [k, l] ----
-    int pRm00 = INTERN_INF + bp, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
+    int pRm00 = seed, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
     int fR1 = INF, fR2 = INF, fMp = INF, fO2 = INF, pK2 = INF;
     struct BV { int wb_k, wbp_k, wp_k, wb_l, wbp_l, wp_l, Rm00k, Mm00k, fRk, PLRk, Kk, Rm00l, Mm00l, Om00l, Mm10l, Om10l, fRl, fOl; };
     auto load_b = [&](int s) {
@@ -1383,8 +1408,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 Q[8] = imin(Q[8], fOl + wpl_ + mask);       // PfromO    :429-431
             }
         };
-        if (1 + part <= b) {
-            int s = 1 + part;
+        if (s_first + part <= b) {
+            int s = s_first + part;
             LB cur = ld(s);
             for (;;) {
                 const int sn = s + split;
@@ -1395,31 +1420,35 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 s = sn;
             }
         }
+        const int r0 = prem ? 0 : 1;
         if (split > 1) {
             int *slot = red + (wib / split) * (split - 1) * LEAD_RED * 64 + lane;
             if (part > 0) {
 #pragma unroll
-                for (int r = 1; r < SHARE_R; ++r) {
+                for (int r = 0; r < SHARE_R; ++r) {
+                    if (r < r0) continue;
 #pragma unroll
-                    for (int f = 0; f < 6; ++f) slot[((part - 1) * LEAD_RED + (r - 1) * 15 + f) * 64] = AK_[r][f];
+                    for (int f = 0; f < 6; ++f) slot[((part - 1) * LEAD_RED + r * 15 + f) * 64] = AK_[r][f];
 #pragma unroll
-                    for (int f = 0; f < 9; ++f) slot[((part - 1) * LEAD_RED + (r - 1) * 15 + 6 + f) * 64] = AL_[r][f];
+                    for (int f = 0; f < 9; ++f) slot[((part - 1) * LEAD_RED + r * 15 + 6 + f) * 64] = AL_[r][f];
                 }
             }
             __syncthreads();
             if (part == 0)
                 for (int p = 1; p < split; ++p)
 #pragma unroll
-                    for (int r = 1; r < SHARE_R; ++r) {
+                    for (int r = 0; r < SHARE_R; ++r) {
+                        if (r < r0) continue;
 #pragma unroll
                         for (int f = 0; f < 6; ++f)
-                            AK_[r][f] = imin(AK_[r][f], slot[((p - 1) * LEAD_RED + (r - 1) * 15 + f) * 64]);
+                            AK_[r][f] = imin(AK_[r][f], slot[((p - 1) * LEAD_RED + r * 15 + f) * 64]);
 #pragma unroll
                         for (int f = 0; f < 9; ++f)
-                            AL_[r][f] = imin(AL_[r][f], slot[((p - 1) * LEAD_RED + (r - 1) * 15 + 6 + f) * 64]);
+                            AL_[r][f] = imin(AL_[r][f], slot[((p - 1) * LEAD_RED + r * 15 + 6 + f) * 64]);
                     }
             __syncthreads();
         }
+        if (!prem) {
         pRm00 = imin(pRm00, imin(AK_[0][0], AL_[0][0]));
         pRm10 = AK_[0][1];
         pMm00 = imin(pMm00, AK_[0][2]);
@@ -1434,13 +1463,15 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         pOm10 = imin(pOm10, AL_[0][6]);
         fR2 = AL_[0][7];
         fO2 = AL_[0][8];
+        }
         if (!lane_ok || part != 0) return;
 #pragma unroll
-        for (int r = 1; r < SHARE_R; ++r) {
+        for (int r = 0; r < SHARE_R; ++r) {
+            if (r < r0) continue;
             const int tf = t + r;
             if (tf >= T.g_hi) break;
             const int Mf = LD[tf].M, mf = m - r;
-            uint4 *ring = T.acc + (long long)((tf % SHARE_R) * SHARE_NACC) * T.accC;
+            uint4 *ring = T.acc + (long long)((tf % SHARE_SLOTS) * SHARE_NACC) * T.accC;
             if (h - r >= 0) {  // k side: AK slots 0..5 (12 bytes; slot 6 belongs to the l-side leader)
                 const int hh = h - r;
                 const unsigned idx = (unsigned)(a * Mf + hh * mf - ((hh * (hh - 1)) >> 1) + i - 1);
@@ -1459,10 +1490,10 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #ifdef CCJ_ABLATE_LINEAR
     if (b < 0)
 #endif
-    if (brole == 1) {
-        if constexpr (LEAD) lead_b();
-    } else if (1 + part <= b_stop) {
-        int s = 1 + part;
+    if (brole == 1 && LEAD) {
+        lead_b();
+    } else if (s_first + part <= b_stop) {
+        int s = s_first + part;
         BV cur = load_b(s);
         for (;;) {
             const int sn = s + split;
@@ -1473,8 +1504,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             s = sn;
         }
     }
-    if (brole == 2) {  // follower: the leaders' partials (split points b%R+1 .. b)
-        const uint4 *ring = T.acc + (long long)((t % SHARE_R) * SHARE_NACC) * T.accC;
+    if (prem ? !LEAD : brole == 2) {  // the b-loop's ring record (as for the a-loop)
+        const uint4 *ring = T.acc + (long long)((t % SHARE_SLOTS) * SHARE_NACC) * T.accC;
         const unsigned idx = (unsigned)(a * Mt) + L0;
         CHKA(idx);
         const uint4 pk = ring[(long long)AK * T.accC + idx], pl = ring[(long long)AL * T.accC + idx];
@@ -1514,6 +1545,27 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         pRm00 = acc[12]; pRm01 = acc[13]; pRm10 = acc[14]; pMm01 = acc[15]; pOm01 = acc[16]; fR1 = acc[17];
         fR2 = acc[18]; fMp = acc[19]; fO2 = acc[20]; pK2 = acc[21];
         if (!lane_ok) return;
+    }
+    if (LEAD && prem) {
+        // prepass launch: the own s >= 2 partials of the full-scan sides go to the ring (the
+        // leaders' sides did inside lead_a / lead_b); the plain launch of level t finishes the cell
+        if (!lane_ok || part != 0) return;
+        uint4 *ring = T.acc + (long long)((t % SHARE_SLOTS) * SHARE_NACC) * T.accC;
+        const unsigned idx = (unsigned)(a * Mt) + L0;
+        CHKA(idx);
+        if (arole == 0) {
+            const int fi[7] = {pLm00, pLm10, pMm10, pOm00, pOm10, fL1, fO1};
+            const int fj[7] = {pLm00, pLm01, pMm00, pLm10, fL2, fM, pK1};
+            ring[(long long)AI * T.accC + idx] = pack_acc(fi, 7);
+            ring[(long long)AJ * T.accC + idx] = pack_acc(fj, 7);
+        }
+        if (brole == 0) {
+            const int fk[7] = {pRm00, pRm10, pMm00, fR1, fMp, pK2, fO2};
+            const int fl[8] = {pRm00, pRm01, pMm01, pOm00, pOm01, pMm10, pOm10, fR2};
+            ring[(long long)AK * T.accC + idx] = pack_acc(fk, 7);
+            ring[(long long)AL * T.accC + idx] = pack_acc(fl, 8);
+        }
+        return;
     }
     // ---- single-step seeds (:519, :533, :566, :580), level t-1
     int vPRm01 = pRm01, vPRm10 = pRm10, vPMm01 = pMm01, vPMm10 = pMm10;
