@@ -7,10 +7,11 @@ interior-loop work lists) followed by the GPU fill of all 22 four-dimensional ga
 2-D matrices, exterior W, traceback and bracket emission (on the GPU; the structure string and MFE
 are copied back) — everything W_final(seq, 2).ccj() does in the reference.  The default sequence
 is the 200-nt headline RNA (random.Random(5), ACGU) with rna_Turner04 tables and dangles 2.
-Inputs are resident before the timed region: the context (HBM allocations, ccj_create) is created
-during setup and its time is reported as `create_ms`.  Every ccj() call returns only after all of
-its streams are synchronized, so the barrier + wall clock around the K steps brackets finished GPU
-work.
+Inputs are resident before the timed region: the contexts (HBM allocations, ccj_create) are
+created during setup and their time is reported as `create_ms`.  With `--inflight 2` a batch of
+folds is pipelined over two contexts per GPU (fold k+1's fill starts when fold k's fill ends, beside
+fold k's W + traceback; measured slower, so the default is 1).  Every fold is complete (ccj_wait)
+before the clock stops, and the barrier + wall clock around the K steps brackets finished GPU work.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 200] [--seed 5] [--params Turner04]
                     [--distinct] [--shard]
@@ -53,6 +54,16 @@ def num_cells(n):
         return 0
     m = n + 1
     return m * (m - 1) * (m - 2) * (m - 3) // 24
+
+
+def footprint_gb(n):
+    """Device memory of one context: 4-D matrices, loop records, interior-loop
+    copies, candidate lists, the sharing ring and the 2-D tables."""
+    cells = num_cells(n)
+    maxc = max(((t + 1) * ((n - t - 2) * (n - t - 1) // 2) for t in range(max(n - 2, 1))), default=0)
+    pmx = 2 * sum((n - t - 2) * n * (t + 1) for t in range(max(n - 2, 0)))
+    plane = (n + 1) * (n + 2)
+    return (44 * cells + 48 * cells + 4 * cells + pmx + 320 * maxc + 2 * 841 * plane + 2 * 848 * 8 * plane) / 1e9
 
 
 def rank_seed(base, rank, world, step, distinct):
@@ -149,6 +160,10 @@ def parse_args(argv=None):
     ap.add_argument("--shard", action="store_true",
                     help="band-shard ONE sequence over all ranks (RCCL all-gather per level, strong scaling) "
                          "instead of one sequence per GPU")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="folds in flight per GPU (contexts): 2 overlaps one fold's traceback and the next "
+                         "sequence's setup with the next fill (default 1, measured faster; 2 only when two "
+                         "contexts fit in HBM, never band-sharded)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the rank launch, barrier and max-over-ranks accounting only (tests)")
     return ap.parse_args(argv)
@@ -201,31 +216,55 @@ def main(argv=None):
     import ctypes
     from ccj_amd import W_final, lib, comm_unique_id
 
+    # 1 by default: with 2 contexts the fill measured 3 ms slower (their streams share
+    # the 4 hardware queues, so one fold's one-wave traceback holds up the other's level launches)
+    inflight = a.inflight if a.inflight is not None else 1
+    if 2 * footprint_gb(a.n) > 200:
+        inflight = 1
+    inflight = 1 if shard else max(1, min(2, inflight))
     t_c = time.perf_counter()
     if shard:
         obj = [comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        wf = W_final(seq_at(0), 2, params=a.params, device=local, shard_world=world, shard_rank=rank, comm_id=obj[0])
+        ctxs = [W_final(seq_at(0), 2, params=a.params, device=local, shard_world=world, shard_rank=rank, comm_id=obj[0])]
     else:
-        wf = W_final(seq_at(0), 2, params=a.params, device=local)
-    create_ms = (time.perf_counter() - t_c) * 1e3
-    for _ in range(a.warmup):
-        wf.reset(seq_at(0))
-        wf.ccj()
+        ctxs = [W_final(seq_at(0), 2, params=a.params, device=local) for _ in range(inflight)]
+    create_ms = (time.perf_counter() - t_c) * 1e3 / len(ctxs)
+
+    def run_steps(nsteps, acc):
+        """nsteps folds, pipelined over the contexts: while fold k's fill (then its W + traceback,
+        one wave) runs on context k % inflight, the host resets the next context to sequence k+1 and
+        enqueues its fill, so the traceback and the setup hide under the next fill."""
+        def start(k):
+            wf = ctxs[k % len(ctxs)]
+            tr = time.perf_counter()
+            wf.reset(seq_at(k))  # per-sequence setup, inside the timed region
+            acc["reset_s"] += time.perf_counter() - tr
+            # the fill of k starts when fill k-1 has ended; k-1's traceback runs beside it
+            wf.fill_async(after=ctxs[(k - 1) % len(ctxs)] if len(ctxs) > 1 and k > 0 else None)
+        start(0)
+        for k in range(nsteps):
+            if len(ctxs) > 1 and k + 1 < nsteps:
+                start(k + 1)
+            wf = ctxs[k % len(ctxs)]
+            wf.wait()
+            tm = wf.timing()
+            acc["level_ms"] += tm["level4d_ms"]  # the levels' durations: HIP events on the level stream
+            acc["fill_ms"] += tm["fill_ms"]
+            acc["last"] = wf
+            if len(ctxs) == 1 and k + 1 < nsteps:
+                start(k + 1)
+
+    run_steps(a.warmup, {"reset_s": 0.0, "level_ms": 0.0, "fill_ms": 0.0}) if a.warmup > 0 else None
     barrier()
+    acc = {"reset_s": 0.0, "level_ms": 0.0, "fill_ms": 0.0, "last": ctxs[0]}
     t0 = time.perf_counter()
-    level_ms = fill_ms = reset_s = 0.0
-    for k in range(a.steps):
-        tr = time.perf_counter()
-        wf.reset(seq_at(k))  # per-sequence setup, inside the timed region
-        reset_s += time.perf_counter() - tr
-        wf.ccj()
-        tm = wf.timing()
-        level_ms += tm["level4d_ms"]  # the levels' durations: HIP events on the level stream
-        fill_ms += tm["fill_ms"]
+    run_steps(a.steps, acc)
     elapsed = time.perf_counter() - t0
     barrier()
-    structure, energy, last_seq = wf.structure, wf.energy, wf.seq
+    reset_s, level_ms, fill_ms = acc["reset_s"], acc["level_ms"], acc["fill_ms"]
+    structure, energy = acc["last"].structure, acc["last"].energy
+    wf = ctxs[0]
     # after the timed region: one fold with marker events around every launch (per-kernel-family
     # times for k_iloop / k_diag2d; the markers slow that fold down, so it is not part of `value`)
     wf.set_timing(2)
@@ -246,7 +285,8 @@ def main(argv=None):
     achieved = (bytes_lv / nlaunch) / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     il_launch_s = il_ms / 1e3 / max(a.n - 6, 1)
     il_achieved = (bytes_il / max(a.n - 6, 1)) / il_launch_s / 1e9 if il_launch_s > 0 else 0.0
-    wf.close()
+    for w in ctxs:
+        w.close()
     # HBM traffic per level, measured with rocprofv3 PMC passes over this same command
     # (tools/gpu_profile.sh -> tools/make_profiles.py -> profiles/traffic.json); null when no
     # profile of this configuration is committed (it is not measured inside this run)
@@ -287,13 +327,15 @@ def main(argv=None):
         "dtype": "int32",
         "data": "synthetic",
         "config": {"workload": f"CCJ pseudoknot MFE fold (ccj_reset + fill + W + traceback) of random ACGU RNA "
-                               f"(random.Random(seed)), rna_{a.params} tables, dangles 2; {wl}",
+                               f"(random.Random(seed)), rna_{a.params} tables, dangles 2; {wl}; "
+                               f"{len(ctxs)} fold(s) in flight per GPU",
                    "n": a.n, "seed": a.seed, "params": a.params, "cells_per_fold": cells,
                    "parallelism": f"band{world}" if shard else f"batch{world}"},
         "sec_per_sequence": sec_per_step,  # latency of one fold (every rank folds one per step in batch mode)
         "sequences_per_s": seqs_per_step * a.steps / elapsed,
         "create_ms": create_ms,
         "setup_ms": reset_s / a.steps * 1e3,
+        "inflight": len(ctxs),
         "mfe": energy,
         "structure": structure,
         "rank0_last_seq_seed": a.seed if shard else rank_seed(a.seed, 0, world, a.steps - 1, a.distinct),

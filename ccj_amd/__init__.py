@@ -98,6 +98,12 @@ def lib() -> ctypes.CDLL:
         getattr(L, fn).restype = ip
     L.ccj_reset.argtypes = [vp, cp]
     L.ccj_reset.restype = ip
+    L.ccj_fill_async.argtypes = [vp]
+    L.ccj_fill_async.restype = ip
+    L.ccj_fill_async_after.argtypes = [vp, vp]
+    L.ccj_fill_async_after.restype = ip
+    L.ccj_wait.argtypes = [vp, cp, ctypes.POINTER(ctypes.c_double), cp, ip]
+    L.ccj_wait.restype = ip
     L.ccj_result.argtypes = [vp, cp, ctypes.POINTER(ctypes.c_double), cp, ip]
     L.ccj_result.restype = ip
     L.ccj_get4.argtypes = [vp, ip, ip, ip, ip, ip]
@@ -315,6 +321,31 @@ class W_final:
         """reference W_final::ccj (W_final.cc:58-105)"""
         self.fill()
         return self.result()
+
+    def fill_async(self, after: Optional["W_final"] = None) -> None:
+        """Enqueue fill + W + traceback and return at once (include/ccj.h ccj_fill_async); with
+        `after`, the fill starts when that context's last enqueued fill has ended."""
+        if after is None:
+            self._check(lib().ccj_fill_async(self._h))
+        else:
+            self._check(lib().ccj_fill_async_after(self._h, after._h))
+
+    def wait(self) -> float:
+        """Finish a fill_async: same results (and exceptions) as ccj()."""
+        L = lib()
+        buf = ctypes.create_string_buffer(self.n + 1)
+        msgs = ctypes.create_string_buffer(1 << 16)
+        e = ctypes.c_double()
+        rc = L.ccj_wait(self._h, buf, ctypes.byref(e), msgs, 1 << 16)
+        self.stdout_msgs = msgs.value.decode()
+        if rc == CCJ_E_BACKTRACK or rc == CCJ_E_INTER_EXIT:
+            err = L.ccj_last_error(self._h).decode()
+            exit_code = 0 if rc == CCJ_E_INTER_EXIT else (134 if "Assertion" in err else 1)
+            raise BacktrackExit(rc, err, exit_code, self.stdout_msgs)
+        self._check(rc)
+        self.structure = buf.value.decode()
+        self.energy = e.value
+        return self.energy
 
     # ---- matrix access (reference getter semantics) ----
     def get4(self, mat, i, j, k, l) -> int:

@@ -33,6 +33,7 @@
 #include "ccj_energy.h"
 #include "ccj_engine.h"
 #include "ccj_backtrack.h"
+#include "ccj_items.h"
 
 using namespace ccj;
 
@@ -146,6 +147,9 @@ struct ccj_ctx {
     std::vector<int> xnmax;               // per level: the largest rank's block count (slice = 22 x nmax x M)
     ccj_group *lgroup = nullptr;          // in-process exchange between contexts (tests), else RCCL
     long long *d_icount = nullptr, *d_ioff = nullptr;  // k_items: items per (t, r), first item
+    long long *h_ioff = nullptr;          // pinned staging of it_off
+    void *h_stage = nullptr;              // pinned staging of the sequence tables
+    hipEvent_t ev_stage = nullptr;        // the uploads from the staging (and h_ioff) are done
     std::vector<long long> it_off;        // first item of (level t, shard r) at t*world + r
     uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
@@ -174,6 +178,12 @@ struct ccj_ctx {
     std::vector<int8_t> hvt;
     std::vector<int> hpt_h;   // pair type table [w][p] host copy (int)
     bool filled = false, mirrored = false, mirrored2d = false;
+    bool pending = false;                 // a fill is enqueued and not yet finished (fill_finish)
+    bool res_pending = false;             // W + traceback enqueued (result_enqueue), not yet read
+    hipEvent_t ev_res = nullptr;          // device traceback results copied to the pinned buffers
+    int *hr_W = nullptr, *hr_fp = nullptr;  // pinned: W, f[].pair, f[].type, the exit record
+    int8_t *hr_ft = nullptr;
+    BtOut *hr_bo = nullptr;
     std::vector<int> W;
 
     double fill_ms = 0, level_ms = 0, diag_ms = 0, pre_ms = 0, il_ms = 0;
@@ -1469,17 +1479,75 @@ static int seq_setup(ccj_ctx *c) {
             }
         }
     lap("tables");
-    HIPCHK(cp, hipMemcpy(c->d_pt, pt.data(), plane, hipMemcpyHostToDevice));
-    // ---- k_iloop work items (one per wave), built on the GPU by k_items: count per (level, shard),
-    // offsets on the host, then write
+    // the sequence tables go up asynchronously on st from pinned staging (a reset never blocks on
+    // work another context has running on the GPU); the fill's launches follow on st
+    const size_t stage_bytes = plane * (1 + sizeof(int) + sizeof(int16_t)) + 2 * (size_t)(n + 2) * sizeof(short);
+    if (!c->h_stage) {
+        HIPCHK(cp, hipHostMalloc(&c->h_stage, stage_bytes, hipHostMallocDefault));
+        HIPCHK(cp, hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
+    } else {
+        HIPCHK(cp, hipEventSynchronize(c->ev_stage));  // the previous uploads have read the staging
+    }
+    char *stg = (char *)c->h_stage;
+    auto up = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
+        memcpy(stg, src, bytes);
+        const hipError_t e = hipMemcpyAsync(dst, stg, bytes, hipMemcpyHostToDevice, c->st);
+        stg += bytes;
+        return e;
+    };
+    HIPCHK(cp, up(c->d_pt, pt.data(), plane));
+    // ---- k_iloop work items (one per wave): counted per (level, shard) on host threads (the same
+    // enumeration as the GPU builder, ccj_items.h; no device round trip, so a reset never waits
+    // for a fold running on the GPU), written by k_items on the GPU at the prefix offsets
     {
         if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
         const int G = c->world;
         const int nb = n * G;
-        HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, nullptr, nullptr, 0, c->st));
-        std::vector<long long> cnt((size_t)nb);
-        HIPCHK(cp, hipMemcpyAsync(cnt.data(), c->d_icount, nb * sizeof(long long), hipMemcpyDeviceToHost, c->st));
-        HIPCHK(cp, hipStreamSynchronize(c->st));
+        const int rs = c->rs;
+        struct HostPT {
+            const int8_t *pt;
+            int rs;
+            int operator()(int i, int j) const { return pt[(size_t)(j - i) * rs + i]; }
+        } hpt{pt.data(), rs};
+        std::vector<long long> cnt((size_t)nb, 0);
+        // default: counted on the GPU by k_items (0.2 ms + one round trip; 0.5 ms setup at n=200);
+        // CCJ_HOST_COUNT=1: on host threads (≈1 ms, but no device round trip, so a reset never
+        // waits behind another context's fill on a shared hardware queue)
+        static const bool host_count = getenv("CCJ_HOST_COUNT") && atoi(getenv("CCJ_HOST_COUNT")) != 0;
+        if (!host_count) {
+            HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, nullptr, nullptr, 0, c->st));
+            HIPCHK(cp, hipMemcpyAsync(cnt.data(), c->d_icount, nb * sizeof(long long), hipMemcpyDeviceToHost, c->st));
+            HIPCHK(cp, hipStreamSynchronize(c->st));
+        }
+        std::atomic<int> next{0};
+        static const bool check = getenv("CCJ_CHECK_ITEMS") && atoi(getenv("CCJ_CHECK_ITEMS")) != 0;
+        std::atomic<bool> bad{false};
+        auto worker = [&]() {
+            for (int b; (b = next.fetch_add(1)) < nb;) {
+                const int t = b / G, r = b % G;
+                if (!(c->simulate || r == c->rank) || t < 4 || t >= c->nlev) continue;
+                const long long hc = count_level_items(pt.data(), rs, n, t, G, r);
+                if (!host_count && hc != cnt[b]) bad = true;  // check mode: host and GPU counts agree
+                cnt[b] = hc;
+                if (check) {  // CCJ_CHECK_ITEMS=1: the generic enumeration must agree
+                    const ItemRows R = item_rows(n, t, G, r);
+                    long long sum = 0;
+                    uint32_t it0;
+                    for (int x = 0; x < R.nPL + R.nPR + R.nPM; ++x) sum += item_row(hpt, n, t, R, x, G, r, it0);
+                    if (sum != cnt[b]) bad = true;
+                }
+            }
+        };
+        if (host_count || check) {
+            if (!host_count) next = nb;  // check mode only: the GPU counts stay
+            if (check) next = 0;
+            const int nth = std::max(1, std::min<int>(8, (int)std::thread::hardware_concurrency()));
+            std::vector<std::thread> pool;
+            for (int x = 1; x < nth; ++x) pool.emplace_back(worker);
+            worker();
+            for (auto &th : pool) th.join();
+        }
+        if (bad) return set_err(cp, CCJ_E_STATE, "k_iloop item count pass disagrees with the enumeration");
         c->it_off.assign((size_t)nb + 1, 0);
         for (int x = 0; x < nb; ++x) c->it_off[x + 1] = c->it_off[x] + cnt[x];
         const size_t total = (size_t)c->it_off[nb];
@@ -1491,14 +1559,17 @@ static int seq_setup(ccj_ctx *c) {
             HIPCHK(cp, hipMalloc(&c->d_items, c->items_cap * sizeof(uint32_t)));
         }
         c->T.items = c->d_items;
-        HIPCHK(cp, hipMemcpyAsync(c->d_ioff, c->it_off.data(), (nb + 1) * sizeof(long long), hipMemcpyHostToDevice, c->st));
+        // pinned staging so the upload is asynchronous on st (the fill's first launches follow it)
+        if (!c->h_ioff) HIPCHK(cp, hipHostMalloc(&c->h_ioff, ((size_t)nb + 1) * sizeof(long long), hipHostMallocDefault));
+        memcpy(c->h_ioff, c->it_off.data(), ((size_t)nb + 1) * sizeof(long long));
+        HIPCHK(cp, hipMemcpyAsync(c->d_ioff, c->h_ioff, (nb + 1) * sizeof(long long), hipMemcpyHostToDevice, c->st));
         HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, c->d_ioff, c->d_items, 1, c->st));
-        // the fill's first launches are on st too (k_iloop waits for ev_pre, recorded on st)
     }
-    HIPCHK(cp, hipMemcpy(c->d_hp, hp.data(), plane * sizeof(int), hipMemcpyHostToDevice));
-    HIPCHK(cp, hipMemcpy(c->d_est, est.data(), plane * sizeof(int16_t), hipMemcpyHostToDevice));
-    HIPCHK(cp, hipMemcpy(c->d_S, c->S.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
-    HIPCHK(cp, hipMemcpy(c->d_S1, c->S1.data(), (n + 2) * sizeof(short), hipMemcpyHostToDevice));
+    HIPCHK(cp, up(c->d_hp, hp.data(), plane * sizeof(int)));
+    HIPCHK(cp, up(c->d_est, est.data(), plane * sizeof(int16_t)));
+    HIPCHK(cp, up(c->d_S, c->S.data(), (n + 2) * sizeof(short)));
+    HIPCHK(cp, up(c->d_S1, c->S1.data(), (n + 2) * sizeof(short)));
+    HIPCHK(cp, hipEventRecord(c->ev_stage, c->st));
     lap("upload");
     c->filled = c->mirrored = c->mirrored2d = false;
     return CCJ_OK;
@@ -1857,21 +1928,30 @@ extern "C" int ccj_reset(ccj_ctx *c, const char *seq) {
     for (char ch : s)
         if (!(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'U' || ch == 'T'))
             return set_err(c, CCJ_E_ARG, "ccj_reset: invalid character in sequence");
+    if (c->pending || c->res_pending) return set_err(c, CCJ_E_STATE, "ccj_reset: a fold is in flight (ccj_wait first)");
     HIPCHK(c, hipSetDevice(c->device));
-    // the previous fold's streams may still read the sequence tables
-    for (hipStream_t q : {c->st, c->st_copy, c->st_p, c->st_il, c->st_d, c->st_pre}) HIPCHK(c, hipStreamSynchronize(q));
+    // no fold is in flight (checked above): ccj_wait / ccj_fill returned only after the fill and
+    // the traceback completed, so the streams are idle.  Only the optional host-mirror copies can
+    // still run.  (A hipStreamSynchronize here would enqueue a marker that can wait behind another
+    // context's fill on a shared hardware queue.)
+    if (c->overlap && c->h4) HIPCHK(c, hipStreamSynchronize(c->st_copy));
     c->seq = s;
     c->W.clear();
     return seq_setup(c);
 }
 
-extern "C" int ccj_fill_device(ccj_ctx *c) {
+// Enqueue the whole fill on the context's streams; it ends with ev_end on st, after which every
+// stream's work of the fill is complete (st waits for the last span, which waits for the last P,
+// and every level waited for its k_iloop / leader launches).
+static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     if (!c) return CCJ_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     const int n = c->n;
     hipStream_t st = c->st;
+    // pipelining (ccj_fill_async_after): start when the other context's last enqueued fill has
+    // ended (its ev_end; its W + traceback may still run beside this fill)
+    if (after && after != c && after->ev_end) HIPCHK(c, hipStreamWaitEvent(st, after->ev_end, 0));
     const auto enq0 = std::chrono::steady_clock::now();
-    const size_t plane = (size_t)(n + 1) * c->rs;
     c->filled = c->mirrored = c->mirrored2d = false;
     HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), st));
     HIPCHK(c, hipEventRecord(c->ev_start, st));
@@ -1984,11 +2064,17 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     // join: the fill ends when the last level and the last span are done
     HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[n - 1], 0));
     HIPCHK(c, hipEventRecord(c->ev_end, st));
-    HIPCHK(c, hipStreamSynchronize(st));
-    HIPCHK(c, hipStreamSynchronize(c->st_p));
-    HIPCHK(c, hipStreamSynchronize(c->st_il));
-    HIPCHK(c, hipStreamSynchronize(c->st_d));
-    HIPCHK(c, hipStreamSynchronize(c->st_pre));
+    c->pending = true;
+    return CCJ_OK;
+}
+
+// Wait for an enqueued fill, check the device error word and read its timings.
+static int fill_finish(ccj_ctx *c) {
+    if (!c || !c->pending) return c ? set_err(c, CCJ_E_STATE, "no fill in flight") : CCJ_E_ARG;
+    c->pending = false;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int n = c->n;
+    HIPCHK(c, hipEventSynchronize(c->ev_end));
     int herr = 0;
     HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (herr & 1) return set_err(c, CCJ_E_PARAMS, "e_intP table value outside int16 range (flags %d)", herr);
@@ -2030,8 +2116,12 @@ extern "C" int ccj_fill_device(ccj_ctx *c) {
     c->diag_ms = dsum;
     c->il_ms = isum;
     c->filled = true;
-    (void)plane;
     return CCJ_OK;
+}
+
+extern "C" int ccj_fill_device(ccj_ctx *c) {
+    if (const int rc = fill_enqueue(c)) return rc;
+    return fill_finish(c);
 }
 
 extern "C" int ccj_sync_host(ccj_ctx *c) {
@@ -2060,6 +2150,7 @@ extern "C" int ccj_sync_host(ccj_ctx *c) {
 }
 
 extern "C" int ccj_fill(ccj_ctx *c) {
+    if (c && (c->pending || c->res_pending)) return set_err(c, CCJ_E_STATE, "ccj_fill: a fold is in flight (ccj_wait first)");
     int rc = ccj_fill_device(c);
     if (rc) return rc;
     // the device traceback needs no host mirror; getters make it on demand (ccj_sync_host)
@@ -2085,25 +2176,42 @@ int ensure_mirror_2d(const ccj_ctx *cc) {
 }
 
 // W + traceback on the GPU (ccj_backtrack.hip); brackets on the host
-int device_result(ccj_ctx *c, std::string &structure, std::string &out) {
-    const auto t0 = std::chrono::steady_clock::now();
+// W + traceback on the GPU (ccj_backtrack.hip), enqueued on st behind the fill; the outputs land in
+// pinned host buffers, ev_res marks them complete
+int result_enqueue(ccj_ctx *c) {
     const int n = c->n;
     HIPCHK(c, hipSetDevice(c->device));
+    if (!c->hr_W) {
+        HIPCHK(c, hipHostMalloc(&c->hr_W, (n + 1) * sizeof(int), hipHostMallocDefault));
+        HIPCHK(c, hipHostMalloc(&c->hr_fp, (n + 1) * sizeof(int), hipHostMallocDefault));
+        HIPCHK(c, hipHostMalloc(&c->hr_ft, n + 1, hipHostMallocDefault));
+        HIPCHK(c, hipHostMalloc(&c->hr_bo, sizeof(BtOut), hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_res, hipEventDisableTiming));
+    }
     HIPCHK(c, (hipError_t)ccjk_compute_W(&c->T, c->d_W, c->d_wterm, c->st));
     const int cap = std::min(4 * n + 64, 3000);
     HIPCHK(c, (hipError_t)ccjk_backtrack(&c->T, c->d_W, c->d_fpair, c->d_ftype, c->d_btout, cap, c->st));
-    BtOut bo{};
-    std::vector<int> fp(n + 1);
-    std::vector<int8_t> ft(n + 1);
-    c->W.assign(n + 1, 0);
-    HIPCHK(c, hipMemcpyAsync(c->W.data(), c->d_W, (n + 1) * sizeof(int), hipMemcpyDeviceToHost, c->st));
-    HIPCHK(c, hipMemcpyAsync(fp.data(), c->d_fpair, (n + 1) * sizeof(int), hipMemcpyDeviceToHost, c->st));
-    HIPCHK(c, hipMemcpyAsync(ft.data(), c->d_ftype, n + 1, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(c, hipMemcpyAsync(&bo, c->d_btout, sizeof bo, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    HIPCHK(c, hipMemcpyAsync(c->hr_W, c->d_W, (n + 1) * sizeof(int), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(c->hr_fp, c->d_fpair, (n + 1) * sizeof(int), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(c->hr_ft, c->d_ftype, n + 1, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(c->hr_bo, c->d_btout, sizeof(BtOut), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipEventRecord(c->ev_res, c->st));
+    c->res_pending = true;
+    return CCJ_OK;
+}
+
+// wait for result_enqueue's outputs; the reference's exits, then brackets on the host
+int result_finish(ccj_ctx *c, std::string &structure, std::string &out, std::chrono::steady_clock::time_point t0) {
+    const int n = c->n;
+    if (!c->res_pending) return set_err(c, CCJ_E_STATE, "no traceback in flight");
+    c->res_pending = false;
+    HIPCHK(c, hipEventSynchronize(c->ev_res));
+    const BtOut bo = *c->hr_bo;
+    c->W.assign(c->hr_W, c->hr_W + n + 1);
     c->w_ms = 0;
     c->bt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->bt_steps = bo.steps;
+    const int cap = std::min(4 * n + 64, 3000);
     for (int x = 0; x < bo.n_snbh; ++x) out += "Should not be here!\n";
     switch (bo.status) {
         case BT_OK: break;
@@ -2126,11 +2234,34 @@ int device_result(ccj_ctx *c, std::string &structure, std::string &out) {
     HostView H(c);
     Backtracker B(H, c);
     for (int x = 1; x <= n; ++x) {
-        B.f[x].pair = fp[x];
-        B.f[x].type = (char)ft[x];
+        B.f[x].pair = c->hr_fp[x];
+        B.f[x].type = (char)c->hr_ft[x];
     }
     B.fill_structure();
     structure = B.structure;
+    return CCJ_OK;
+}
+
+int device_result(ccj_ctx *c, std::string &structure, std::string &out) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (const int rc = result_enqueue(c)) return rc;
+    return result_finish(c, structure, out, t0);
+}
+
+// the reference's outputs of W_final::ccj() (W_final.cc:79-104) into the caller's buffers
+int emit_result(ccj_ctx *c, int rc, const std::string &st, const std::string &out, char *structure, double *energy_kcal,
+                char *msgs, int msgs_cap) {
+    if (msgs && msgs_cap > 0) {
+        const size_t nb = std::min((size_t)msgs_cap - 1, out.size());
+        memcpy(msgs, out.data(), nb);
+        msgs[nb] = 0;
+    }
+    if (rc != CCJ_OK) return rc;
+    if (energy_kcal) *energy_kcal = c->W[c->n] / 100.0;
+    if (structure) {
+        memcpy(structure, st.data() + 1, c->n);
+        structure[c->n] = 0;
+    }
     return CCJ_OK;
 }
 }  // namespace
@@ -2161,18 +2292,34 @@ extern "C" int ccj_result(ccj_ctx *c, char *structure, double *energy_kcal, char
         st = B.structure;
         out = B.out;
     }
-    if (msgs && msgs_cap > 0) {
-        const size_t nb = std::min((size_t)msgs_cap - 1, out.size());
-        memcpy(msgs, out.data(), nb);
-        msgs[nb] = 0;
+    return emit_result(c, rc, st, out, structure, energy_kcal, msgs, msgs_cap);
+}
+
+extern "C" int ccj_fill_async_after(ccj_ctx *c, const ccj_ctx *after) {
+    if (!c) return CCJ_E_ARG;
+    if (c->pending || c->res_pending) return set_err(c, CCJ_E_STATE, "ccj_fill_async: a fold is already in flight");
+    if (after && after->device != c->device) return set_err(c, CCJ_E_ARG, "ccj_fill_async_after: contexts on different devices");
+    if (const int rc = fill_enqueue(c, after)) return rc;
+    // the device traceback follows the fill on the same stream; the host traceback needs the mirror
+    return c->host_tb ? CCJ_OK : result_enqueue(c);
+}
+
+extern "C" int ccj_fill_async(ccj_ctx *c) { return ccj_fill_async_after(c, nullptr); }
+
+extern "C" int ccj_wait(ccj_ctx *c, char *structure, double *energy_kcal, char *msgs, int msgs_cap) {
+    if (!c) return CCJ_E_ARG;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (const int rc = fill_finish(c)) {
+        c->res_pending = false;
+        return rc;
     }
-    if (rc != CCJ_OK) return rc;
-    if (energy_kcal) *energy_kcal = c->W[c->n] / 100.0;
-    if (structure) {
-        memcpy(structure, st.data() + 1, c->n);
-        structure[c->n] = 0;
+    if (c->host_tb) {
+        if (const int rc = ccj_sync_host(c)) return rc;
+        return ccj_result(c, structure, energy_kcal, msgs, msgs_cap);
     }
-    return CCJ_OK;
+    std::string st, out;
+    const int rc = result_finish(c, st, out, t0);
+    return emit_result(c, rc, st, out, structure, energy_kcal, msgs, msgs_cap);
 }
 
 extern "C" int ccj_get4(const ccj_ctx *c, int mat, int i, int j, int k, int l) {
@@ -2526,6 +2673,14 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_items);
     hipFree(c->d_send);
     hipFree(c->d_recv);
+    if (c->h_ioff) hipHostFree(c->h_ioff);
+    if (c->h_stage) hipHostFree(c->h_stage);
+    if (c->ev_stage) hipEventDestroy(c->ev_stage);
+    if (c->hr_W) hipHostFree(c->hr_W);
+    if (c->hr_fp) hipHostFree(c->hr_fp);
+    if (c->hr_ft) hipHostFree(c->hr_ft);
+    if (c->hr_bo) hipHostFree(c->hr_bo);
+    if (c->ev_res) hipEventDestroy(c->ev_res);
     hipFree(c->d_icount);
     hipFree(c->d_ioff);
     hipFree(c->d_ilseg);

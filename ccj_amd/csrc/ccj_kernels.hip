@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include "ccj_engine.h"
 #include "ccj_energy.h"
+#include "ccj_items.h"
 
 using namespace ccj;
 
@@ -499,52 +500,11 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
 // (level t, shard r) walks its "rows" (one closing pair each) 256 at a time; pass 0 counts the
 // items, pass 1 writes them at offs[t*G+r] + an exclusive scan of the row counts.
 // ------------------------------------------------------------------------------------------
-struct ItemRows {
-    int m, oPL0, nPLa, nPRa, nPL, nPR, nPM;
+// the row enumeration (ItemRows, item_row) is shared with the host's count pass: ccj_items.h
+struct DevPT {
+    const DevTables *T;
+    __device__ int operator()(int i, int j) const { return ptype(*T, i, j); }
 };
-// rows of level t for rank r of G (its own a-blocks, ccj_engine.h shard_a)
-__device__ __forceinline__ ItemRows item_rows(int n, int t, int G, int r) {
-    ItemRows R;
-    R.m = n - t - 2;
-    R.oPL0 = shard_ceil(6, G, r);
-    R.nPLa = imax(0, shard_count(t, G, r) - R.oPL0);
-    R.nPRa = t >= 6 ? shard_count(t - 6, G, r) : 0;
-    R.nPL = R.nPLa * R.m;
-    R.nPR = R.nPRa * R.m;
-    R.nPM = imax(0, R.m - 2) * n;
-    return R;
-}
-// rank r's a-blocks of a PM pair (j, k = j+h+2) at level t: own indices [o0, o1]
-__device__ __forceinline__ void pm_own_range(int n, int t, int j, int k, int G, int r, int &o0, int &o1) {
-    const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, j - 1);
-    o0 = shard_ceil(alo, G, r);
-    o1 = ahi >= alo ? shard_count(ahi, G, r) - 1 : o0 - 1;
-}
-// items of row x and the first of them (chunk 0); 0 when the pair cannot pair
-__device__ __forceinline__ int item_row(const DevTables &T, int t, const ItemRows &R, int x, int G, int r, uint32_t &it0) {
-    const int n = T.n, m = R.m;
-    if (x < R.nPL) {
-        const int a = shard_a(R.oPL0 + x / m, G, r), i = 1 + x % m;
-        it0 = (0u << 30) | ((uint32_t)a << 20) | ((uint32_t)i << 10);
-        return ptype(T, i, i + a) > 0 ? (m - i) / 64 + 1 : 0;
-    }
-    x -= R.nPL;
-    if (x < R.nPR) {
-        const int a = shard_a(x / m, G, r), q = x % m;
-        const int k = q + a + 3, b = t - a;
-        it0 = (1u << 30) | ((uint32_t)a << 20) | ((uint32_t)q << 10);
-        return ptype(T, k, k + b) > 0 ? q / 64 + 1 : 0;
-    }
-    x -= R.nPR;
-    const int h = 2 + x / n, j = 1 + x % n;
-    const int k = j + h + 2;
-    if (k > n) return 0;
-    int o0, o1;
-    pm_own_range(n, t, j, k, G, r, o0, o1);
-    if (o0 > o1 || ptype(T, j, k) <= 0) return 0;
-    it0 = (2u << 30) | ((uint32_t)h << 20) | ((uint32_t)j << 10);
-    return (o1 - o0) / 64 + 1;
-}
 
 __global__ __launch_bounds__(256) void k_items(DevTables T, int G, int rank, int simulate,
                                                long long *counts, const long long *__restrict__ offs, uint32_t *items,
@@ -559,12 +519,13 @@ __global__ __launch_bounds__(256) void k_items(DevTables T, int G, int rank, int
         return;  // whole workgroup
     }
     const ItemRows R = item_rows(T.n, t, G, r);
+    const DevPT pt{&T};
     const int nrows = R.nPL + R.nPR + R.nPM;
     long long base = pass ? offs[b] : 0;
     for (int c0 = 0; c0 < nrows; c0 += 256) {
         const int x = c0 + tid;
         uint32_t it0 = 0;
-        const int cnt = x < nrows ? item_row(T, t, R, x, G, r, it0) : 0;
+        const int cnt = x < nrows ? item_row(pt, T.n, t, R, x, G, r, it0) : 0;
         // exclusive scan of cnt over the workgroup: wave scan, then the wave totals
         int inc = cnt;
 #pragma unroll
@@ -876,7 +837,7 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         const int g = h + 2, k = j + g;
         // the rank's own a-blocks in the window (all of [alo, ahi] when unsharded): lanes = own index
         int o0, o1;
-        pm_own_range(n, t, j, k, G_SH, rank, o0, o1);
+        pm_own_range(n, t, j, k, G_SH, rank, o0, o1);  // ccj_items.h
         const ILGroups lg = il_groups(imin(64, o1 - o0 - zc * 64 + 1), lane);
         const int G = lg.G, gq = lg.gq;
         const int o = o0 + zc * 64 + lg.rl;

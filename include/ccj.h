@@ -110,6 +110,18 @@ int  ccj_sync_host(ccj_ctx *ctx);
  * ("Should not be here!\n" lines, W_final.cc:715), NUL-terminated, may be NULL. */
 int  ccj_result(ccj_ctx *ctx, char *structure, double *energy_kcal, char *stdout_msgs, int msgs_cap);
 
+/* Asynchronous fold, for pipelining a batch over contexts: ccj_fill_async enqueues the fill and
+ * (device traceback) W + traceback on the context's streams and returns at once; ccj_wait blocks
+ * until they are done and returns exactly what ccj_fill + ccj_result would.  While one context's
+ * traceback (one wave) runs, another context's fill can use the rest of the GPU.  One fold in
+ * flight per context; ccj_reset / ccj_fill refuse with CCJ_E_STATE until ccj_wait. */
+int  ccj_fill_async(ccj_ctx *ctx);
+/* The same, but the fill starts only when `after`'s last enqueued fill has ended (not its W +
+ * traceback): two contexts on one device then alternate fills back to back while each fold's
+ * traceback runs beside the next fill.  after == NULL: ccj_fill_async. */
+int  ccj_fill_async_after(ccj_ctx *ctx, const ccj_ctx *after);
+int  ccj_wait(ccj_ctx *ctx, char *structure, double *energy_kcal, char *stdout_msgs, int msgs_cap);
+
 /* Reference getter semantics (matrices.hh:177-182: INF outside i<=j<k-1<=l-1). */
 int  ccj_get4(const ccj_ctx *ctx, int mat, int i, int j, int k, int l);
 /* Raw 2-D value for 1 <= i <= j <= n (ccj_mat2). */

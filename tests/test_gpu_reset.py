@@ -88,3 +88,43 @@ def test_reset_sharded_simulation():
             o.close()
     finally:
         wf.close()
+
+
+def test_pipelined_contexts_match_synchronous_folds():
+    """Two contexts in flight (ccj_fill_async / ccj_wait, as bench.py runs a batch): every fold
+    equals the synchronous fold of the same sequence, backtrack exits included."""
+    from ccj_amd import W_final, CCJError
+    n = 90
+    seqs = [_rseq(300 + k, n, "ACGU" if k % 3 else "GGCCAU") for k in range(6)]
+    sync = []
+    ref = W_final(seqs[0], 2, params="Turner04")
+    try:
+        for sq in seqs:
+            ref.reset(sq)
+            sync.append(_outcome(ref))
+    finally:
+        ref.close()
+
+    def waited(wf):
+        from ccj_amd import BacktrackExit
+        try:
+            return ("ok", wf.wait(), wf.structure, wf.stdout_msgs)
+        except BacktrackExit as ex:
+            return ("exit", ex.exit_code, ex.msg, ex.stdout)
+
+    ctx = [W_final(seqs[0], 2, params="Turner04"), W_final(seqs[1], 2, params="Turner04")]
+    try:
+        got = []
+        ctx[0].fill_async()
+        with pytest.raises(CCJError):
+            ctx[0].reset(seqs[2])  # a fold is in flight
+        for k in range(len(seqs)):
+            if k + 1 < len(seqs):
+                nxt = ctx[(k + 1) % 2]
+                nxt.reset(seqs[k + 1])
+                nxt.fill_async()
+            got.append(waited(ctx[k % 2]))
+        assert got == sync
+    finally:
+        for wf in ctx:
+            wf.close()
