@@ -33,31 +33,31 @@ struct DV {
     const int *W;
     mutable int bad;  // Matrix4D::get_uc assert (matrices.hh:167) hit by this lane
 
-    __device__ int pr(int i, int j) const { return T.pair[T.S[i] * 8 + T.S[j]]; }
-    __device__ int a2(const int *A, int i, int j) const { return A[(j - i) * rs + i]; }
+    __device__ __forceinline__ int pr(int i, int j) const { return T.pair[T.S[i] * 8 + T.S[j]]; }
+    __device__ __forceinline__ int a2(const int *A, int i, int j) const { return A[(j - i) * rs + i]; }
     // s_energy_matrix.hh:37-43
-    __device__ int V(int i, int j) const { return i >= j ? INF : a2(T.V, i, j); }
-    __device__ int Vtype(int i, int j) const { return T.Vt[(j - i) * rs + i]; }
-    __device__ int WM(int i, int j) const { return i >= j ? INF : a2(T.WM, i, j); }
-    __device__ int WMv(int i, int j) const { return i >= j ? INF : a2(T.WMv, i, j); }
-    __device__ int WMp(int i, int j) const { return i >= j ? INF : a2(T.WMp, i, j); }
+    __device__ __forceinline__ int V(int i, int j) const { return i >= j ? INF : a2(T.V, i, j); }
+    __device__ __forceinline__ int Vtype(int i, int j) const { return T.Vt[(j - i) * rs + i]; }
+    __device__ __forceinline__ int WM(int i, int j) const { return i >= j ? INF : a2(T.WM, i, j); }
+    __device__ __forceinline__ int WMv(int i, int j) const { return i >= j ? INF : a2(T.WMv, i, j); }
+    __device__ __forceinline__ int WMp(int i, int j) const { return i >= j ? INF : a2(T.WMp, i, j); }
     // TriangleMatrix::get (matrices.hh:38-41)
-    __device__ int Pg(int i, int j) const { return i > j ? INF : a2(T.P, i, j); }
-    __device__ int WBPg(int i, int j) const { return i > j ? INF : a2(T.WBP, i, j); }
-    __device__ int WPPg(int i, int j) const { return i > j ? INF : a2(T.WPP, i, j); }
+    __device__ __forceinline__ int Pg(int i, int j) const { return i > j ? INF : a2(T.P, i, j); }
+    __device__ __forceinline__ int WBPg(int i, int j) const { return i > j ? INF : a2(T.WBP, i, j); }
+    __device__ __forceinline__ int WPPg(int i, int j) const { return i > j ? INF : a2(T.WPP, i, j); }
     // pseudo_loop.cc:647-661
-    __device__ int WB(int i, int j) const {
+    __device__ __forceinline__ int WB(int i, int j) const {
         if (i <= 0 || j <= 0 || i > n || j > n) return INF;
         if (i > j) return 0;
         return imin(T.pen.cp * (j - i + 1), WBPg(i, j));
     }
-    __device__ int WP(int i, int j) const {
+    __device__ __forceinline__ int WP(int i, int j) const {
         if (i <= 0 || j <= 0 || i > n || j > n) return INF;
         if (i > j) return 0;
         return imin(T.pen.PUP * (j - i + 1), WPPg(i, j));
     }
     // Matrix4D::get (matrices.hh:177-182) with get_uc's live assert
-    __device__ int g4(int x, int i, int j, int k, int l) const {
+    __device__ __forceinline__ int g4(int x, int i, int j, int k, int l) const {
         if (!(i <= j && j < k - 1 && k <= l)) return INF;
         if (i <= 0 || l > n) {
             bad = 1;
@@ -67,17 +67,17 @@ struct DV {
         const LvlDev L = T.ld[t];
         return (int)T.d4[L.lb + (long long)x * L.C + (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) + i - 1];
     }
-    __device__ bool can_pair(int i, int j) const { return (j - i > TURN) && pr(i, j) > 0; }  // pseudo_loop.hh:131-135
+    __device__ __forceinline__ bool can_pair(int i, int j) const { return (j - i > TURN) && pr(i, j) > 0; }  // pseudo_loop.hh:131-135
     // pseudo_loop.cc:822-840 (lrint = round-half-even in double)
-    __device__ int compute_int(int i, int j, int k, int l) const {
+    __device__ __forceinline__ int compute_int(int i, int j, int k, int l) const {
         return E_IntLoop(T.prm, T.lx, k - i - 1, j - l - 1, pr(i, j), T.rtype[pr(k, l)], T.S1[i + 1], T.S1[j - 1],
                          T.S1[k - 1], T.S1[l + 1]);
     }
-    __device__ int e_stP(int i, int j) const {
+    __device__ __forceinline__ int e_stP(int i, int j) const {
         if (i + 1 == j - 1) return INF;
         return (int)rint(T.e_stP * (double)compute_int(i, j, i + 1, j - 1));
     }
-    __device__ int e_intP(int i, int ip, int jp, int j) const { return (int)rint(T.e_intP * (double)compute_int(i, j, ip, jp)); }
+    __device__ __forceinline__ int e_intP(int i, int ip, int jp, int j) const { return (int)rint(T.e_intP * (double)compute_int(i, j, ip, jp)); }
 };
 
 __device__ __forceinline__ int lane_id() { return (int)threadIdx.x; }
@@ -93,11 +93,41 @@ __device__ __forceinline__ void wreduce(int &v, int &x) {
     }
 }
 
+// The traceback workgroup has BT_MAXW waves at most.  Every wave walks the same nodes in lockstep
+// (all control flow is uniform: it depends only on scan results, which every lane holds).  A scan
+// of at most REPL_MAX candidates is evaluated by every wave redundantly (lane x: x, x+64, ...) and
+// reduced inside the wave — no barrier; a longer one is spread over the whole workgroup (thread t:
+// t, t+blockDim, ...) and the waves' partial minima meet in LDS.  Either way every lane ends with
+// the lexicographic (value, position) minimum, i.e. the reference's first strict minimum.
+constexpr int BT_MAXW = 16;
+constexpr int BT_WAVES_DEFAULT = 8;
+constexpr int REPL_MAX = 64;
+
+__device__ __forceinline__ void block_reduce(int &v, int &x) {
+    __shared__ int rv[BT_MAXW], rx[BT_MAXW];
+    const int w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);
+    if ((threadIdx.x & 63) == 0) {
+        rv[w] = v;
+        rx[w] = x;
+    }
+    __syncthreads();
+    for (int q = 0; q < nw; ++q) {
+        const int v2 = rv[q], x2 = rx[q];
+        if (v2 < v || (v2 == v && x2 < x)) {
+            v = v2;
+            x = x2;
+        }
+    }
+    __syncthreads();  // rv/rx are reused by the next scan
+}
+
 // first minimum (value, position) over candidate positions [0, count) in loop order
 template <class F>
 __device__ __forceinline__ void scan(int count, F f, int &bv, int &bx) {
     int v = BIG, x = BIG;
-    for (int c = lane_id(); c < count; c += 64) {
+    const bool spread = count > REPL_MAX && blockDim.x > 64;
+    const int c0 = spread ? (int)threadIdx.x : (int)(threadIdx.x & 63), dc = spread ? (int)blockDim.x : 64;
+    for (int c = c0; c < count; c += dc) {
         const int t = f(c);
         if (t < v) {
             v = t;
@@ -105,6 +135,7 @@ __device__ __forceinline__ void scan(int count, F f, int &bv, int &bx) {
         }
     }
     wreduce(v, x);
+    if (spread) block_reduce(v, x);
     bv = v;
     bx = x;
 }
@@ -112,12 +143,13 @@ __device__ __forceinline__ void scan(int count, F f, int &bv, int &bx) {
 template <class F>
 __device__ __forceinline__ int wmin(int count, F f) {
     int v = BIG, x = 0;
-    for (int c = lane_id(); c < count; c += 64) v = imin(v, f(c));
+    const bool spread = count > REPL_MAX && blockDim.x > 64;
+    const int c0 = spread ? (int)threadIdx.x : (int)(threadIdx.x & 63), dc = spread ? (int)blockDim.x : 64;
+    for (int c = c0; c < count; c += dc) v = imin(v, f(c));
     wreduce(v, x);
+    if (spread) block_reduce(v, x);
     return v;
 }
-
-__device__ __forceinline__ bool any_lane(int p) { return __ballot(p != 0) != 0ull; }
 
 // W_final.cc:118-173
 __device__ int E_ext_Stem(const DV &H, int dangles, int vij, int vi1j, int vij1, int vi1j1, int i, int j) {
@@ -163,6 +195,45 @@ __global__ __launch_bounds__(256) void k_w_terms(DevTables T, int *S) {
     S[(size_t)j * T.rs + k] = imin(e2, e3);
 }
 
+// The recurrence with W held in registers: W[x] lives in lane x % 64, slot x / 64 (Q slots cover
+// 0..n), so a step is a register pass plus a wave reduction — no LDS, no barrier — and the S row
+// of step j+1 is loaded while step j reduces, which hides the load latency behind the chain.
+template <int Q>
+__global__ __launch_bounds__(64) void k_compute_W_reg(DevTables T, const int *S, int *Wout) {
+    const int n = T.n, lane = (int)threadIdx.x;
+    int w[Q], s_cur[Q], s_nxt[Q];
+    // S(k, j) for k = lane + 64q + 1, which adds to W[k-1] = w[q]; k runs 1 .. j-TURN-1
+    auto load = [&](int j, int *s) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int k = lane + 64 * q + 1;
+            s[q] = (j <= n && k <= j - TURN - 1) ? S[(size_t)j * T.rs + k] : BIG;
+        }
+    };
+#pragma unroll
+    for (int q = 0; q < Q; ++q) w[q] = 0;
+    load(TURN + 1, s_cur);
+    int wprev = 0;
+    for (int j = TURN + 1; j <= n; ++j) {
+        load(j + 1, s_nxt);
+        int m = INF;
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            if (s_cur[q] != BIG) m = imin(m, w[q] + s_cur[q]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = imin(m, __shfl_xor(m, o));
+        wprev = imin(wprev, m);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (lane + 64 * q == j) w[q] = wprev;
+            s_cur[q] = s_nxt[q];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+        if (lane + 64 * q <= n) Wout[lane + 64 * q] = w[q];
+}
+
 __global__ __launch_bounds__(64) void k_compute_W(DevTables T, const int *S, int *Wout) {
     extern __shared__ int Ws[];
     const int n = T.n;
@@ -188,7 +259,7 @@ struct Bt {
     int8_t *f_type;
     BtOut st;  // uniform
 
-    __device__ void push(int i, int j, int k, int l, int type) {
+    __device__ __forceinline__ void push(int i, int j, int k, int l, int type) {
         if (sp >= cap) {
             st.status = BT_OVERFLOW;
             return;
@@ -196,10 +267,10 @@ struct Bt {
         if (lane_id() == 0) stk[sp] = Interval{i, j, k, l, type};
         ++sp;
     }
-    __device__ void push2(int i, int j, int type) { push(i, j, 0, 0, type); }
+    __device__ __forceinline__ void push2(int i, int j, int type) { push(i, j, 0, 0, type); }
     // pseudo_loop::insert_node(i, j, k, l, type): fields i, j(=l of the region), k(=j), l(=k)
-    __device__ void push4(int i, int j, int k, int l, int type) { push(i, j, k, l, type); }
-    __device__ void pairup(int p, int q, int type) {
+    __device__ __forceinline__ void push4(int i, int j, int k, int l, int type) { push(i, j, k, l, type); }
+    __device__ __forceinline__ void pairup(int p, int q, int type) {
         if (lane_id() == 0) {
             f_pair[p] = q;
             f_pair[q] = p;
@@ -207,19 +278,19 @@ struct Bt {
             f_type[q] = (int8_t)type;
         }
     }
-    __device__ void die(int prefix, int node) {
+    __device__ __forceinline__ void die(int prefix, int node) {
         st.status = BT_DIE;
         st.prefix = prefix;
         st.node = node;
     }
-    __device__ bool in_range4(int i, int j, int k, int l) const {
+    __device__ __forceinline__ bool in_range4(int i, int j, int k, int l) const {
         const int n = H.n;
         return !(i <= 0 || j <= 0 || k <= 0 || l <= 0 || i > n || j > n || k > n || l > n);
     }
-    __device__ static bool order4(int i, int j, int k, int l) { return i <= j && j < k - 1 && k <= l; }
+    __device__ __forceinline__ static bool order4(int i, int j, int k, int l) { return i <= j && j < k - 1 && k <= l; }
 
     // get_P?iloop, value only, with can_pair (pseudo_loop.cc:682-808)
-    __device__ int get_PLiloop(int i, int j, int k, int l) const {
+    __device__ __forceinline__ int get_PLiloop(int i, int j, int k, int l) const {
         if (!order4(i, j, k, l) || !H.can_pair(i, j)) return INF;
         int mn = INF;
         if (i + TURN + 2 < j) mn = H.g4(PL, i + 1, j - 1, k, l) + H.e_stP(i, j);
@@ -230,7 +301,7 @@ struct Bt {
             return H.e_intP(i, d, dp, j) + H.g4(PL, d, dp, k, l);
         }));
     }
-    __device__ int get_PRiloop(int i, int j, int k, int l) const {
+    __device__ __forceinline__ int get_PRiloop(int i, int j, int k, int l) const {
         if (!order4(i, j, k, l) || !H.can_pair(k, l)) return INF;
         int mn = INF;
         if (k + TURN + 2 < l) mn = H.g4(PR, i, j, k + 1, l - 1) + H.e_stP(k, l);
@@ -241,7 +312,7 @@ struct Bt {
             return H.e_intP(k, d, dp, l) + H.g4(PR, i, j, d, dp);
         }));
     }
-    __device__ int get_PMiloop(int i, int j, int k, int l) const {
+    __device__ __forceinline__ int get_PMiloop(int i, int j, int k, int l) const {
         if (!order4(i, j, k, l) || !H.can_pair(j, k)) return INF;
         int mn = INF;
         if (i < j && k < l) mn = H.g4(PM, i, j - 1, k + 1, l) + H.e_stP(j - 1, k + 1);
@@ -253,7 +324,7 @@ struct Bt {
             return H.e_intP(d, j, k, dp) + H.g4(PM, i, d, dp, l);
         }));
     }
-    __device__ int get_POiloop(int i, int j, int k, int l) const {
+    __device__ __forceinline__ int get_POiloop(int i, int j, int k, int l) const {
         if (!order4(i, j, k, l) || !H.can_pair(i, l)) return INF;
         int mn = INF;
         if (i < j && k < l) mn = H.g4(PO, i + 1, j, k, l - 1) + H.e_stP(i, l);
@@ -265,7 +336,7 @@ struct Bt {
             return H.e_intP(i, d, dp, l) + H.g4(PO, d, j, dp, k);
         }));
     }
-    __device__ int get_PXmloop(int m10, int m01, int i2, int j2, int k2, int l2, int i, int j, int k, int l) const {
+    __device__ __forceinline__ int get_PXmloop(int m10, int m01, int i2, int j2, int k2, int l2, int i, int j, int k, int l) const {
         if (!order4(i, j, k, l)) return INF;
         const int b1 = H.g4(m10, i2, j2, k2, l2) + H.T.pen.ap + H.T.pen.bp;
         const int b2 = H.g4(m01, i2, j2, k2, l2) + H.T.pen.ap + H.T.pen.bp;
@@ -273,16 +344,16 @@ struct Bt {
     }
 
     // one node (W_final::backtrack W_final.cc:175-719, pseudo_loop::backtrack pseudo_loop.cc:861-2820)
-    __device__ void node(const Interval &cur);
-    __device__ void bt_loop(const Interval &cur);
-    __device__ void bt_free(const Interval &cur);
-    __device__ void bt_wm(const Interval &cur);
-    __device__ void bt_wmv(const Interval &cur);
-    __device__ void bt_wmp(const Interval &cur);
-    __device__ void pl(const Interval &cur);
+    __device__ __forceinline__ void node(const Interval &cur);
+    __device__ __forceinline__ void bt_loop(const Interval &cur);
+    __device__ __forceinline__ void bt_free(const Interval &cur);
+    __device__ __forceinline__ void bt_wm(const Interval &cur);
+    __device__ __forceinline__ void bt_wmv(const Interval &cur);
+    __device__ __forceinline__ void bt_wmp(const Interval &cur);
+    __device__ __forceinline__ void pl(const Interval &cur);
 };
 
-__device__ void Bt::node(const Interval &cur) {
+__device__ __forceinline__ void Bt::node(const Interval &cur) {
     switch (cur.type) {
         case LOOP: bt_loop(cur); break;
         case FREE: bt_free(cur); break;
@@ -302,7 +373,7 @@ __device__ void Bt::node(const Interval &cur) {
     }
 }
 
-__device__ void Bt::bt_loop(const Interval &cur) {
+__device__ __forceinline__ void Bt::bt_loop(const Interval &cur) {
     const int i = cur.i, j = cur.j;
     if (i >= j) return;
     const int type = H.Vtype(i, j);
@@ -381,7 +452,7 @@ __device__ void Bt::bt_loop(const Interval &cur) {
     }
 }
 
-__device__ void Bt::bt_free(const Interval &cur) {
+__device__ __forceinline__ void Bt::bt_free(const Interval &cur) {
     const int j = cur.j, n = H.n;
     if (j == 1) return;
     const short *S = H.T.S;
@@ -450,7 +521,7 @@ __device__ void Bt::bt_free(const Interval &cur) {
     }
 }
 
-__device__ void Bt::bt_wm(const Interval &cur) {
+__device__ __forceinline__ void Bt::bt_wm(const Interval &cur) {
     const int i = cur.i, j = cur.j;
     const int MLb = H.T.prm->MLbase;
     int mn = H.WM(i, j - 1) + MLb;
@@ -479,7 +550,7 @@ __device__ void Bt::bt_wm(const Interval &cur) {
     }
 }
 
-__device__ void Bt::bt_wmv(const Interval &cur) {
+__device__ __forceinline__ void Bt::bt_wmv(const Interval &cur) {
     const int i = cur.i, j = cur.j, n = H.n;
     const short *S = H.T.S;
     const ccj_energy_params *P = H.T.prm;
@@ -511,14 +582,14 @@ __device__ void Bt::bt_wmv(const Interval &cur) {
     }
 }
 
-__device__ void Bt::bt_wmp(const Interval &cur) {
+__device__ __forceinline__ void Bt::bt_wmp(const Interval &cur) {
     const int i = cur.i, j = cur.j;
     const int mn = H.Pg(i, j) + H.T.pen.PSM + H.T.pen.b;
     const int tmp = H.WMp(i, j - 1) + H.T.prm->MLbase;
     if (tmp < mn) push2(i, j - 1, M_WMp);  // case 1 is commented out in the reference (A-B2)
 }
 
-__device__ void Bt::pl(const Interval &cur) {
+__device__ __forceinline__ void Bt::pl(const Interval &cur) {
     const Penalties &pe = H.T.pen;
     const int PB = pe.PB, bp = pe.bp, cp = pe.cp, ap = pe.ap, n = H.n;
     const int i = cur.i, l = cur.j, j = cur.k, k = cur.l;
@@ -1060,15 +1131,16 @@ __device__ void Bt::pl(const Interval &cur) {
     }
 }
 
-// one wave; LDS: the node stack (cap entries)
-__global__ __launch_bounds__(64) void k_backtrack(DevTables T, const int *W, int *f_pair, int8_t *f_type, BtOut *out, int cap) {
+// one workgroup of 1..BT_MAXW waves; LDS: the node stack (cap entries)
+__global__ __launch_bounds__(64 * BT_MAXW) void k_backtrack(DevTables T, const int *W, int *f_pair, int8_t *f_type, BtOut *out, int cap) {
     extern __shared__ Interval stk[];
     const int n = T.n;
     DV H{T, n, T.rs, W, 0};
-    for (int x = lane_id(); x <= n; x += 64) {
+    for (int x = (int)threadIdx.x; x <= n; x += (int)blockDim.x) {
         f_pair[x] = -1;
         f_type[x] = (int8_t)T_NONE;
     }
+    __syncthreads();  // the pair list is cleared before lane 0 starts writing pairs
     Bt B{H, stk, cap, 0, f_pair, f_type, BtOut{}};
     B.push2(1, n, FREE);  // W_final.cc:84-99
     __syncthreads();
@@ -1078,8 +1150,8 @@ __global__ __launch_bounds__(64) void k_backtrack(DevTables T, const int *W, int
         --B.sp;
         ++B.st.steps;
         B.node(cur);
-        if (any_lane(H.bad)) B.st.status = BT_ASSERT;
-        __syncthreads();
+        // a get_uc assert on any lane of any wave; the barrier also publishes lane 0's pushes
+        if (__syncthreads_or(H.bad)) B.st.status = BT_ASSERT;
     }
     if (lane_id() == 0) *out = B.st;
 }
@@ -1095,14 +1167,30 @@ extern "C" int ccjk_compute_W(const void *Tv, int *W, int *S, void *stream) {
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }
-    hipLaunchKernelGGL(k_compute_W, dim3(1), dim3(64), (n + 1) * sizeof(int), (hipStream_t)stream, *T, S, W);
+    const hipStream_t s = (hipStream_t)stream;
+    switch ((n + 64) / 64) {  // slots for W[0..n]
+        case 1: hipLaunchKernelGGL(k_compute_W_reg<1>, dim3(1), dim3(64), 0, s, *T, S, W); break;
+        case 2: hipLaunchKernelGGL(k_compute_W_reg<2>, dim3(1), dim3(64), 0, s, *T, S, W); break;
+        case 3: hipLaunchKernelGGL(k_compute_W_reg<3>, dim3(1), dim3(64), 0, s, *T, S, W); break;
+        case 4: hipLaunchKernelGGL(k_compute_W_reg<4>, dim3(1), dim3(64), 0, s, *T, S, W); break;
+        case 5: hipLaunchKernelGGL(k_compute_W_reg<5>, dim3(1), dim3(64), 0, s, *T, S, W); break;
+        case 6: hipLaunchKernelGGL(k_compute_W_reg<6>, dim3(1), dim3(64), 0, s, *T, S, W); break;
+        case 7: hipLaunchKernelGGL(k_compute_W_reg<7>, dim3(1), dim3(64), 0, s, *T, S, W); break;
+        case 8: hipLaunchKernelGGL(k_compute_W_reg<8>, dim3(1), dim3(64), 0, s, *T, S, W); break;
+        default: hipLaunchKernelGGL(k_compute_W, dim3(1), dim3(64), (n + 1) * sizeof(int), s, *T, S, W);
+    }
     return (int)hipGetLastError();
 }
 
 extern "C" int ccjk_backtrack(const void *Tv, const int *W, int *f_pair, int8_t *f_type, BtOut *out, int stack_cap,
                               void *stream) {
     const DevTables *T = (const DevTables *)Tv;
-    hipLaunchKernelGGL(k_backtrack, dim3(1), dim3(64), (size_t)stack_cap * sizeof(Interval), (hipStream_t)stream, *T, W,
-                       f_pair, f_type, out, stack_cap);
+    static const int waves = [] {
+        const char *e = getenv("CCJ_BT_WAVES");
+        const int w = e ? atoi(e) : BT_WAVES_DEFAULT;
+        return w < 1 ? 1 : (w > BT_MAXW ? BT_MAXW : w);
+    }();
+    hipLaunchKernelGGL(k_backtrack, dim3(1), dim3(64 * waves), (size_t)stack_cap * sizeof(Interval), (hipStream_t)stream,
+                       *T, W, f_pair, f_type, out, stack_cap);
     return (int)hipGetLastError();
 }
