@@ -18,7 +18,8 @@ from typing import Optional
 
 __all__ = [
     "W_final", "ccj", "load_params", "load_par", "ParFileError", "param_path", "CCJError", "BacktrackExit", "lib", "MAT4", "MAT2",
-    "num_cells", "comm_unique_id", "shard_blocks", "level_layout", "LocalGroup",
+    "num_cells", "comm_unique_id", "shard_blocks", "level_layout", "LocalGroup", "W_final_pf", "PF_MAT4", "PF_MAT2",
+    "SampleExit", "pf_exp_hashes", "load_pfraw",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -34,6 +35,12 @@ MAT4 = ["PK", "PL", "PR", "PM", "PO", "PfromL", "PfromR", "PfromM", "PfromMprime
         "PMmloop00", "PMmloop01", "PMmloop10", "POmloop00", "POmloop01", "POmloop10"]
 MAT2 = ["P", "WBP", "WPP", "V", "Vtype", "WM", "WMv", "WMp"]
 HASH_NAMES = MAT4 + MAT2 + ["W"]
+# ccj_pf.h enums (partition function)
+PF_MAT4 = ["PK", "PL", "PR", "PM", "PO", "PfromL", "PfromR", "PfromM", "PfromO",
+           "PLmloop00", "PLmloop01", "PLmloop10", "PRmloop00", "PRmloop01", "PRmloop10",
+           "PMmloop00", "PMmloop01", "PMmloop10", "POmloop00", "POmloop01", "POmloop10"]
+PF_MAT2 = ["V", "VM", "WM", "WMv", "WMp", "WBP", "WPP", "P"]
+CCJ_E_PF_SAMPLE = 8  # include/ccj_pf.h
 
 CCJ_OK, CCJ_E_ARG, CCJ_E_OOM, CCJ_E_HIP, CCJ_E_PARAMS, CCJ_E_BACKTRACK, CCJ_E_STATE, CCJ_E_INTER_EXIT = range(8)
 CCJ_E_PARFILE = 8  # include/ccj_parfile.h
@@ -146,6 +153,34 @@ def lib() -> ctypes.CDLL:
     L.ccj_params_load_par.restype = ip
     L.ccj_params_load_par_string.argtypes = [cp, cp, cp, cp, ip]
     L.ccj_params_load_par_string.restype = ip
+    # partition function (include/ccj_pf.h)
+    u64p, dp = ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)
+    L.ccj_pf_create.argtypes = [ctypes.POINTER(_Problem), cp, ip, ctypes.POINTER(vp)]
+    L.ccj_pf_create.restype = ip
+    L.ccj_pf_destroy.argtypes = [vp]
+    L.ccj_pf_destroy.restype = None
+    L.ccj_pf_fill.argtypes = [vp, dp]
+    L.ccj_pf_fill.restype = ip
+    L.ccj_pf_W.argtypes = [vp, dp]
+    L.ccj_pf_W.restype = ip
+    L.ccj_pf_get2.argtypes = [vp, ip, dp]
+    L.ccj_pf_get2.restype = ip
+    L.ccj_pf_hashes.argtypes = [vp, u64p, u64p]
+    L.ccj_pf_hashes.restype = ip
+    L.ccj_pf_exp_hashes.argtypes = [vp, u64p, ip]
+    L.ccj_pf_exp_hashes.restype = ip
+    L.ccj_pf_exp_hashes_params.argtypes = [cp, cp, vp, u64p, ip]
+    L.ccj_pf_exp_hashes_params.restype = ip
+    L.ccj_pf_exp_names.argtypes = []
+    L.ccj_pf_exp_names.restype = cp
+    L.ccj_pf_srand.argtypes = [vp, ctypes.c_uint]
+    L.ccj_pf_srand.restype = ip
+    L.ccj_pf_sample.argtypes = [vp, ip, cp, ctypes.POINTER(ip)]
+    L.ccj_pf_sample.restype = ip
+    L.ccj_pf_last_message.argtypes = [vp]
+    L.ccj_pf_last_message.restype = cp
+    L.ccj_pf_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.ccj_pf_timing.restype = ip
     _lib = L
     return L
 
@@ -457,3 +492,147 @@ def ccj(seq: str, dangle: int = 2, params: str | bytes = "DirksPierce09", noGU: 
         return wf.structure, energy
     finally:
         wf.close()
+
+
+def load_pfraw(name_or_path) -> Optional[bytes]:
+    """Raw (unclamped) dangle / mismatch tables of a bundled set (ccj_amd/params/<set>.pfraw,
+    include/ccj_pf.h ccj_pf_raw), or None (the engine then takes the pair-type-0 rows as INF)."""
+    if not isinstance(name_or_path, str):
+        return None
+    if os.path.isfile(name_or_path) and not name_or_path.endswith(".ccjp"):
+        return None  # a .par file read natively: no raw tables (type-0 rows taken as INF)
+    try:
+        p = param_path(name_or_path)
+    except Exception:
+        return None
+    raw = p[:-5] + ".pfraw" if p.endswith(".ccjp") else None
+    if raw and os.path.exists(raw):
+        return _read_blob(raw)
+    return None
+
+
+def pf_exp_hashes(params: str | bytes = "DirksPierce09") -> dict:
+    """FNV-1a of the partition function's Boltzmann tables for a parameter set (host only)."""
+    blob = params if isinstance(params, (bytes, bytearray)) else load_params(params)
+    raw = load_pfraw(params)
+    names = lib().ccj_pf_exp_names().decode().split()
+    out = (ctypes.c_uint64 * len(names))()
+    got = lib().ccj_pf_exp_hashes_params(bytes(blob), raw, None, out, len(names))
+    if got != len(names):
+        raise CCJError(CCJ_E_ARG, "ccj_pf_exp_hashes_params")
+    return {k: "%016x" % v for k, v in zip(names, out)}
+
+
+class SampleExit(CCJError):
+    """A Sample_* failure path of the reference (it prints ``stdout`` and calls exit(0))."""
+
+    def __init__(self, msg: str, structures: list):
+        super().__init__(CCJ_E_PF_SAMPLE, msg)
+        self.stdout = msg
+        self.structures = structures
+
+
+class W_final_pf:
+    """Mirror of the reference class W_final_pf (src/part_func.hh:28-194, part_func.cc).
+
+    ``W_final_pf(seq, MFE_structure, MFE_energy, dangle, num_samples, PSplot).ccj_pf()`` runs the
+    CCJ partition function on the GPU (include/ccj_pf.h) and returns the ensemble free energy in
+    kcal/mol, bit-identical to the reference's part_func.cc evaluated without floating-point
+    contraction.  MFE_structure, MFE_energy and PSplot are accepted and stored like the reference
+    (which ignores them: pf_scale is forced to 1).  ``srand(seed)`` + ``sample(k)`` is the
+    reference's stochastic traceback Sample_W(1, n) (stoch_backtrack.cc), drawing rand()/RAND_MAX
+    like vrna_urn() in the reference build.
+    """
+
+    def __init__(self, seq: str, MFE_structure: str = "", MFE_energy: float = 0.0, dangle: int = 2,
+                 num_samples: int = 0, PSplot: bool = False, params: str | bytes = "DirksPierce09",
+                 noGU: bool = False, device: int = 0):
+        self.seq = seq
+        self.n = len(seq)
+        self.MFE_structure = MFE_structure
+        self.MFE_energy = MFE_energy
+        self.num_samples = num_samples
+        self.PSplot = PSplot
+        self.structure = "." * self.n
+        self.structures: dict = {}
+        self._blob = params if isinstance(params, (bytes, bytearray)) else load_params(params)
+        self._blob_buf = ctypes.create_string_buffer(bytes(self._blob), len(self._blob))
+        self._seq_buf = ctypes.create_string_buffer(seq.encode())
+        L = lib()
+        prob = _Problem(ctypes.cast(self._seq_buf, ctypes.c_char_p), dangle, 1 if noGU else 0,
+                        ctypes.cast(self._blob_buf, ctypes.c_void_p), None)
+        h = ctypes.c_void_p()
+        self._raw = load_pfraw(params)
+        rc = L.ccj_pf_create(ctypes.byref(prob), self._raw, device, ctypes.byref(h))
+        if rc != CCJ_OK:
+            raise CCJError(rc, "ccj_pf_create failed (see stderr)")
+        self._h = h
+        self.energy: Optional[float] = None
+
+    def _check(self, rc: int):
+        if rc != CCJ_OK:
+            raise CCJError(rc, lib().ccj_pf_last_message(self._h).decode())
+
+    def ccj_pf(self) -> float:
+        e = ctypes.c_double()
+        self._check(lib().ccj_pf_fill(self._h, ctypes.byref(e)))
+        self.energy = e.value
+        return e.value
+
+    def W(self) -> list:
+        out = (ctypes.c_double * (self.n + 1))()
+        self._check(lib().ccj_pf_W(self._h, out))
+        return list(out)
+
+    def get2(self, name: str) -> list:
+        """One 2-D matrix in canonical order (i = 1..n, j = i..n)."""
+        out = (ctypes.c_double * (self.n * (self.n + 1) // 2))()
+        self._check(lib().ccj_pf_get2(self._h, PF_MAT2.index(name), out))
+        return list(out)
+
+    def hashes(self) -> dict:
+        h4 = (ctypes.c_uint64 * len(PF_MAT4))()
+        h2 = (ctypes.c_uint64 * len(PF_MAT2))()
+        self._check(lib().ccj_pf_hashes(self._h, h4, h2))
+        d = {k: "%016x" % v for k, v in zip(PF_MAT4, h4)}
+        d.update({k: "%016x" % v for k, v in zip(PF_MAT2, h2)})
+        return d
+
+    def exp_hashes(self) -> dict:
+        names = lib().ccj_pf_exp_names().decode().split()
+        out = (ctypes.c_uint64 * len(names))()
+        got = lib().ccj_pf_exp_hashes(self._h, out, len(names))
+        if got != len(names):
+            raise CCJError(CCJ_E_ARG, "ccj_pf_exp_hashes")
+        return {k: "%016x" % v for k, v in zip(names, out)}
+
+    def srand(self, seed: int) -> None:
+        """srand(seed) for this context's vrna_urn() generator (rand()/RAND_MAX, like the reference build)."""
+        self._check(lib().ccj_pf_srand(self._h, seed))
+
+    def sample(self, count: int) -> list:
+        """count x Sample_W(1, n) (stoch_backtrack.cc), continuing this context's rand() stream."""
+        buf = ctypes.create_string_buffer(max(count, 1) * (self.n + 1))
+        done = ctypes.c_int()
+        rc = lib().ccj_pf_sample(self._h, count, buf, ctypes.byref(done))
+        got = [buf.raw[s * (self.n + 1): s * (self.n + 1) + self.n].decode() for s in range(done.value)]
+        if rc == CCJ_E_PF_SAMPLE:
+            raise SampleExit(lib().ccj_pf_last_message(self._h).decode(), got)
+        self._check(rc)
+        return got
+
+    def fill_ms(self) -> float:
+        t = ctypes.c_float()
+        self._check(lib().ccj_pf_timing(self._h, ctypes.byref(t)))
+        return t.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ccj_pf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

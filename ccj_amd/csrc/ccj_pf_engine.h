@@ -1,0 +1,61 @@
+// ccj_pf_engine.h — device-side layout of the partition-function fill (ccj_pf.hip, ccj_pf.cc).
+//
+// 4-D matrices: the MFE engine's level-major layout with int32 cells and the 21
+// matrices of W_final_pf (part_func.hh:86-113):
+//   elem(x,t,a,h,i) = lb_t + x*C_t + a*M_t + h*m_t - h(h-1)/2 + (i-1),  m_t = n-t-2,
+//   M_t = m_t(m_t+1)/2, C_t = (t+1) M_t.
+// 2-D matrices: doubles, span-major [w][p] with row stride rs = n+2.
+// Interior-loop weights ie[u1][u2][w][p] = get_e_intP of the loop closed by (p, p+w) around
+// (p+1+u1, p+w-1-u2) (part_func.cc:886-891), u1, u2 < PF_IEW.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/ccj_pf.h"
+#include "ccj_pf_energy.h"
+
+namespace ccj {
+
+enum {
+    PF_PK = CCJ_PF_PK, PF_PL = CCJ_PF_PL, PF_PR = CCJ_PF_PR, PF_PM = CCJ_PF_PM, PF_PO = CCJ_PF_PO,
+    PF_PfromL = CCJ_PF_PfromL, PF_PfromR = CCJ_PF_PfromR, PF_PfromM = CCJ_PF_PfromM, PF_PfromO = CCJ_PF_PfromO,
+    PF_PLmloop00 = CCJ_PF_PLmloop00, PF_PLmloop01 = CCJ_PF_PLmloop01, PF_PLmloop10 = CCJ_PF_PLmloop10,
+    PF_PRmloop00 = CCJ_PF_PRmloop00, PF_PRmloop01 = CCJ_PF_PRmloop01, PF_PRmloop10 = CCJ_PF_PRmloop10,
+    PF_PMmloop00 = CCJ_PF_PMmloop00, PF_PMmloop01 = CCJ_PF_PMmloop01, PF_PMmloop10 = CCJ_PF_PMmloop10,
+    PF_POmloop00 = CCJ_PF_POmloop00, PF_POmloop01 = CCJ_PF_POmloop01, PF_POmloop10 = CCJ_PF_POmloop10,
+    PF_NMAT4 = CCJ_PF_NMAT4
+};
+
+constexpr int PF_IEW = MAXLOOP - 1;  // interior-loop window per side: u <= 28
+
+struct PfLvl {
+    long long lb;  // element offset of level t
+    long long C;   // cells of one matrix at level t
+    int M;         // cells of one a-block
+    int pad;
+};
+
+struct PfDev {
+    int n, rs, dangles, ap_int;  // ap_int: the int ap_penalty (get_PLmloop multiplies an int by it)
+    const PfExp *E;
+    const short *S, *S1;
+    const int8_t *pt;     // [w][p] pair[S[p]][S[p+w]]
+    const int8_t *pair;   // 8x8
+    const int8_t *rtype;  // 8
+    const double *hp;     // [w][p] HairpinE
+    const double *est;    // [w][p] get_e_stP
+    const double *ie;     // [u1][u2][w][p] get_e_intP
+    const double *mlb, *cpp, *pup;  // expMLbase[], expcp_pen[], expPUP_pen[] (n+2)
+    double *V, *VM, *WM, *WMv, *WMp, *WBP, *WPP, *P;  // [w][p]
+    long long *Pacc;      // [w][p] exact integer P sums
+    int *d4;
+    const PfLvl *ld;
+};
+
+}  // namespace ccj
+
+extern "C" {
+int ccjk_pf_pterm(const ccj::PfDev *D, int s, void *stream);
+int ccjk_pf_diag(const ccj::PfDev *D, int s, void *stream);
+int ccjk_pf_level(const ccj::PfDev *D, const ccj::PfLvl *Lh, int t, void *stream);
+int ccjk_pf_canon(const ccj::PfDev *D, int x, const long long *rowoff, int nrows, int *out, void *stream);
+}

@@ -1,0 +1,69 @@
+"""Partition function on the GPU against the reference's own W_final_pf.
+
+tests/golden/pf_golden.json holds, per case, what src/part_func.cc (-ffp-contract=off) produced:
+the ensemble energy, the IEEE bits of W[0..n], FNV-1a hashes of the 8 2-D matrices (IEEE bits)
+and of the 21 4-D matrices (their int32 values, canonical order), and for some cases 5 stochastic
+samples after srand(seed) — or the reference's "backtracking failed" line where it exits.
+The bar is bit-identity: the fill evaluates every sum in the reference's order without
+contraction.
+"""
+import json
+import os
+
+import pytest
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "pf_golden.json")
+
+with open(GOLD) as _f:
+    CASES = json.load(_f)["cases"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_pf_matches_reference(case):
+    import struct
+
+    import ccj_amd
+    pf = ccj_amd.W_final_pf(case["seq"], dangle=case["dangles"], params=case["params"])
+    try:
+        e = pf.ccj_pf()
+        assert repr(e) == repr(float(case["energy"])) or (e != e and case["energy"] == "nan")
+        wbits = ["%016x" % struct.unpack("<Q", struct.pack("<d", w))[0] for w in pf.W()]
+        assert wbits == case["wbits"]
+        h = pf.hashes()
+        bad = {k: (h[k], v) for k, v in {**case["h2"], **case["h4"]}.items() if h[k] != v}
+        assert not bad
+        assert pf.exp_hashes() == case["exp"]
+        if "srand" in case:
+            pf.srand(case["srand"])
+            try:
+                got = pf.sample(5)
+                assert "sample_exit" not in case
+                assert got == case["samples"]
+            except ccj_amd.SampleExit as ex:
+                assert ex.structures == case["samples"]
+                assert ex.stdout == case["sample_exit"]
+    finally:
+        pf.close()
+
+
+@pytest.mark.gpu
+def test_pf_refill_is_identical():
+    import ccj_amd
+    c = next(c for c in CASES if c["name"] == "big40_default")
+    pf = ccj_amd.W_final_pf(c["seq"], params=c["params"])
+    try:
+        e1, h1 = pf.ccj_pf(), pf.hashes()
+        e2, h2 = pf.ccj_pf(), pf.hashes()
+        assert repr(e1) == repr(e2) and h1 == h2
+    finally:
+        pf.close()
+
+
+@pytest.mark.gpu
+def test_pf_rejects_bad_input():
+    import ccj_amd
+    with pytest.raises(ccj_amd.CCJError):
+        ccj_amd.W_final_pf("ACGX")
+    with pytest.raises(ccj_amd.CCJError):
+        ccj_amd.W_final_pf("A" * 300)
