@@ -581,13 +581,15 @@ struct Sampler {
         qbt1 += V_temp;
         if (qbt1 >= r) return;
         const int max_k = std::min(j - TURN - 2, i + MAXLOOP + 1);
-        const int tc = c.ptype(i, j);
+        // stoch_backtrack.cc:112,119 read `pair` of ViennaRNA/pair_mat.h, a static array every
+        // translation unit owns; only part_func.cc's copy is filled (make_pair_matrix in the
+        // constructor), so here every pair type is 0 and rtype[0] is 0.
+        const int tc = 0, t2 = 0;
         for (k = i + 1; k <= max_k; k++) {
             const int min_l = std::max(k + TURN + 1 + MAXLOOP + 2, k + j - i) - MAXLOOP - 2;
             for (l = j - 1; l >= min_l; --l) {
                 const int u1 = k - i - 1, u2 = j - l - 1;
-                V_temp = V(k, l) * exp_E_IntLoop_pf(c.E, u1, u2, tc, c.rtype[c.ptype(k, l)], c.S1[i + 1], c.S1[j - 1],
-                                                    c.S1[k - 1], c.S1[l + 1]);
+                V_temp = V(k, l) * exp_E_IntLoop_pf(c.E, u1, u2, tc, t2, c.S1[i + 1], c.S1[j - 1], c.S1[k - 1], c.S1[l + 1]);
                 V_temp *= 1.0;
                 qbt1 += V_temp;
                 if (qbt1 >= r) break;
