@@ -165,6 +165,8 @@ def lib() -> ctypes.CDLL:
     L.ccj_pf_W.restype = ip
     L.ccj_pf_get2.argtypes = [vp, ip, dp]
     L.ccj_pf_get2.restype = ip
+    L.ccj_pf_get4.argtypes = [vp, ip, ip, ip, ip, ip, ctypes.POINTER(ip)]
+    L.ccj_pf_get4.restype = ip
     L.ccj_pf_hashes.argtypes = [vp, u64p, u64p]
     L.ccj_pf_hashes.restype = ip
     L.ccj_pf_exp_hashes.argtypes = [vp, u64p, ip]
@@ -589,6 +591,12 @@ class W_final_pf:
         out = (ctypes.c_double * (self.n * (self.n + 1) // 2))()
         self._check(lib().ccj_pf_get2(self._h, PF_MAT2.index(name), out))
         return list(out)
+
+    def get4(self, name: str, i: int, j: int, k: int, l: int) -> int:
+        """Matrix4DPF::get: the stored int, 0 outside i <= j < k-1, k <= l."""
+        v = ctypes.c_int()
+        self._check(lib().ccj_pf_get4(self._h, PF_MAT4.index(name), i, j, k, l, ctypes.byref(v)))
+        return v.value
 
     def hashes(self) -> dict:
         h4 = (ctypes.c_uint64 * len(PF_MAT4))()

@@ -797,6 +797,22 @@ int ccj_pf_get2(ccj_pf_ctx *c, int which, double *out) {
     return CCJ_OK;
 }
 
+int ccj_pf_get4(ccj_pf_ctx *c, int x, int i, int j, int k, int l, int *out) {
+    if (!c || !out || x < 0 || x >= CCJ_PF_NMAT4) return CCJ_E_ARG;
+    if (!c->filled) return CCJ_E_STATE;
+    if (!(i <= j && j < k - 1 && k <= l)) {  // Matrix4DPF::get (matrices.hh:258-263)
+        *out = 0;
+        return CCJ_OK;
+    }
+    if (i <= 0 || l > c->n) return CCJ_E_ARG;  // the reference's get_uc assert
+    const int a = j - i, b = l - k, t = a + b, h = k - j - 2, m = c->n - t - 2;
+    const PfLvl &L = c->lv[t];
+    const long long off = L.lb + (long long)x * L.C + (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) + i - 1;
+    PFCHK(c, hipSetDevice(c->device));
+    PFCHK(c, hipMemcpy(out, c->d_d4 + off, sizeof(int), hipMemcpyDeviceToHost));
+    return CCJ_OK;
+}
+
 int ccj_pf_hashes(ccj_pf_ctx *c, uint64_t *h4, uint64_t *h2) {
     if (!c) return CCJ_E_ARG;
     if (!c->filled) return CCJ_E_STATE;

@@ -341,7 +341,11 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         double c = 0;
         if (G.pt(j, k) > 0) {
             double r = 0;
-            r += G.g4(PF_PM, i, j - 1, k + 1, l) * D.est[(h + 4) * rs + (j - 1)];
+            // get_e_stP(j-1, k+1): for j == 1 or k == n the reference indexes pair[][] with S[0] (= n)
+            // or S[n+1]; the factor multiplies PM(i, j-1, k+1, l), which is then outside the matrix
+            // (0), so any finite value gives 0 — use 0 instead of reading past the table
+            const double est_m = (j > 1 && k < n) ? D.est[(h + 4) * rs + (j - 1)] : 0.0;
+            r += G.g4(PF_PM, i, j - 1, k + 1, l) * est_m;
             const int dmin = imax(i, j - MAXLOOP), dpmax = imin(l, k + MAXLOOP);
             for (int d = j - 1; d > dmin; --d) {
                 const int u1 = j - d - 1;

@@ -84,6 +84,9 @@ int ccj_pf_W(ccj_pf_ctx *ctx, double *W);
 /* One 2-D matrix, canonical order i = 1..n, j = i..n (n(n+1)/2 doubles). */
 int ccj_pf_get2(ccj_pf_ctx *ctx, int which, double *out);
 
+/* One 4-D value with Matrix4DPF::get semantics (matrices.hh:258-263): 0 outside i <= j < k-1, k <= l. */
+int ccj_pf_get4(ccj_pf_ctx *ctx, int which, int i, int j, int k, int l, int *out);
+
 /* FNV-1a of every matrix in canonical order: h4[CCJ_PF_NMAT4] over the int32 values of the 4-D
  * matrices (i <= j < k-1, k <= l), h2[CCJ_PF_NMAT2] over the IEEE bits of the 2-D matrices. */
 int ccj_pf_hashes(ccj_pf_ctx *ctx, uint64_t *h4, uint64_t *h2);

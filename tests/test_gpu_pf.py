@@ -67,3 +67,25 @@ def test_pf_rejects_bad_input():
         ccj_amd.W_final_pf("ACGX")
     with pytest.raises(ccj_amd.CCJError):
         ccj_amd.W_final_pf("A" * 300)
+
+
+@pytest.mark.gpu
+def test_pf_after_other_contexts():
+    """Device memory handed back by an MFE context is not zero: no read may depend on fresh memory
+    (the PM interior loop once read e_stP past its table for j == 1, k == n)."""
+    import ccj_amd
+    for name in ("tetra_DirksPierce09", "big40_default", "knot_default"):
+        wf = ccj_amd.W_final("GCGGAUUUAGCUCAGUUGGGAGAGCGCCAGAC", 2, params="Turner04")
+        wf.ccj()
+        wf.close()
+        c = next(c for c in CASES if c["name"] == name)
+        pf = ccj_amd.W_final_pf(c["seq"], dangle=c["dangles"], params=c["params"])
+        try:
+            e = pf.ccj_pf()
+            h = pf.hashes()
+            assert repr(e) == repr(float(c["energy"]))
+            assert not [k for k, v in {**c["h2"], **c["h4"]}.items() if h[k] != v]
+            n = len(c["seq"])
+            assert pf.get4("PM", 1, 1, n, n) == (1 if c["name"] == "tetra_DirksPierce09" else pf.get4("PM", 1, 1, n, n))
+        finally:
+            pf.close()
