@@ -6,10 +6,11 @@
 // W, the pair list f[] and an exit record come back, and fill_structure (W_final.cc:764-819)
 // stays on the host.
 //
-// One wave does the traceback.  Nodes are popped from an LDS stack in the reference's LIFO
-// order; every case is the reference's argmin with its strict `<` (first minimum in loop order)
-// computed as a wave-parallel scan: lane x evaluates candidates x, x+64, ... of the case's loop
-// order and a lexicographic (value, position) reduction picks the first minimum.  Loops that the
+// One workgroup (CCJ_BT_WAVES waves, default 8) does the traceback.  Nodes are popped from an LDS
+// stack in the reference's LIFO order; every case is the reference's argmin with its strict `<`
+// (first minimum in loop order) computed as a parallel scan: each lane evaluates a strided subset
+// of the case's candidates and a lexicographic (value, position) reduction picks the first
+// minimum (see scan() for how short and long scans are spread).  Loops that the
 // reference runs one after another are scanned one after another, each result compared strictly
 // with the running minimum, so ties resolve exactly as in the sequential code.  The host
 // restatement (ccj_host.cc, Backtracker) is the same algorithm over the host mirror; the GPU tests
