@@ -21,6 +21,13 @@
 // int (interior-loop windows): such terms are skipped.
 #pragma clang fp contract(off)
 
+// CCJ_PF_ABLATE_ILOOP (timing experiments only, wrong results): skip the interior-loop windows
+#ifdef CCJ_PF_ABLATE_ILOOP
+#define PF_ILOOP_ON 0
+#else
+#define PF_ILOOP_ON 1
+#endif
+
 #include <hip/hip_runtime.h>
 
 #include "ccj_pf_energy.h"
@@ -290,7 +297,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         if (G.pt(i, j) > 0) {
             double r = 0;
             r += G.g4(PF_PL, i + 1, j - 1, k, l) * D.est[a * rs + i];
-            const int dmax = imin(j, i + MAXLOOP);
+            const int dmax = PF_ILOOP_ON ? imin(j, i + MAXLOOP) : 0;
             for (int d = i + 1; d < dmax; ++d) {
                 const int u1 = d - i - 1;
                 const int dpmin = imax(d + TURN, j - MAXLOOP);
@@ -316,7 +323,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         if (G.pt(k, l) > 0) {
             double r = 0;
             r += G.g4(PF_PR, i, j, k + 1, l - 1) * D.est[b * rs + k];
-            const int dmax = imin(l, k + MAXLOOP);
+            const int dmax = PF_ILOOP_ON ? imin(l, k + MAXLOOP) : 0;
             for (int d = k + 1; d < dmax; ++d) {
                 const int u1 = d - k - 1;
                 const int dpmin = imax(d + TURN, l - MAXLOOP);
@@ -346,7 +353,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
             // (0), so any finite value gives 0 — use 0 instead of reading past the table
             const double est_m = (j > 1 && k < n) ? D.est[(h + 4) * rs + (j - 1)] : 0.0;
             r += G.g4(PF_PM, i, j - 1, k + 1, l) * est_m;
-            const int dmin = imax(i, j - MAXLOOP), dpmax = imin(l, k + MAXLOOP);
+            const int dmin = PF_ILOOP_ON ? imax(i, j - MAXLOOP) : j, dpmax = imin(l, k + MAXLOOP);
             for (int d = j - 1; d > dmin; --d) {
                 const int u1 = j - d - 1;
                 for (int dp = k + 1; dp < dpmax; ++dp) {

@@ -102,6 +102,21 @@ def run(case):
     return rec
 
 
+SETS = {"default": [], "Turner04": ["-P", PARDIR + "/rna_Turner04.par"],
+        "DirksPierce09": ["-P", PARDIR + "/rna_DirksPierce09.par"], "DirksPierce03": ["-P", PARDIR + "/rna_DirksPierce03.par"],
+        "CaoChen06": ["-P", PARDIR + "/rna_CaoChen06.par"], "CaoChen09": ["-P", PARDIR + "/rna_CaoChen09.par"],
+        "Matthews04": ["-P", PARDIR + "/dna_Matthews04.par"], "DNA_Mathews2004": ["--dna"]}
+
+
+def exp_tables():
+    """The Boltzmann-table hashes of every bundled parameter set (a 9-nt run of each)."""
+    out = {}
+    for name, args in SETS.items():
+        p = subprocess.run([DRV, "GGGAAACCC"] + args, capture_output=True, text=True, timeout=600)
+        out[name] = {w[1]: w[2] for w in (l.split() for l in p.stdout.splitlines()) if w and w[0] == "EXP"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=8)
@@ -112,7 +127,7 @@ def main():
         recs = list(ex.map(run, cs))
     with open(OUT, "w") as f:
         json.dump({"generator": "oracle/gen_pf_golden.py", "driver": "oracle/_ref/pf_driver (part_func.cc, -ffp-contract=off)",
-                   "cases": recs}, f, indent=0)
+                   "exp_sets": exp_tables(), "cases": recs}, f, indent=0)
     print("wrote %d cases to %s" % (len(recs), OUT))
 
 

@@ -48,16 +48,25 @@ def test_golden_file_complete():
     assert any(c.get("samples") for c in cs)
 
 
-@pytest.mark.parametrize("params", ["default", "DirksPierce09"])
+def _exp_sets():
+    with open(GOLD) as f:
+        return json.load(f)["exp_sets"]
+
+
+@pytest.mark.parametrize("params", ["default", "Turner04", "DirksPierce09", "DirksPierce03", "CaoChen06", "CaoChen09",
+                                    "Matthews04", "DNA_Mathews2004"])
 def test_boltzmann_tables_match_reference(params):
+    """Every bundled set, with its .pfraw raw tables, against scale_pf_parameters() of the reference."""
     import ccj_amd
     try:
         ccj_amd.lib()
     except ccj_amd.CCJError:
         pytest.skip("libccj_hip.so not built")
-    ref = next(c["exp"] for c in _cases() if c["params"] == params)
-    ours = ccj_amd.pf_exp_hashes(params)
-    assert ours == ref
+    ref = _exp_sets()[params]
+    assert ccj_amd.pf_exp_hashes(params) == ref
+    for c in _cases():  # and what each golden case's own run printed
+        if c["params"] == params:
+            assert c["exp"] == ref
 
 
 def test_raw_tables_shipped_for_every_bundled_set():
