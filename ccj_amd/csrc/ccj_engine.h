@@ -196,6 +196,7 @@ int ccjk_level4d_lead(const ccj::DevTables *T, int t, int G, int rank, void *str
 int ccjk_pack(const ccj::DevTables *T, int t, int G, int r, int nmax, int16_t *send, void *stream);
 int ccjk_unpack(const ccj::DevTables *T, int t, int G, int r, int nmax, const int16_t *recv, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
+int ccjk_ppush(const ccj::DevTables *T, int lev, void *stream);
 int ccjk_canon(const ccj::DevTables *T, int x, const long long *offij, int16_t *out, void *stream);
 int ccjk_items(const ccj::DevTables *T, int G, int rank, int simulate, long long *counts, const long long *offs,
                uint32_t *items, int pass, void *stream);

@@ -1943,6 +1943,16 @@ extern "C" int ccj_reset(ccj_ctx *c, const char *seq) {
 // Enqueue the whole fill on the context's streams; it ends with ev_end on st, after which every
 // stream's work of the fill is complete (st waits for the last span, which waits for the last P,
 // and every level waited for its k_iloop / leader launches).
+// The P terms that complete P(lev+3): by default every term whose operands' highest level is lev
+// (k_ppush), or with CCJ_PTERM_PULL=1 the per-span pull form k_pterm(lev+3).
+static int pterm_launch(const ccj::DevTables *T, int lev, hipStream_t s) {
+    static const bool pull = [] {
+        const char *e = getenv("CCJ_PTERM_PULL");
+        return e && atoi(e) != 0;
+    }();
+    return pull ? ccjk_pterm(T, lev + 3, s) : ccjk_ppush(T, lev, s);
+}
+
 static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     if (!c) return CCJ_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -2050,11 +2060,11 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
             // P(s+3) only needs PK levels <= s
             if (s + 3 < n) {
                 HIPCHK(c, hipStreamWaitEvent(c->st_p, c->lev_done[s], 0));
-                HIPCHK(c, (hipError_t)ccjk_pterm(&c->T, s + 3, c->st_p));
+                HIPCHK(c, (hipError_t)pterm_launch(&c->T, s, c->st_p));
                 HIPCHK(c, hipEventRecord(c->p_done[s + 3], c->st_p));
             }
         } else if (s + 3 < n && s + 3 >= 3) {
-            HIPCHK(c, (hipError_t)ccjk_pterm(&c->T, s + 3, c->st_p));
+            HIPCHK(c, (hipError_t)pterm_launch(&c->T, s, c->st_p));
             HIPCHK(c, hipEventRecord(c->p_done[s + 3], c->st_p));
         }
     }

@@ -436,6 +436,200 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
 }
 
 // ------------------------------------------------------------------------------------------
+// P terms pushed by level (the default; k_pterm above is the per-span pull form, CCJ_PTERM_PULL=1).
+// A term of P(i, i+sigma) reads A = PK(i,j,d+1,k) at level t1 = jo+(ko-do-1) and
+// B = PK(j+1,d,k+1,l) at level t2 = (do-jo-1)+(sigma-ko-1), with t1 + t2 = sigma-3 (offsets
+// jo = j-i, do = d-i, ko = k-i).  k_ppush(T), enqueued after level T, evaluates every term with
+// max(t1, t2) = T: part A t1 = T (t2 <= T), part B t2 = T (t1 < T).  That completes P(T+3), exactly
+// what the pull launch k_pterm(T+3) did at the same point of the schedule, and leaves partial
+// minima of P(sigma > T+3) in T.Pk.  The gain: the level-T operand of a term is the same cell for
+// PP_S consecutive spans, so a wave loads it once and pairs it with PP_S partners (1 + 1/PP_S loads
+// per term instead of 2), and it is the level just written (L2 / MALL resident).
+//   part A wave: (jo, 64 consecutive i, PP_S consecutive t2), loop h1 = do-jo-1 ascending:
+//       A = level T, block jo, row h1, position i          (once per h1)
+//       B = level t2, block h1, row T-jo, position i+jo+1  (per t2, valid while h1 <= t2)
+//   part B wave: (a2 = do-jo-1, 64 consecutive l, PP_S consecutive t1), loop h2 = ko-do-1 descending:
+//       B = level T, block a2, row h2, position l-h2-T-2            (once per h2)
+//       A = level t1, block t1-h2, row a2, position l-T-3-t1 = i    (per t1, valid while h2 <= t1)
+// Both loops visit the terms of one output in ascending (jo, do, ko) order, so a strict < keeps the
+// reference's first minimum within a wave; across waves the 64-bit key atomicMin does (k_pterm).
+// ------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ const int16_t *pk_row(const DevTables &T, int t, int a, int h) {
+    const int m = T.n - t - 2;
+    const LvlDev *__restrict__ LD = T.ld;  // read-only in the kernel: scalar loads
+    const LvlDev L = LD[t];
+    return T.d4 + L.lb + (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) - 1;  // + position (1-based)
+}
+
+// one int16 of a PK row: wave-uniform row pointer + 32-bit lane offset (saddr + voffset load)
+__device__ __forceinline__ int pk_at(const DevTables &T, const int16_t *row, int t, int a, int h, int pos) {
+#ifdef CCJ_DEBUG_BOUNDS
+    if (t < 0 || t >= T.nlev || a < 0 || a > t || h < 0 || h >= T.n - t - 2 || pos < 1 || pos > T.n - t - 2 - h) {
+        atomicOr(T.err, 32);
+        return 0;
+    }
+#endif
+    typedef const __attribute__((address_space(1))) char gchar;
+    typedef const __attribute__((address_space(1))) int16_t gshort;
+    return (int)*(gshort *)((gchar *)row + (unsigned)(pos << 1));  // global_load saddr + voffset
+}
+
+// a wave-uniform pointer, marked so (keeps row bases in SGPRs: saddr loads, no 64-bit VALU adds)
+__device__ __forceinline__ const int16_t *uni(const int16_t *p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    return (const int16_t *)(((unsigned long long)hi << 32) | lo);
+}
+
+// A wave's running minimum per span is one int: (value << 10) + code, code = the step's position in
+// the reference order (h1 in part A, 1023 - h2 in part B; n <= 1023), so v_min keeps the first
+// minimum.  Steps that are not terms of a span (h > its t) add PP_OFF and never win.
+constexpr int PP_OFF = 1 << 30;
+
+template <int PP_S>
+__global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, int npairs, int hs_len, int blocksA) {
+    const int n = T.n, rs = T.rs;
+    const int lane = threadIdx.x & 63;
+    const int partB = (int)blockIdx.x >= blocksA;
+    // wave-uniform (readfirstlane: lets the compiler keep every index below in SGPRs)
+    const int item = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - (partB ? blocksA : 0)) * 4 + (int)(threadIdx.x >> 6));
+    // item = (pair * ngrp + g) * (lev+1) + outer; outer = jo (part A) / a2 (part B); pair = one
+    // (chunk c of PP_S spans, slice hs = [hs*hs_len, +hs_len) of the inner loop h1 / h2), so long
+    // loops spread over waves.  Chunk c's inner loop runs over h < min((c+1)*PP_S, nmax), so it has
+    // ceil(that / hs_len) slices; the pairs are enumerated chunk by chunk (part A's count, nmax).
+    const int outer = item % (lev + 1);
+    int pr = item / (lev + 1);
+    const int g = pr % ngrp;
+    pr /= ngrp;
+    if (pr >= npairs) return;  // whole wave
+    const int nmax = imin(lev, n - 4 - lev) + 1;
+    int c = 0;
+    for (;; ++c) {  // scalar: at most nmax / PP_S steps
+        const int cnt = (imin((c + 1) * PP_S, nmax) + hs_len - 1) / hs_len;
+        if (pr < cnt) break;
+        pr -= cnt;
+    }
+    const int hs = pr;
+    const int nother = (partB ? imin(lev - 1, n - 4 - lev) : imin(lev, n - 4 - lev)) + 1;  // t2 (A) / t1 (B) count
+    const int o0 = c * PP_S;
+    if (o0 >= nother) return;
+    const int ns = imin(PP_S, nother - o0);
+    const int h_lo = hs * hs_len;
+    const int hmax = imin(o0 + ns - 1, h_lo + hs_len - 1);
+    if (h_lo > hmax) return;
+    int bv[PP_S];
+#pragma unroll
+    for (int s = 0; s < PP_S; ++s) bv[s] = 0x7fffffff;
+    const int mT = n - lev - 2;
+    const LvlDev *__restrict__ LD = T.ld;
+    const int16_t *lev0 = T.d4 + LD[lev].lb - 1;
+    if (!partB) {
+        const int jo = outer, b1 = lev - jo;
+        const int i = 1 + g * 64 + lane;
+        if (1 + g * 64 > n - (lev + 3 + o0)) return;  // no lane has an interval of the shortest span
+        const int16_t *rowA0 = lev0 + (long long)jo * LD[lev].M;
+        const int16_t *rowB[PP_S];
+        int Ms[PP_S], offB[PP_S];
+#pragma unroll
+        for (int s = 0; s < PP_S; ++s) {
+            const int t2 = imin(o0 + s, o0 + ns - 1);
+            rowB[s] = pk_row(T, t2, 0, b1);  // block h1 added per step
+            Ms[s] = LD[t2].M;
+            offB[s] = imin(i, n - (lev + 3 + t2)) + jo + 1;
+        }
+        // two steps per iteration, all 2 * (PP_S + 1) loads in flight together (the second step of
+        // an odd tail re-reads the first and is masked)
+        for (int h1 = h_lo; h1 <= hmax; h1 += 2) {
+            int va[2], vb[2][PP_S], hh[2];
+            hh[0] = h1;
+            hh[1] = imin(h1 + 1, hmax);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int h = hh[u];
+                va[u] = pk_at(T, uni(rowA0 + h * mT - ((h * (h - 1)) >> 1)), lev, jo, h, imin(i, mT - h));
+                // every load unconditional (steps with h1 > t2 read a clamped valid cell and are
+                // masked)
+#pragma unroll
+                for (int s = 0; s < PP_S; ++s) {
+                    const int t2 = imin(o0 + s, o0 + ns - 1), hc = imin(h, t2);
+                    vb[u][s] = pk_at(T, uni(rowB[s] + (long long)hc * Ms[s]), t2, hc, b1, offB[s]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const bool live = u == 0 || h1 + 1 <= hmax;
+#pragma unroll
+                for (int s = 0; s < PP_S; ++s) {
+                    const int code = (live && s < ns && hh[u] <= o0 + s) ? hh[u] : PP_OFF;
+                    bv[s] = imin(bv[s], ((va[u] + vb[u][s]) << 10) + code);
+                }
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < PP_S; ++s) {
+            const int sg = lev + 3 + o0 + s;
+            if (s < ns && i + sg <= n && bv[s] < (PP_OFF >> 1)) {
+                const unsigned dd = (unsigned)(jo + 1 + (bv[s] & 1023)), ko = dd + 1u + (unsigned)b1;
+                const unsigned key = ((unsigned)jo * (unsigned)sg + dd) * (unsigned)sg + ko;
+                atomicMin(T.Pk + sg * rs + i, ((unsigned long long)((unsigned)(bv[s] >> 10) + 0x80000000u) << 32) | key);
+            }
+        }
+    } else {
+        const int a2 = outer;
+        const int l = lev + 4 + o0 + g * 64 + lane;
+        if (lev + 4 + o0 + g * 64 > n) return;
+        const int lc = imin(l, n);
+        const int16_t *rowB0 = lev0 + (long long)a2 * LD[lev].M;
+        const int16_t *rowA[PP_S];
+        int Ms[PP_S], offA[PP_S];
+#pragma unroll
+        for (int s = 0; s < PP_S; ++s) {
+            const int t1 = imin(o0 + s, o0 + ns - 1);
+            rowA[s] = pk_row(T, t1, t1, a2);  // block t1-h2: minus h2*M per step
+            Ms[s] = LD[t1].M;
+            offA[s] = imax(1, lc - (lev + 3 + t1));
+        }
+        for (int h2 = hmax; h2 >= h_lo; h2 -= 2) {  // two steps per iteration, as in part A
+            int vb[2], va[2][PP_S], hh[2];
+            hh[0] = h2;
+            hh[1] = imax(h2 - 1, h_lo);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int h = hh[u];
+                vb[u] = pk_at(T, uni(rowB0 + h * mT - ((h * (h - 1)) >> 1)), lev, a2, h, imax(1, imin(lc - h - lev - 2, mT - h)));
+#pragma unroll
+                for (int s = 0; s < PP_S; ++s) {  // unconditional loads, clamped and masked as in part A
+                    const int t1 = imin(o0 + s, o0 + ns - 1), hc = imin(h, t1);
+                    va[u][s] = pk_at(T, uni(rowA[s] - (long long)hc * Ms[s]), t1, t1 - hc, a2, offA[s]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const bool live = u == 0 || h2 - 1 >= h_lo;
+#pragma unroll
+                for (int s = 0; s < PP_S; ++s) {
+                    const int code = (live && s < ns && hh[u] <= o0 + s) ? 1023 - hh[u] : PP_OFF;
+                    bv[s] = imin(bv[s], ((va[u][s] + vb[u]) << 10) + code);
+                }
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < PP_S; ++s) {
+            const int sg = lev + 3 + o0 + s;
+            const int i = l - sg;
+            if (s < ns && l <= n && i >= 1 && bv[s] < (PP_OFF >> 1)) {
+                const unsigned h2 = 1023u - (unsigned)(bv[s] & 1023);
+                const unsigned jo = (unsigned)(o0 + s) - h2, dd = jo + 1u + (unsigned)a2, ko = dd + 1u + h2;
+                const unsigned key = (jo * (unsigned)sg + dd) * (unsigned)sg + ko;
+                atomicMin(T.Pk + sg * rs + i, ((unsigned long long)((unsigned)(bv[s] >> 10) + 0x80000000u) << 32) | key);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Interior-loop candidate lists (once per problem, after k_precompute_ie).
 // For pair (p, q = p+w):
 //   il  — loops closed by (p,q) around an inner pair (d,dp) = (p+1+u1, q-1-u2), the window of
@@ -1728,6 +1922,39 @@ extern "C" int ccjk_pterm(const DevTables *T, int sigma, void *stream) {
     const int blocks = xcd ? 8 * xcd * ((total + 8 * xcd - 1) / (8 * xcd)) : total;
     hipLaunchKernelGGL(k_pterm, dim3((unsigned)blocks), dim3(64 * PT_WAVES), 0, (hipStream_t)stream, *T, sigma, ngroups, gx,
                        total, xcd);
+    return (int)hipGetLastError();
+}
+
+// P terms of every span whose operands' highest level is lev (k_ppush); completes P(lev+3).
+extern "C" int ccjk_ppush(const DevTables *T, int lev, void *stream) {
+#ifdef CCJ_ABLATE_PTERM
+    return 0;
+#endif
+    const int n = T->n;
+    const int nmax = imin(lev, n - 4 - lev) + 1;  // t2 values of part A (part B has one fewer or equal)
+    if (nmax <= 0) return 0;
+    const int ngrp = (n - lev - 3 + 63) / 64;
+    static const int S = [] {  // spans per wave = partners per reused load (8; CCJ_PP_S=4 / 16)
+        const char *e = getenv("CCJ_PP_S");
+        return e && (atoi(e) == 16 || atoi(e) == 4) ? atoi(e) : 8;
+    }();
+    const int nch = (nmax + S - 1) / S;
+    static const int hs_len = [] {
+        const char *e = getenv("CCJ_PP_HS");
+        return e && atoi(e) > 0 ? atoi(e) : 32;
+    }();
+    int npairs = 0;  // (chunk, inner-loop slice) pairs, as k_ppush enumerates them
+    for (int c = 0; c < nch; ++c) npairs += (imin((c + 1) * S, nmax) + hs_len - 1) / hs_len;
+    const int blocksA = (npairs * ngrp * (lev + 1) + 3) / 4;
+    if (S == 4)
+        hipLaunchKernelGGL(k_ppush<4>, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp,
+                           npairs, hs_len, blocksA);
+    else if (S == 16)
+        hipLaunchKernelGGL(k_ppush<16>, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp,
+                           npairs, hs_len, blocksA);
+    else
+        hipLaunchKernelGGL(k_ppush<8>, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp,
+                           npairs, hs_len, blocksA);
     return (int)hipGetLastError();
 }
 
