@@ -1653,19 +1653,28 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_il, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_d, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_pre, hipStreamNonBlocking));
+    // The cross-stream events only order work on this device, so they are recorded without the
+    // default system-scope fence (hipEventDisableSystemFence: fill -0.65 ms at n=200);
+    // CCJ_EV_FENCE=0 restores it.  ev_start / ev_end, which the host waits on, keep it.
+    static const unsigned fence_fl = [] {
+        const char *e = getenv("CCJ_EV_FENCE");
+        return (e && atoi(e) == 0) ? 0u : (unsigned)hipEventDisableSystemFence;
+    }();
+    const unsigned sync_fl = hipEventDisableTiming | fence_fl;
     c->pre_done.resize(n + 1);
-    for (auto &e : c->pre_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto &e : c->pre_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
     c->il_done.resize(n + 1);
-    for (auto &e : c->il_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto &e : c->il_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
     c->dg_done.resize(n + 1);
-    for (auto &e : c->dg_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto &e : c->dg_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
     HIPCHK(cp, hipEventCreate(&c->ev_start));
     HIPCHK(cp, hipEventCreate(&c->ev_end));
     HIPCHK(cp, hipEventCreate(&c->ev_pre));
     c->lev_done.resize(n + 1);
-    for (auto &e : c->lev_done) HIPCHK(cp, hipEventCreate(&e));  // timed: the level durations (mode 1)
+    // timed: the level durations (mode 1)
+    for (auto &e : c->lev_done) HIPCHK(cp, hipEventCreateWithFlags(&e, fence_fl));
     c->p_done.resize(n + 1);
-    for (auto &e : c->p_done) HIPCHK(cp, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto &e : c->p_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
     c->tev.resize(7 * (size_t)n + 7);
     for (auto &e : c->tev) HIPCHK(cp, hipEventCreate(&e));
 

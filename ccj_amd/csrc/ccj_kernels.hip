@@ -825,30 +825,43 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
             const int c = il_e(E[u].x) + v[u];
             if (PMWIN) {
                 const int u1 = il_u1(E[u].x), u2 = il_dt(E[u].x) - 2 - u1;
-                b1 = imin(b1, (u1 <= as - 2 && u2 <= bs - 2) ? c : INF);  // get_PMiloop: d > i, dp < l
+                // get_PMiloop: d > i, dp < l.  Branch-free (a select of constants): a branch here
+                // splits the loop body, and the compiler then sign-extends the next batch's loads
+                // in the latch, draining every load before the back-edge
+                b1 = imin(b1, c + ((u1 > as - 2) | (u2 > bs - 2) ? INF : 0));
             } else {
                 b1 = imin(b1, c);
             }
         }
     };
-    uint2 E[IL_B];
-    int v[IL_B];
-    fetch(0, E);
-    issue(E, v);
+    // Ping-pong buffers, two batches per trip: a batch's registers are written only after the
+    // batch they replace was reduced, so the loop carries no register copies.  (With one buffer
+    // and a copy per trip, the copy of a just-issued load made the compiler wait for every load
+    // before the back-edge: one full memory latency per batch instead of overlapped batches.)
+    uint2 Ea[IL_B], Eb[IL_B];
+    int va[IL_B], vb[IL_B];
+    fetch(0, Ea);
+    issue(Ea, va);
+    int e0 = IL_B;
 #pragma unroll 1
-    for (int e0 = IL_B; e0 < cnt; e0 += IL_B) {
-        uint2 En[IL_B];
-        int vn[IL_B];
-        fetch(e0, En);
-        issue(En, vn);
-        reduce(E, v);
-#pragma unroll
-        for (int u = 0; u < IL_B; ++u) {
-            E[u] = En[u];
-            v[u] = vn[u];
+    while (true) {
+        if (e0 >= cnt) {
+            reduce(Ea, va);
+            break;
         }
+        fetch(e0, Eb);
+        issue(Eb, vb);
+        reduce(Ea, va);
+        e0 += IL_B;
+        if (e0 >= cnt) {
+            reduce(Eb, vb);
+            break;
+        }
+        fetch(e0, Ea);
+        issue(Ea, va);
+        reduce(Eb, vb);
+        e0 += IL_B;
     }
-    reduce(E, v);
     return b1;
 }
 
@@ -908,31 +921,42 @@ __device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__rest
             const int c = il_e(E[u]) + v[u];
             if (PMWIN) {
                 const int u1 = il_u1(E[u]), u2 = il_dt(E[u]) - 2 - u1;
-                b1 = imin(b1, (u1 <= as - 2 && u2 <= bs - 2) ? c : INF);
+                b1 = imin(b1, c + ((u1 > as - 2) | (u2 > bs - 2) ? INF : 0));
             } else {
                 b1 = imin(b1, c);
             }
         }
     };
-    uint32_t E[ILG_B];
-    int v[ILG_B];
+    // Ping-pong as in il_scan, with the (per-lane, vector-memory) entries loaded one batch ahead:
+    // loads return in order, so waiting for batch k+1's entries also waits for batch k's partners;
+    // issuing k+1's partners together with k+2's entries keeps two loads per lane in flight
+    // across each wait instead of one.
+    uint32_t Ea[ILG_B], Eb[ILG_B];
+    int va[ILG_B], vb[ILG_B];
     const int stepE = G * ILG_B;
-    fetch(0, E);
-    issue(E, v);
+    fetch(0, Ea);
+    issue(Ea, va);
+    fetch(stepE, Eb);
+    int e0 = stepE;
 #pragma unroll 1
-    for (int e0 = stepE; e0 < cnt; e0 += stepE) {
-        uint32_t En[ILG_B];
-        int vn[ILG_B];
-        fetch(e0, En);
-        issue(En, vn);
-        reduce(E, v);
-#pragma unroll
-        for (int u = 0; u < ILG_B; ++u) {
-            E[u] = En[u];
-            v[u] = vn[u];
+    while (true) {
+        if (e0 >= cnt) {
+            reduce(Ea, va);
+            break;
         }
+        issue(Eb, vb);
+        reduce(Ea, va);
+        fetch(e0 + stepE, Ea);
+        e0 += stepE;
+        if (e0 >= cnt) {
+            reduce(Eb, vb);
+            break;
+        }
+        issue(Ea, va);
+        reduce(Eb, vb);
+        fetch(e0 + stepE, Eb);
+        e0 += stepE;
     }
-    reduce(E, v);
     for (int off = W; off < 64; off <<= 1) b1 = imin(b1, __shfl_xor(b1, off));
     return b1;
 }
