@@ -1121,6 +1121,63 @@ __device__ __forceinline__ void write_records(const DevTables &T, long long lr, 
     rp[2u * (unsigned)C + cell] = make_uint4(pk16(Rm00, Mm00), pk16(Om00, Mm10), pk16(Om10, fR), pk16(fO, INTERN_INF));
 }
 
+
+// Software-pipelined split scan: visits s = s0, s0+step, ... <= last, issuing the loads of step
+// s+step before reducing step s (mask: 0 while s < mlim, INF on the last split point).  The loads
+// return raw registers (records, (WBP, WP) pairs) and every field is unpacked in the reduce, so
+// nothing waits on a load before its step is reduced; and the two buffers alternate (ping-pong),
+// so the loop carries no register copies.  (Round 2 before this: unpack at load time and
+// `cur = nxt` each trip, which made the compiler wait for every load of the next step before the
+// back-edge — one full memory latency per split step.)
+template <class V, class LD, class ST>
+__device__ __forceinline__ void pipe_scan(int s, int step, int last, int mlim, LD ld, ST st) {
+    V A = ld(s);
+#pragma unroll 1
+    for (;;) {
+        int sn = s + step;
+        if (sn > last) {
+            st(A, s < mlim ? 0 : INF);
+            return;
+        }
+        const V B = ld(sn);
+        st(A, s < mlim ? 0 : INF);
+        s = sn;
+        sn = s + step;
+        if (sn > last) {
+            st(B, s < mlim ? 0 : INF);
+            return;
+        }
+        A = ld(sn);
+        st(B, s < mlim ? 0 : INF);
+        s = sn;
+    }
+}
+// The one-buffer loop shape (`cur = nxt`).  The leaders' loops keep it: their ping-pong form
+// needs 241 VGPRs instead of ~150 (2 waves/SIMD) and measured fill +5 ms; CCJ_PIPE_LEAD_NEW builds
+// it, CCJ_PIPE_OLD uses the one-buffer shape for every split loop (fill +0.6 ms).
+template <class V, class LD, class ST>
+__device__ __forceinline__ void pipe_scan_old(int s, int step, int last, int mlim, LD ld, ST st) {
+    V cur = ld(s);
+    for (;;) {
+        const int sn = s + step;
+        const V nxt = ld(imin(sn, last));
+        st(cur, s < mlim ? 0 : INF);
+        if (sn > last) break;
+        cur = nxt;
+        s = sn;
+    }
+}
+#ifdef CCJ_PIPE_OLD
+#define PIPE_SCAN pipe_scan_old
+#define PIPE_SCAN_LEAD pipe_scan_old
+#elif defined(CCJ_PIPE_LEAD_NEW)
+#define PIPE_SCAN pipe_scan
+#define PIPE_SCAN_LEAD pipe_scan
+#else
+#define PIPE_SCAN pipe_scan
+#define PIPE_SCAN_LEAD pipe_scan_old
+#endif
+
 // ------------------------------------------------------------------------------------------
 // 4-D level t: one lane per cell (i,j,k,l); all lanes of a wave share (t, a) so every loop bound
 // is wave-uniform.  pseudo_loop.cc:181-644, 663-808.
@@ -1199,11 +1256,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #define LDX(lp, L, x, U, ln) ((int)(lp)[(unsigned)((x) * (L).C + (U)) + (ln)])
     // WB of an interval of `len` bases from its WBP, as k_diag2d stores it (get_WB,
     // pseudo_loop.cc:647-653: min(cp*len, WBP)): one load fewer per split side
-#ifdef CCJ_WB_LOAD
-#define WBD(wbp, len, idx) ((int)WB[idx])
-#else
-#define WBD(wbp, len, idx) imin(cp * (len), (wbp))
-#endif
+#define WBD(wbp, len) imin(cp * (len), (wbp))
 #ifdef CCJ_DEBUG_BOUNDS
 #define CHK(dt, ap_, dh, di) \
     if ((dt) < 1 || (dt) > t || (ap_) < 0 || (ap_) > t - (dt) || h + (dh) >= m + (dt) || i + (di) < 1 || \
@@ -1255,15 +1308,13 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     int pLm00 = seed, pLm01 = INF, pLm10 = INF, pMm00 = seed, pMm10 = INF;
     int pOm00 = seed, pOm10 = INF;
     int fL1 = INF, fL2 = INF, fM = INF, fO1 = INF, pK1 = INF;
-    struct AV { int wb_i, wbp_i, wp_i, wb_j, wbp_j, wp_j, Lm00i, Mm00i, Om00i, fLi, fOi, Lm00j, Mm00j, Lm10j, fLj, fMpj, Kj; };
+    struct AV { int2 w2i, w2j; uint4 wi, wj; int s; };  // raw loads of one split step
     auto load_a = [&](int s) {
         AV v;
+        v.s = s;
         const int r2 = (s - 1) * rs, jl = j - s + 1;
-        const int2 w2i = WBW[r2 + i], w2j = WBW[r2 + jl];  // (WBP, WP) of (i, i+s-1) and (j-s+1, j)
-        v.wbp_i = w2i.x; v.wp_i = w2i.y;
-        v.wbp_j = w2j.x; v.wp_j = w2j.y;
-        v.wb_i = WBD(v.wbp_i, s, r2 + i);
-        v.wb_j = WBD(v.wbp_j, s, r2 + jl);
+        v.w2i = WBW[r2 + i];  // (WBP, WP) of (i, i+s-1)
+        v.w2j = WBW[r2 + jl];  // (WBP, WP) of (j-s+1, j)
         CHK(s, a - s, 0, s);
         CHK(s, a - s, s, 0);
 #ifdef CCJ_ABLATE_LOCAL
@@ -1279,27 +1330,29 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         const uint4 *rp = T.rec + L.lr;
         CHKR(L.lr + (unsigned)Ui + lh);
         CHKR(L.lr + (unsigned)Uj + L0);
-        const uint4 wi = rp[(unsigned)Ui + lh];
-        const uint4 wj = rp[(unsigned)Uj + L0];
-        v.Lm00i = lo16(wi.x); v.Mm00i = hi16(wi.x); v.Om00i = lo16(wi.y); v.fLi = hi16(wi.y); v.fOi = lo16(wi.z);
-        v.Lm00j = lo16(wj.x); v.Mm00j = hi16(wj.x); v.fLj = hi16(wj.y); v.Lm10j = hi16(wj.z);
-        v.fMpj = lo16(wj.w); v.Kj = hi16(wj.w);
+        v.wi = rp[(unsigned)Ui + lh];
+        v.wj = rp[(unsigned)Uj + L0];
         return v;
     };
     auto step_a = [&](const AV &v, int mask) {
-        pLm00 = imin(pLm00, imin(v.wb_i + v.Lm00i, v.Lm00j + v.wb_j));  // :449-458
-        pLm01 = imin(pLm01, v.Lm00j + v.wbp_j);                         // :468-471
-        pLm10 = imin(pLm10, v.wbp_i + v.Lm00i);                         // :481-483
-        pMm00 = imin(pMm00, v.Mm00j + v.wb_j);                          // :548-551
-        pMm10 = imin(pMm10, v.wbp_i + v.Mm00i);                         // :581-584
-        pOm00 = imin(pOm00, v.wb_i + v.Om00i);                          // :599-602
-        pOm10 = imin(pOm10, v.wbp_i + v.Om00i);                         // :632-635
-        fL1 = imin(fL1, v.fLi + v.wp_i + mask);         // PfromL(d,j,k,l) + WP(i,d-1)      :357-359
-        fO1 = imin(fO1, v.fOi + v.wp_i + mask);         // PfromO(d,j,k,l) + WP(i,d-1)      :425-427
-        pLm10 = imin(pLm10, v.Lm10j + v.wb_j + mask);   // PLmloop10(i,d,k,l) + WB(d+1,j)   :484-486
-        fL2 = imin(fL2, v.fLj + v.wp_j + mask);         // PfromL(i,d,k,l) + WP(d+1,j)      :360-361
-        fM = imin(fM, v.fMpj + v.wp_j + mask);          // PfromMprime(i,d,k,l) + WP(d+1,j) :399-401
-        pK1 = imin(pK1, v.Kj + v.wp_j + mask);          // PK(i,d,k,l) + WP(d+1,j)          :184-187
+        const int wbp_i = v.w2i.x, wp_i = v.w2i.y, wbp_j = v.w2j.x, wp_j = v.w2j.y;
+        const int wb_i = WBD(wbp_i, v.s), wb_j = WBD(wbp_j, v.s);
+        const int Lm00i = lo16(v.wi.x), Mm00i = hi16(v.wi.x), Om00i = lo16(v.wi.y), fLi = hi16(v.wi.y), fOi = lo16(v.wi.z);
+        const int Lm00j = lo16(v.wj.x), Mm00j = hi16(v.wj.x), fLj = hi16(v.wj.y), Lm10j = hi16(v.wj.z);
+        const int fMpj = lo16(v.wj.w), Kj = hi16(v.wj.w);
+        pLm00 = imin(pLm00, imin(wb_i + Lm00i, Lm00j + wb_j));  // :449-458
+        pLm01 = imin(pLm01, Lm00j + wbp_j);                     // :468-471
+        pLm10 = imin(pLm10, wbp_i + Lm00i);                     // :481-483
+        pMm00 = imin(pMm00, Mm00j + wb_j);                      // :548-551
+        pMm10 = imin(pMm10, wbp_i + Mm00i);                     // :581-584
+        pOm00 = imin(pOm00, wb_i + Om00i);                      // :599-602
+        pOm10 = imin(pOm10, wbp_i + Om00i);                     // :632-635
+        fL1 = imin(fL1, fLi + wp_i + mask);        // PfromL(d,j,k,l) + WP(i,d-1)      :357-359
+        fO1 = imin(fO1, fOi + wp_i + mask);        // PfromO(d,j,k,l) + WP(i,d-1)      :425-427
+        pLm10 = imin(pLm10, Lm10j + wb_j + mask);  // PLmloop10(i,d,k,l) + WB(d+1,j)   :484-486
+        fL2 = imin(fL2, fLj + wp_j + mask);        // PfromL(i,d,k,l) + WP(d+1,j)      :360-361
+        fM = imin(fM, fMpj + wp_j + mask);         // PfromMprime(i,d,k,l) + WP(d+1,j) :399-401
+        pK1 = imin(pK1, Kj + wp_j + mask);         // PK(i,d,k,l) + WP(d+1,j)          :184-187
     };
     // a-leader: one scan of s = 1..a for this cell (r = 0) and its followers r = 1..R-1:
     //   i side: cell (i-r, j, k, l) (level t+r, block a+r, row h), term X(i+s,j,k,l) + W(i-r, i+s-1)
@@ -1311,9 +1364,10 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         for (int r = 0; r < SHARE_R; ++r)
 #pragma unroll
             for (int f = 0; f < 7; ++f) AI_[r][f] = AJ_[r][f] = INF;
-        struct LA { uint4 wi, wj; wv_t qb, qbp, qp, pb, pbp, pp; };
+        struct LA { uint4 wi, wj; int2 q[SHARE_R], p[SHARE_R]; int s; };  // raw loads of one split step
         auto ld = [&](int s) {
             LA v;
+            v.s = s;
             const LvlDev L = LD[t - s];
             const int Ui = (a - s) * L.M + s;
             const int Uj = (a - s) * L.M + s * m + ((s * (s + 1)) >> 1);
@@ -1327,11 +1381,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
-                const int2 wq = WBW[o + i - r], wp2 = WBW[o + j - s + 1];
-                v.qbp[SHARE_R - 1 - r] = wq.x; v.qp[SHARE_R - 1 - r] = wq.y;
-                v.pbp[r] = wp2.x; v.pp[r] = wp2.y;
-                v.qb[SHARE_R - 1 - r] = WBD(v.qbp[SHARE_R - 1 - r], s + r, o + i - r);
-                v.pb[r] = WBD(v.pbp[r], s + r, o + j - s + 1);
+                v.q[r] = WBW[o + i - r];
+                v.p[r] = WBW[o + j - s + 1];
             }
             return v;
         };
@@ -1342,8 +1393,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             const int fMpj = lo16(v.wj.w), Kj = hi16(v.wj.w);
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
-                const int wbi = v.qb[SHARE_R - 1 - r], wbpi = v.qbp[SHARE_R - 1 - r], wpi = v.qp[SHARE_R - 1 - r];
-                const int wbj = v.pb[r], wbpj = v.pbp[r], wpj = v.pp[r];
+                const int wbpi = v.q[r].x, wpi = v.q[r].y, wbi = WBD(wbpi, v.s + r);
+                const int wbpj = v.p[r].x, wpj = v.p[r].y, wbj = WBD(wbpj, v.s + r);
                 int *I = AI_[r], *J = AJ_[r];
                 I[0] = imin(I[0], wbi + Lm00i);          // PLmloop00 :449-458
                 I[1] = imin(I[1], wbpi + Lm00i);         // PLmloop10 :481-483
@@ -1361,18 +1412,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 J[6] = imin(J[6], Kj + wpj + mask);      // PK        :184-187
             }
         };
-        if (s_first + part <= a) {
-            int s = s_first + part;
-            LA cur = ld(s);
-            for (;;) {
-                const int sn = s + split;
-                const LA nxt = ld(imin(sn, a));
-                st(cur, s < a ? 0 : INF);
-                if (sn > a) break;
-                cur = nxt;
-                s = sn;
-            }
-        }
+        if (s_first + part <= a) PIPE_SCAN_LEAD<LA>(s_first + part, split, a, a, ld, st);
         // slices handed over through the ring: the followers' (r >= 1), and in the prepass scheme
         // the cell's own (r = 0) too; otherwise r = 0 stays in this wave's accumulators
         const int r0 = prem ? 0 : 1;
@@ -1442,16 +1482,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     if (arole == 1 && LEAD) {
         lead_a();
     } else if (s_first + part <= a_stop) {
-        int s = s_first + part;
-        AV cur = load_a(s);
-        for (;;) {
-            const int sn = s + split;
-            const AV nxt = load_a(imin(sn, a_stop));  // the last one re-reads step a_stop (discarded)
-            step_a(cur, s < a ? 0 : INF);
-            if (sn > a_stop) break;
-            cur = nxt;
-            s = sn;
-        }
+        PIPE_SCAN<AV>(s_first + part, split, a_stop, a, load_a, step_a);
     }
     // the ring record of the a-loop: a follower's leader partial (split points a%R+1 .. a, or
     // a%R+2 .. a in the prepass scheme), and in the prepass scheme the own s >= 2 partial of a
@@ -1477,15 +1508,13 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     // ---- fused b-loop: split point d inside [k, l] ----
     int pRm00 = seed, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
     int fR1 = INF, fR2 = INF, fMp = INF, fO2 = INF, pK2 = INF;
-    struct BV { int wb_k, wbp_k, wp_k, wb_l, wbp_l, wp_l, Rm00k, Mm00k, fRk, PLRk, Kk, Rm00l, Mm00l, Om00l, Mm10l, Om10l, fRl, fOl; };
+    struct BV { int2 w2k, w2l; uint4 wk, wl; int s; };  // raw loads of one split step
     auto load_b = [&](int s) {
         BV v;
+        v.s = s;
         const int r2 = (s - 1) * rs, ll = l - s + 1;
-        const int2 w2k = WBW[r2 + k], w2l = WBW[r2 + ll];  // (WBP, WP) of (k, k+s-1) and (l-s+1, l)
-        v.wbp_k = w2k.x; v.wp_k = w2k.y;
-        v.wbp_l = w2l.x; v.wp_l = w2l.y;
-        v.wb_k = WBD(v.wbp_k, s, r2 + k);
-        v.wb_l = WBD(v.wbp_l, s, r2 + ll);
+        v.w2k = WBW[r2 + k];   // (WBP, WP) of (k, k+s-1)
+        v.w2l = WBW[r2 + ll];  // (WBP, WP) of (l-s+1, l)
         CHK(s, a, s, 0);
         CHK(s, a, 0, 0);
 #ifdef CCJ_ABLATE_LOCAL
@@ -1502,28 +1531,30 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         const uint4 *rp = T.rec + L.lr;
         CHKR(L.lr + L.C + (unsigned)Uk + L0);
         CHKR(L.lr + 2 * L.C + (unsigned)Ul + lh);
-        const uint4 wk = rp[(unsigned)(L.C + Uk) + L0];
-        const uint4 wl = rp[(unsigned)(2 * L.C + Ul) + lh];
-        v.Rm00k = lo16(wk.x); v.Mm00k = hi16(wk.x); v.fRk = lo16(wk.y); v.PLRk = hi16(wk.y); v.Kk = lo16(wk.z);
-        v.Rm00l = lo16(wl.x); v.Mm00l = hi16(wl.x); v.Om00l = lo16(wl.y); v.Mm10l = hi16(wl.y);
-        v.Om10l = lo16(wl.z); v.fRl = hi16(wl.z); v.fOl = lo16(wl.w);
+        v.wk = rp[(unsigned)(L.C + Uk) + L0];
+        v.wl = rp[(unsigned)(2 * L.C + Ul) + lh];
         return v;
     };
     auto step_b = [&](const BV &v, int mask) {
-        pRm00 = imin(pRm00, imin(v.wb_k + v.Rm00k, v.Rm00l + v.wb_l));  // :499-508
-        pRm10 = imin(pRm10, v.wbp_k + v.Rm00k);                         // :534-537
-        pRm01 = imin(pRm01, v.Rm00l + v.wbp_l);                         // :520-523
-        pMm00 = imin(pMm00, v.Mm00k + v.wb_k);                          // :552-555
-        pMm01 = imin(pMm01, v.Mm00l + v.wbp_l);                         // :567-570
-        pOm00 = imin(pOm00, v.Om00l + v.wb_l);                          // :603-606
-        pOm01 = imin(pOm01, v.Om00l + v.wbp_l);                         // :618-621
-        fR1 = imin(fR1, v.fRk + v.wp_k + mask);                    // PfromR(i,j,d,l) + WP(k,d-1)     :379-381
-        fMp = imin(fMp, v.PLRk + PB + v.wp_k + mask);         // PfromM'' (:663-679) + WP(k,d-1) :412-414
-        pK2 = imin(pK2, v.Kk + v.wp_k + mask);                     // PK(i,j,d,l) + WP(k,d-1)         :189-192
-        pMm10 = imin(pMm10, v.Mm10l + v.wb_l + mask);              // PMmloop10(i,j,k,d) + WB(d+1,l)  :585-588
-        pOm10 = imin(pOm10, v.Om10l + v.wb_l + mask);              // POmloop10(i,j,k,d) + WB(d+1,l)  :636-639
-        fR2 = imin(fR2, v.fRl + v.wp_l + mask);                    // PfromR(i,j,k,d) + WP(d+1,l)     :382-383
-        fO2 = imin(fO2, v.fOl + v.wp_l + mask);                    // PfromO(i,j,k,d) + WP(d+1,l)     :429-431
+        const int wbp_k = v.w2k.x, wp_k = v.w2k.y, wbp_l = v.w2l.x, wp_l = v.w2l.y;
+        const int wb_k = WBD(wbp_k, v.s), wb_l = WBD(wbp_l, v.s);
+        const int Rm00k = lo16(v.wk.x), Mm00k = hi16(v.wk.x), fRk = lo16(v.wk.y), PLRk = hi16(v.wk.y), Kk = lo16(v.wk.z);
+        const int Rm00l = lo16(v.wl.x), Mm00l = hi16(v.wl.x), Om00l = lo16(v.wl.y), Mm10l = hi16(v.wl.y);
+        const int Om10l = lo16(v.wl.z), fRl = hi16(v.wl.z), fOl = lo16(v.wl.w);
+        pRm00 = imin(pRm00, imin(wb_k + Rm00k, Rm00l + wb_l));  // :499-508
+        pRm10 = imin(pRm10, wbp_k + Rm00k);                     // :534-537
+        pRm01 = imin(pRm01, Rm00l + wbp_l);                     // :520-523
+        pMm00 = imin(pMm00, Mm00k + wb_k);                      // :552-555
+        pMm01 = imin(pMm01, Mm00l + wbp_l);                     // :567-570
+        pOm00 = imin(pOm00, Om00l + wb_l);                      // :603-606
+        pOm01 = imin(pOm01, Om00l + wbp_l);                     // :618-621
+        fR1 = imin(fR1, fRk + wp_k + mask);               // PfromR(i,j,d,l) + WP(k,d-1)     :379-381
+        fMp = imin(fMp, PLRk + PB + wp_k + mask);         // PfromM'' (:663-679) + WP(k,d-1) :412-414
+        pK2 = imin(pK2, Kk + wp_k + mask);                // PK(i,j,d,l) + WP(k,d-1)         :189-192
+        pMm10 = imin(pMm10, Mm10l + wb_l + mask);         // PMmloop10(i,j,k,d) + WB(d+1,l)  :585-588
+        pOm10 = imin(pOm10, Om10l + wb_l + mask);         // POmloop10(i,j,k,d) + WB(d+1,l)  :636-639
+        fR2 = imin(fR2, fRl + wp_l + mask);               // PfromR(i,j,k,d) + WP(d+1,l)     :382-383
+        fO2 = imin(fO2, fOl + wp_l + mask);               // PfromO(i,j,k,d) + WP(d+1,l)     :429-431
     };
     // b-leader: one scan of s = 1..b for this cell and its followers r = 1..R-1:
     //   k side: cell (i, j, k-r, l) (level t+r, block a, row h-r), term X(i,j,k+s,l) + W(k-r, k+s-1)
@@ -1537,9 +1568,10 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #pragma unroll
             for (int f = 0; f < 9; ++f) AL_[r][f] = INF;
         }
-        struct LB { uint4 wk, wl; wv_t qb, qbp, qp, pb, pbp, pp; };
+        struct LB { uint4 wk, wl; int2 q[SHARE_R], p[SHARE_R]; int s; };  // raw loads of one split step
         auto ld = [&](int s) {
             LB v;
+            v.s = s;
             const LvlDev L = LD[t - s];
             const int Uk = a * L.M + s * m + ((s * (s + 1)) >> 1);
             const int Ul = a * L.M;
@@ -1552,11 +1584,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
-                const int2 wq = WBW[o + k - r], wp2 = WBW[o + l - s + 1];
-                v.qbp[SHARE_R - 1 - r] = wq.x; v.qp[SHARE_R - 1 - r] = wq.y;
-                v.pbp[r] = wp2.x; v.pp[r] = wp2.y;
-                v.qb[SHARE_R - 1 - r] = WBD(v.qbp[SHARE_R - 1 - r], s + r, o + k - r);
-                v.pb[r] = WBD(v.pbp[r], s + r, o + l - s + 1);
+                v.q[r] = WBW[o + k - r];
+                v.p[r] = WBW[o + l - s + 1];
             }
             return v;
         };
@@ -1567,8 +1596,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             const int Om10l = lo16(v.wl.z), fRl = hi16(v.wl.z), fOl = lo16(v.wl.w);
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
-                const int wbk = v.qb[SHARE_R - 1 - r], wbpk = v.qbp[SHARE_R - 1 - r], wpk = v.qp[SHARE_R - 1 - r];
-                const int wbl = v.pb[r], wbpl = v.pbp[r], wpl_ = v.pp[r];
+                const int wbpk = v.q[r].x, wpk = v.q[r].y, wbk = WBD(wbpk, v.s + r);
+                const int wbpl = v.p[r].x, wpl_ = v.p[r].y, wbl = WBD(wbpl, v.s + r);
                 int *K = AK_[r], *Q = AL_[r];
                 K[0] = imin(K[0], wbk + Rm00k);             // PRmloop00 :499-508
                 K[1] = imin(K[1], wbpk + Rm00k);            // PRmloop10 :534-537
@@ -1587,18 +1616,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 Q[8] = imin(Q[8], fOl + wpl_ + mask);       // PfromO    :429-431
             }
         };
-        if (s_first + part <= b) {
-            int s = s_first + part;
-            LB cur = ld(s);
-            for (;;) {
-                const int sn = s + split;
-                const LB nxt = ld(imin(sn, b));
-                st(cur, s < b ? 0 : INF);
-                if (sn > b) break;
-                cur = nxt;
-                s = sn;
-            }
-        }
+        if (s_first + part <= b) PIPE_SCAN_LEAD<LB>(s_first + part, split, b, b, ld, st);
         const int r0 = prem ? 0 : 1;
         if (split > 1) {
             int *slot = red + (wib / split) * (split - 1) * LEAD_RED * 64 + lane;
@@ -1672,16 +1690,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     if (brole == 1 && LEAD) {
         lead_b();
     } else if (s_first + part <= b_stop) {
-        int s = s_first + part;
-        BV cur = load_b(s);
-        for (;;) {
-            const int sn = s + split;
-            const BV nxt = load_b(imin(sn, b_stop));
-            step_b(cur, s < b ? 0 : INF);
-            if (sn > b_stop) break;
-            cur = nxt;
-            s = sn;
-        }
+        PIPE_SCAN<BV>(s_first + part, split, b_stop, b, load_b, step_b);
     }
     if (prem ? !LEAD : brole == 2) {  // the b-loop's ring record (as for the a-loop)
         const uint4 *ring = T.acc + (long long)((t % SHARE_SLOTS) * SHARE_NACC) * T.accC;
