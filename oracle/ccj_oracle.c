@@ -24,6 +24,9 @@
 #include <string.h>
 #include <stdio.h>
 #include "ccj_params.h"
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define INF CCJ_INF
 #define TURN CCJ_TURN
@@ -44,10 +47,15 @@ typedef struct oracle {
     /* 2-D: dense (n+2)*(n+2) */
     int *V; char *Vt; int *WM, *WMv, *WMp, *Pm, *WBP, *WPP;
     int *W;
-    /* 4-D: reference-style 3-D offset table + l-k */
-    size_t *idx3;
+    /* 4-D: the reference's offsets (Matrix4D::construct_index, matrices.hh:208-221), held as a
+       2-D (i,j) base table plus the closed form of its inner k sum, + l-k */
+    size_t *idx2;
     size_t slice;
     int16_t *M4[NMAT4];
+    /* memo of get_e_intP (pseudo_loop.cc:827-840) over every pseudoknot interior-loop window:
+       eint[(p*(n+2)+q)*29*29 + u1*29 + u2] = lrint(e_intP * E_IntLoop) for the outer pair (p,q)
+       and the inner pair (p+1+u1, q-1-u2); the same value the reference recomputes per candidate */
+    int *eint;
 } oracle;
 
 /* matrix ids, reference allocate_space order (pseudo_loop.cc:37-62) */
@@ -180,8 +188,9 @@ static inline int tri_get(const oracle *o, const int *m, int i, int j) { /* matr
 }
 
 static inline size_t idx4(const oracle *o, int i, int j, int k, int l) { /* matrices.hh:229-231 */
-    size_t n = (size_t)o->n;
-    return o->idx3[(size_t)(i - 1) * n * n + (size_t)(j - 1) * n + (size_t)(k - 1)] + (size_t)(l - k);
+    /* construct_index adds (n - k') for k' = j..k-1 (0-based) to the (i,j) base */
+    size_t n = (size_t)o->n, dk = (size_t)(k - j);
+    return o->idx2[(size_t)(i - 1) * n + (size_t)(j - 1)] + dk * n - dk * (size_t)(k + j - 3) / 2 + (size_t)(l - k);
 }
 static inline int get4(const oracle *o, int m, int i, int j, int k, int l) { /* matrices.hh:177-182 */
     if (!(i <= j && j < k - 1 && k <= l)) return INF;
@@ -218,9 +227,14 @@ static int get_e_stP(const oracle *o, int i, int j) {
     int ss = compute_int(o, i, j, i + 1, j - 1);
     return (int)lrint(o->pen.e_stP * ss);
 }
-static int get_e_intP(const oracle *o, int i, int ip, int jp, int j) {
+static int get_e_intP_direct(const oracle *o, int i, int ip, int jp, int j) {
     int e = compute_int(o, i, j, ip, jp);
     return (int)lrint(o->pen.e_intP * e);
+}
+enum { EW = MAXLOOP - 1 };  /* u1, u2 <= 28 in every iloop window of pseudo_loop.cc:682-808 */
+static inline int get_e_intP(const oracle *o, int i, int ip, int jp, int j) {
+    return o->eint[((size_t)i * (size_t)(o->n + 2) + (size_t)j) * EW * EW + (size_t)(ip - i - 1) * EW +
+                   (size_t)(j - jp - 1)];
 }
 
 /* ---- s_energy_matrix.cc ---- */
@@ -671,7 +685,7 @@ static int E_ext_Stem(const oracle *o, int vij, int vi1j, int vij1, int vi1j1, i
 /* ------------------------------------------------------------------------------------------ */
 void ccj_oracle_free(oracle *o);
 
-oracle *ccj_oracle_fold(const char *seq, const ccj_energy_params *P, int dangles, int noGU) {
+static oracle *oracle_alloc(const char *seq, const ccj_energy_params *P, int dangles, int noGU) {
     oracle *o = (oracle *)calloc(1, sizeof(oracle));
     int n = (int)strlen(seq);
     o->n = n;
@@ -713,35 +727,39 @@ oracle *ccj_oracle_fold(const char *seq, const ccj_energy_params *P, int dangles
 
     /* Matrix4D::construct_index, matrices.hh:208-221 */
     if (n >= 1) {
-        o->idx3 = (size_t *)malloc((size_t)n * n * n * sizeof(size_t));
-        size_t idx = 0, nn = (size_t)n * n;
+        o->idx2 = (size_t *)malloc((size_t)n * n * sizeof(size_t));
+        size_t idx = 0;
         for (int i = 0; i < n; ++i)
-            for (int j = i; j < n; ++j)
-                for (int k = j; k < n; ++k) {
-                    o->idx3[(size_t)i * nn + (size_t)j * n + k] = idx;
-                    idx += (size_t)(n - k);
-                }
+            for (int j = i; j < n; ++j) {
+                o->idx2[(size_t)i * n + (size_t)j] = idx;
+                for (int k = j; k < n; ++k) idx += (size_t)(n - k);
+            }
         o->slice = idx;
+        o->eint = (int *)malloc((size_t)(n + 2) * (size_t)(n + 2) * EW * EW * sizeof(int));
+        if (!o->eint) { ccj_oracle_free(o); return NULL; }
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int p = 1; p <= n; ++p)
+            for (int q = p + 1; q <= n; ++q)
+                for (int u1 = 0; u1 < EW; ++u1)
+                    for (int u2 = 0; u2 < EW; ++u2) {
+                        int ip = p + 1 + u1, jp = q - 1 - u2;
+                        o->eint[((size_t)p * (size_t)(n + 2) + (size_t)q) * EW * EW + (size_t)u1 * EW + (size_t)u2] =
+                            ip < jp ? get_e_intP_direct(o, p, ip, jp, q) : INF;
+                    }
         for (int m = 0; m < NMAT4; ++m) {
             o->M4[m] = (int16_t *)malloc(o->slice * sizeof(int16_t));
             if (!o->M4[m]) { ccj_oracle_free(o); return NULL; }
+#pragma omp parallel for schedule(static)
             for (size_t x = 0; x < o->slice; ++x) o->M4[m][x] = INTERN_INF;
         }
     }
 
-    /* fill, W_final.cc:60-67 and pseudo_loop.cc:69-132 */
-    for (int i = n; i >= 1; --i)
-        for (int l = i; l <= n; ++l) {
-            compute_V(o, i, l);
-            compute_P(o, i, l);
-            compute_WBP(o, i, l);
-            compute_WPP(o, i, l);
-            for (int j = i; j < l; ++j)
-                for (int k = l; k >= j + 2; --k) compute_cell(o, i, j, k, l);
-            compute_WMv_WMp(o, i, l, tri_get(o, o->Pm, i, l));
-            compute_energy_WM(o, i, l);
-        }
+    return o;
+}
+
+static void oracle_exterior(oracle *o) {
     /* exterior, W_final.cc:68-77 */
+    int n = o->n;
     for (int j = TURN + 1; j <= n; ++j) {
         int m1 = o->W[j - 1], m2 = INF, m3 = INF;
         for (int k = 1; k <= j - TURN - 1; ++k) {
@@ -755,6 +773,84 @@ oracle *ccj_oracle_fold(const char *seq, const ccj_energy_params *P, int dangles
         }
         o->W[j] = MIN2(MIN2(m1, m2), m3);
     }
+}
+
+
+oracle *ccj_oracle_fold(const char *seq, const ccj_energy_params *P, int dangles, int noGU) {
+    oracle *o = oracle_alloc(seq, P, dangles, noGU);
+    if (!o) return NULL;
+    int n = o->n;
+    /* fill, W_final.cc:60-67 and pseudo_loop.cc:69-132 */
+    for (int i = n; i >= 1; --i)
+        for (int l = i; l <= n; ++l) {
+            compute_V(o, i, l);
+            compute_P(o, i, l);
+            compute_WBP(o, i, l);
+            compute_WPP(o, i, l);
+            for (int j = i; j < l; ++j)
+                for (int k = l; k >= j + 2; --k) compute_cell(o, i, j, k, l);
+            compute_WMv_WMp(o, i, l, tri_get(o, o->Pm, i, l));
+            compute_energy_WM(o, i, l);
+        }
+    oracle_exterior(o);
+    return o;
+}
+
+/*
+ * Level-parallel restatement of the same fill, for the sizes the
+ * sequential loop cannot reach in a test budget (config 5, n=400).  Write a cell as (i,j,k,l),
+ * a = j-i, b = l-k, level t = a+b.  Every 4-D read of the reference recurrences
+ * (pseudo_loop.cc:181-820) other than the same cell targets a level < t; every 2-D value a level-t
+ * cell reads has span <= t-1; a 2-D interval of span s (s_energy_matrix.cc:206-358,
+ * pseudo_loop.cc:134-179) reads only 4-D levels <= s-3, 2-D spans < s and, for WBP/WPP/WMv/WM, the
+ * V/P of its own interval, which the reference computes first (W_final.cc:60-67).  So
+ *     for t = 0..n:  all intervals of span t-1 (each in the reference's per-interval order),
+ *                    then all cells of level t (each in compute_cell's in-cell order)
+ * reads exactly the values the reference's i-descending / l-ascending loop reads; the intervals of
+ * one span and the cells of one level are independent and run on OpenMP threads.
+ * tests/test_oracle.py checks this mode against the reference's hashes and the sequential mode.
+ */
+static void fill_span(oracle *o, int s) {
+    int n = o->n;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int i = n - s; i >= 1; --i) {
+        int l = i + s;
+        compute_V(o, i, l);
+        compute_P(o, i, l);
+        compute_WBP(o, i, l);
+        compute_WPP(o, i, l);
+        compute_WMv_WMp(o, i, l, tri_get(o, o->Pm, i, l));
+        compute_energy_WM(o, i, l);
+    }
+}
+
+static void fill_level(oracle *o, int t) {
+    int n = o->n;
+    long rows = (long)n * (t + 1);  /* (i, a) pairs */
+#pragma omp parallel for schedule(dynamic, 4)
+    for (long x = 0; x < rows; ++x) {
+        int i = (int)(x / (t + 1)) + 1, a = (int)(x % (t + 1)), b = t - a;
+        int j = i + a;
+        for (int k = j + 2; k + b <= n; ++k) compute_cell(o, i, j, k, k + b);
+    }
+}
+
+oracle *ccj_oracle_fold_par(const char *seq, const ccj_energy_params *P, int dangles, int noGU, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
+    oracle *o = oracle_alloc(seq, P, dangles, noGU);
+    if (!o) return NULL;
+    int n = o->n;
+    int progress = getenv("CCJ_ORACLE_PROGRESS") != NULL;
+    for (int t = 0; t <= n; ++t) {
+        if (t >= 1) fill_span(o, t - 1);
+        if (t <= n - 3) fill_level(o, t);
+        if (progress && t % 10 == 0) { fprintf(stderr, "oracle level %d/%d\n", t, n); fflush(stderr); }
+    }
+    oracle_exterior(o);
     return o;
 }
 
@@ -762,7 +858,7 @@ void ccj_oracle_free(oracle *o) {
     if (!o) return;
     free(o->seq); free(o->S); free(o->S1);
     free(o->V); free(o->Vt); free(o->WM); free(o->WMv); free(o->WMp);
-    free(o->Pm); free(o->WBP); free(o->WPP); free(o->W); free(o->idx3);
+    free(o->Pm); free(o->WBP); free(o->WPP); free(o->W); free(o->idx2); free(o->eint);
     for (int m = 0; m < NMAT4; ++m) free(o->M4[m]);
     free(o);
 }
@@ -798,6 +894,7 @@ static uint64_t fnv(uint64_t h, const void *p, size_t n) {
 /* 22 + 8 + 1 hashes in ref_driver order: 4-D matrices, P WBP WPP V Vtype WM WMv WMp, W */
 void ccj_oracle_hashes(const oracle *o, uint64_t *out) {
     int n = o->n;
+#pragma omp parallel for schedule(dynamic, 1)
     for (int m = 0; m < NMAT4; ++m) {
         uint64_t h = 1469598103934665603ull;
         for (int i = 1; i <= n; ++i)

@@ -29,8 +29,11 @@ def oracle_lib():
         L = ctypes.CDLL(ORACLE_SO)
         L.ccj_oracle_fold.restype = ctypes.c_void_p
         L.ccj_oracle_fold.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        L.ccj_oracle_fold_par.restype = ctypes.c_void_p
+        L.ccj_oracle_fold_par.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.ccj_oracle_hashes.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
         L.ccj_oracle_free.argtypes = [ctypes.c_void_p]
+        L.ccj_oracle_W.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.ccj_oracle_get4.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5
         L.ccj_oracle_get4.restype = ctypes.c_int
         L.ccj_oracle_get2.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3
@@ -44,11 +47,16 @@ def oracle_lib():
 class OracleFold:
     """CPU restatement of the fill for one sequence (reference loop order)."""
 
-    def __init__(self, seq, blob: bytes, dangles=2, noGU=0):
+    def __init__(self, seq, blob: bytes, dangles=2, noGU=0, threads=None):
+        """threads=None: the sequential fill in the reference's own loop order; threads=k (0: all
+        cores): the level-parallel restatement (ccj_oracle_fold_par, OpenMP)."""
         L = oracle_lib()
         self._blob = ctypes.create_string_buffer(blob, len(blob))
         self.n = len(seq)
-        self.h = L.ccj_oracle_fold(seq.encode(), self._blob, dangles, noGU)
+        if threads is None:
+            self.h = L.ccj_oracle_fold(seq.encode(), self._blob, dangles, noGU)
+        else:
+            self.h = L.ccj_oracle_fold_par(seq.encode(), self._blob, dangles, noGU, threads)
         if not self.h:
             raise MemoryError("oracle allocation failed")
 

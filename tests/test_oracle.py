@@ -34,3 +34,29 @@ def test_golden_coverage():
     trna = [c for c in e2e if c["seq"] == "GCGGAUUUAGCUCAGUUGGGAGAGCGCCAGAC" and c["params"] == "Turner04"
             and c["dangles"] == 2 and not c["noGU"]]
     assert trna and trna[0]["stdout"].splitlines()[-1] == ".........((((..[[[[..)))).]]]].. (-8.54)"
+
+
+@pytest.mark.parametrize("case", CASES[::7], ids=lambda c: f"n{len(c['seq'])}-{c['params']}-d{c['dangles']}-g{c['noGU']}")
+def test_level_parallel_oracle_matches_reference(case):
+    """The level-parallel restatement (ccj_oracle_fold_par: spans and levels in the wavefront order
+    of SURVEY.md F4, OpenMP threads) reproduces the reference's matrices exactly."""
+    o = OracleFold(case["seq"], blob(case["params"]), case["dangles"], case["noGU"], threads=4)
+    try:
+        got = o.hashes()
+        bad = [k for k in case["hashes"] if got[k] != case["hashes"][k]]
+        assert not bad, f"matrices differ from reference: {bad}"
+        assert o.W(len(case["seq"])) == case["mfe"]
+    finally:
+        o.close()
+
+
+def test_level_parallel_oracle_matches_reference_n100():
+    """n=100 (BASELINE config 2's sequence): the parallel restatement against the reference's 31 hashes."""
+    case = [c for c in golden("hashes_large.json") if c["tag"] == "t04_100"][0]
+    o = OracleFold(case["seq"], blob(case["params"]), 2, 0, threads=0)
+    try:
+        got = o.hashes()
+        assert got == case["hashes"]
+        assert o.W(100) == case["mfe"]
+    finally:
+        o.close()
