@@ -1420,6 +1420,11 @@ static int local_allgather(ccj_ctx *c, size_t slice) {
     ccj_group *g = c->lgroup;
     HIPCHK(c, hipStreamSynchronize(c->st));  // own slice packed
     if (!g->barrier()) return set_err(c, CCJ_E_STATE, "local exchange: a group member failed");
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        for (int r = 0; r < g->world; ++r)
+            if (!g->members[r]) return set_err(c, CCJ_E_STATE, "local exchange: rank %d has no context", r);
+    }
     for (int r = 0; r < g->world; ++r)
         HIPCHK(c, hipMemcpyAsync(c->d_recv + (size_t)r * slice, g->members[r]->d_send, slice * sizeof(int16_t),
                                  hipMemcpyDeviceToDevice, c->st));
@@ -1496,9 +1501,12 @@ static int seq_setup(ccj_ctx *c) {
         return e;
     };
     HIPCHK(cp, up(c->d_pt, pt.data(), plane));
-    // ---- k_iloop work items (one per wave): counted per (level, shard) on host threads (the same
-    // enumeration as the GPU builder, ccj_items.h; no device round trip, so a reset never waits
-    // for a fold running on the GPU), written by k_items on the GPU at the prefix offsets
+    // ---- k_iloop work items (one per wave), counted per (level, shard), then written by k_items
+    // on the GPU at the prefix offsets.  By default the count pass runs on the GPU too (k_items
+    // pass 0 on st) and the host WAITS for it (hipStreamSynchronize): the offsets are needed on
+    // the host to size the k_iloop launches, so ccj_reset blocks until the context's stream has
+    // run it.  CCJ_HOST_COUNT=1 counts on host threads instead (the same enumeration, ccj_items.h;
+    // slower, ~1.3 ms at n=200, but no device round trip).
     {
         if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
         const int G = c->world;
@@ -1654,12 +1662,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_d, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_pre, hipStreamNonBlocking));
     // The cross-stream events only order work on this device, so they are recorded without the
-    // default system-scope fence (hipEventDisableSystemFence: fill -0.65 ms at n=200);
-    // CCJ_EV_FENCE=0 restores it.  ev_start / ev_end, which the host waits on, keep it.
-    static const unsigned fence_fl = [] {
-        const char *e = getenv("CCJ_EV_FENCE");
-        return (e && atoi(e) == 0) ? 0u : (unsigned)hipEventDisableSystemFence;
-    }();
+    // default system-scope fence (hipEventDisableSystemFence: fill -0.65 ms at n=200).
+    // ev_start / ev_end, which the host waits on, keep it.
+    constexpr unsigned fence_fl = (unsigned)hipEventDisableSystemFence;
     const unsigned sync_fl = hipEventDisableTiming | fence_fl;
     c->pre_done.resize(n + 1);
     for (auto &e : c->pre_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
@@ -1693,12 +1698,12 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     if (c->share) {
         // from the first level that runs unsplit to the last level: the narrow early levels keep
         // their split loops (short scans); on the narrow late levels k_level4d_lead splits the long
-        // scans like the level heuristic would (ccjk_level4d_lead).  CCJ_SHARE_LATE=0 limits
-        // sharing to the unsplit middle levels (measured 0.6 ms slower at n=200).
+        // scans like the level heuristic would (ccjk_level4d_lead).  (Sharing on the unsplit middle
+        // levels only measured 0.6 ms slower at n=200.)
         g_lo = -1;
         for (int t = 0; t < c->nlev && g_lo < 0; ++t)
             if (ccjk_level_split(n, t, t + 1, c->split_target) == 1) g_lo = t;
-        if (g_lo < 0 || (getenv("CCJ_SHARE_LATE") && atoi(getenv("CCJ_SHARE_LATE")) == 0)) {
+        if (g_lo < 0) {
             g_hi = g_lo < 0 ? 0 : g_lo;
             for (int t = std::max(g_lo, 0); g_lo >= 0 && t < c->nlev; ++t)
                 if (ccjk_level_split(n, t, t + 1, c->split_target) == 1 && g_hi == t) g_hi = t + 1;
@@ -1708,7 +1713,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         }
         for (int t = g_lo; t < g_hi; ++t) accC = std::max<long long>(accC, c->lv_host[t].C);
     }
-    if (g_hi > g_lo && !(getenv("CCJ_LEAD_ORDER") && atoi(getenv("CCJ_LEAD_ORDER")) == 0)) {
+    if (g_hi > g_lo) {
         // the a-blocks k_level4d_lead runs on each sharing level (a leader or a full scan on either
         // side; the roles of level4d_body), ordered by scan cost, longest first, so the longest
         // waves do not start last.  A leader step costs about 2.5 plain steps.  One list per
@@ -1952,15 +1957,9 @@ extern "C" int ccj_reset(ccj_ctx *c, const char *seq) {
 // Enqueue the whole fill on the context's streams; it ends with ev_end on st, after which every
 // stream's work of the fill is complete (st waits for the last span, which waits for the last P,
 // and every level waited for its k_iloop / leader launches).
-// The P terms that complete P(lev+3): by default every term whose operands' highest level is lev
-// (k_ppush), or with CCJ_PTERM_PULL=1 the per-span pull form k_pterm(lev+3).
-static int pterm_launch(const ccj::DevTables *T, int lev, hipStream_t s) {
-    static const bool pull = [] {
-        const char *e = getenv("CCJ_PTERM_PULL");
-        return e && atoi(e) != 0;
-    }();
-    return pull ? ccjk_pterm(T, lev + 3, s) : ccjk_ppush(T, lev, s);
-}
+// The P terms that complete P(lev+3): every term whose operands' highest level is lev (k_ppush,
+// DESIGN.md §4).
+static int pterm_launch(const ccj::DevTables *T, int lev, hipStream_t s) { return ccjk_ppush(T, lev, s); }
 
 static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     if (!c) return CCJ_E_ARG;
@@ -2139,6 +2138,8 @@ static int fill_finish(ccj_ctx *c) {
 }
 
 extern "C" int ccj_fill_device(ccj_ctx *c) {
+    if (!c) return CCJ_E_ARG;
+    if (c->pending || c->res_pending) return set_err(c, CCJ_E_STATE, "ccj_fill_device: a fold is in flight (ccj_wait first)");
     if (const int rc = fill_enqueue(c)) return rc;
     return fill_finish(c);
 }
@@ -2645,6 +2646,8 @@ extern "C" void ccj_group_destroy(ccj_group *g) { delete g; }
 extern "C" int ccj_comm_init_local(ccj_ctx *c, ccj_group *g) {
     if (!c || !g || g->world != c->world || c->world < 2 || c->simulate) return CCJ_E_ARG;
     std::lock_guard<std::mutex> lk(g->mu);
+    if (g->members[c->rank] && g->members[c->rank] != c)
+        return set_err(c, CCJ_E_STATE, "ccj_comm_init_local: rank %d of the group is already taken", c->rank);
     g->members[c->rank] = c;
     c->lgroup = g;
     return CCJ_OK;
@@ -2655,6 +2658,11 @@ extern "C" const char *ccj_last_error(const ccj_ctx *c) { return c ? c->err.c_st
 
 extern "C" void ccj_destroy(ccj_ctx *c) {
     if (!c) return;
+    if (c->lgroup) {  // leave the in-process group: no member may copy from this context's buffers
+        std::lock_guard<std::mutex> lk(c->lgroup->mu);
+        if (c->lgroup->members[c->rank] == c) c->lgroup->members[c->rank] = nullptr;
+        c->lgroup = nullptr;
+    }
     hipSetDevice(c->device);
     if (c->st) hipStreamSynchronize(c->st);
     if (c->st_copy) hipStreamSynchronize(c->st_copy);

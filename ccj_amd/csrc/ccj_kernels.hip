@@ -256,8 +256,8 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
         }
     }
 
-    // ---- P(i,l) was reduced into T.P by k_pterm(sigma) (ordered before this kernel by an event)
-    if (tid == 0) {  // value half of k_pterm's (value, first split) minimum; never set -> INF+1
+    // ---- P(i,l) was reduced into T.Pk by k_ppush (ordered before this kernel by an event)
+    if (tid == 0) {  // value half of the (value, first split) minimum; never set -> INF+1
         const unsigned long long pk = T.Pk[cell];
         sh_p = pk == ~0ull ? INF + 1 : (int)((unsigned)(pk >> 32) - 0x80000000u);
         T.P[cell] = sh_p;
@@ -320,129 +320,20 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// P(i, i+sigma) = min over i<=j<d<k<l of PK(i,j,d+1,k) + PK(j+1,d,k+1,l)   (pseudo_loop.cc:166-179)
-// One wave = (jo = j-i, do = d-i, a group of 64 consecutive intervals i), looping over k: for fixed
-// offsets the two PK cells of neighbouring intervals are neighbours in HBM, so every load is
-// coalesced.  Each lane keeps its first minimum in the reference's loop order as one 64-bit key,
-// (P + 2^31) << 32 | (j-i, d-i, k-i) split, the 4 waves of a workgroup (4 consecutive do)
-// min-reduce it in LDS, and one 64-bit atomicMin per interval lands in T.Pk (initialised all-ones
-// = "never set"; every candidate is <= 65534 < INF/2, A-Q4).  k_diag2d(sigma) takes P from it and
-// the P_P traceback its split (pseudo_loop.cc:867-896), without a rescan.  Needs PK levels
-// <= sigma-3 only, so it runs on a side stream three levels ahead of k_diag2d(sigma).
-// ------------------------------------------------------------------------------------------
+// readlane of a 64-bit value (two 32-bit readlanes)
 __device__ __forceinline__ unsigned long long rdl64(unsigned long long v, int l) {
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
     return ((unsigned long long)hi << 32) | lo;
 }
 
-constexpr int PT_WAVES = 4;  // waves per k_pterm workgroup = consecutive do values sharing jo
-
-// Grid: one workgroup per (jo, ddc, grp), linear id L = jo*gx + ddc*ngroups + grp.  With xcd = C > 0
-// (CCJ_PTERM_XCD) the dispatch order is remapped so that each XCD (workgroups are dealt round-robin
-// to the 8 XCDs) runs runs of C consecutive L: workgroups of one jo and neighbouring ddc / grp,
-// which read neighbouring rows and straddle the same 128-B lines, share one L2.
-__global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngroups, int gx, int total, int xcd) {
-    __shared__ unsigned long long red[PT_WAVES][64];
-    const int n = T.n;
-    const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
-    int L = (int)blockIdx.x;
-    if (xcd) {  // runs of xcd consecutive workgroups per XCD, runs interleaved over the XCDs
-        const int q = L >> 3;
-        L = ((q / xcd) * 8 + (L & 7)) * xcd + q % xcd;
-    }
-    if (L >= total) return;  // whole workgroup
-    const int jo = L / gx;
-    const int bx = L - jo * gx;
-    const int ddc = bx / ngroups;
-    const int grp = bx - ddc * ngroups;
-    const int dd0 = jo + 1 + ddc * PT_WAVES;
-    if (dd0 > sigma - 2) return;  // whole workgroup
-    const int dd = dd0 + w;
-    const int i0_ = grp * 64 + lane + 1;
-    const int i = i0_;
-    // (value, key) of the first minimum in the reference's loop order, key = (jo*sigma + do)*sigma + ko
-    unsigned long long best = ~0ull;
-    // wave-uniform guard only: the readlane tables below need every lane; lanes past the last
-    // interval re-read the last one and drop their result
-    if (dd <= sigma - 2) {
-        // PK(i, j, d+1, k): level jo+(ko-dd-1), a = jo, h = dd-jo-1, interval start i
-        // PK(j+1, d, k+1, l): level (dd-jo-1)+(sigma-ko-1), a = dd-jo-1, h = ko-dd-1, start i+jo+1
-        const int a1 = jo, h1 = dd - jo - 1, a2 = dd - jo - 1;
-        const int g1 = (h1 * (h1 - 1)) >> 1;
-        const int16_t *__restrict__ D4 = T.d4;
-        const LvlDev *__restrict__ LD = T.ld;
-        const unsigned kbase = ((unsigned)jo * (unsigned)sigma + (unsigned)dd) * (unsigned)sigma;
-        int bv = INF + 1, bk = 0;
-#ifdef CCJ_PTERM_SLOAD
-        const int i = imin(i0_, n - sigma);
-#pragma unroll 4
-        for (int ko = dd + 1; ko < sigma; ++ko) {
-            const int h2 = ko - dd - 1;
-            const int t1 = a1 + h2, t2 = a2 + (sigma - ko - 1);
-            const LvlDev L1 = LD[t1], L2 = LD[t2];
-            const int o1 = PK * L1.C + a1 * L1.M + h1 * (n - t1 - 2) - g1 - 1;
-            const int o2 = PK * L2.C + a2 * L2.M + h2 * (n - t2 - 2) - ((h2 * (h2 - 1)) >> 1) + jo;
-            const int v = (int)(D4 + L1.lb + o1)[i] + (int)(D4 + L2.lb + o2)[i];
-            if (v < bv) {  // strict: keeps the first ko of the minimum
-                bv = v;
-                bk = ko;
-            }
-        }
-#else
-        // the row bases of both operands for 64 consecutive ko at a time, one per lane, fetched
-        // with readlane in the loop: no scalar descriptor load on the load chain
-        const unsigned ioff = 2u * (unsigned)imin(i, n - sigma);
-        for (int kb = dd + 1; kb < sigma; kb += 64) {
-            const int kl = imin(kb + lane, sigma - 1);
-            const int h2 = kl - dd - 1;
-            const int t1 = a1 + h2, t2 = a2 + (sigma - kl - 1);
-            const LvlDev L1 = LD[t1], L2 = LD[t2];
-            const long long o1 = L1.lb + PK * (long long)L1.C + a1 * L1.M + h1 * (n - t1 - 2) - g1 - 1;
-            const long long o2 = L2.lb + PK * (long long)L2.C + a2 * L2.M + h2 * (n - t2 - 2) - ((h2 * (h2 - 1)) >> 1) + jo;
-            const unsigned long long p1 = (unsigned long long)(D4 + o1), p2 = (unsigned long long)(D4 + o2);
-            const int cnt = imin(64, sigma - kb);
-            // 8 terms per batch: all 16 loads in flight before the first compare (entries past cnt
-            // re-read lane cnt-1's rows and are masked)
-            for (int x0 = 0; x0 < cnt; x0 += 8) {
-                int v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int x = imin(x0 + u, cnt - 1);
-                    const char *q1 = (const char *)rdl64(p1, x) + ioff, *q2 = (const char *)rdl64(p2, x) + ioff;
-                    v[u] = (int)*(const __attribute__((address_space(1))) int16_t *)q1 +
-                           (int)*(const __attribute__((address_space(1))) int16_t *)q2;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (x0 + u < cnt && v[u] < bv) {  // strict: keeps the first ko of the minimum
-                        bv = v[u];
-                        bk = kb + x0 + u;
-                    }
-            }
-        }
-#endif
-        if (bv <= INF && i0_ + sigma <= n) best = ((unsigned long long)((unsigned)bv + 0x80000000u) << 32) | (kbase + (unsigned)bk);
-    }
-    red[w][lane] = best;
-    __syncthreads();
-    if (w == 0 && i + sigma <= n) {
-        unsigned long long v = red[0][lane];
-        for (int x = 1; x < PT_WAVES; ++x) v = red[x][lane] < v ? red[x][lane] : v;
-        if (v != ~0ull) atomicMin(T.Pk + sigma * T.rs + i, v);
-    }
-}
-
 // ------------------------------------------------------------------------------------------
-// P terms pushed by level (the default; k_pterm above is the per-span pull form, CCJ_PTERM_PULL=1).
-// A term of P(i, i+sigma) reads A = PK(i,j,d+1,k) at level t1 = jo+(ko-do-1) and
+// P(i, i+sigma) = min over i<=j<d<k<l of PK(i,j,d+1,k) + PK(j+1,d,k+1,l)   (pseudo_loop.cc:166-179),
+// pushed by level.  A term of P(i, i+sigma) reads A = PK(i,j,d+1,k) at level t1 = jo+(ko-do-1) and
 // B = PK(j+1,d,k+1,l) at level t2 = (do-jo-1)+(sigma-ko-1), with t1 + t2 = sigma-3 (offsets
 // jo = j-i, do = d-i, ko = k-i).  k_ppush(T), enqueued after level T, evaluates every term with
-// max(t1, t2) = T: part A t1 = T (t2 <= T), part B t2 = T (t1 < T).  That completes P(T+3), exactly
-// what the pull launch k_pterm(T+3) did at the same point of the schedule, and leaves partial
-// minima of P(sigma > T+3) in T.Pk.  The gain: the level-T operand of a term is the same cell for
+// max(t1, t2) = T: part A t1 = T (t2 <= T), part B t2 = T (t1 < T).  That completes P(T+3) (the
+// last span whose terms all sit at levels <= T) and leaves partial minima of P(sigma > T+3) in T.Pk.  The gain: the level-T operand of a term is the same cell for
 // PP_S consecutive spans, so a wave loads it once and pairs it with PP_S partners (1 + 1/PP_S loads
 // per term instead of 2), and it is the level just written (L2 / MALL resident).
 //   part A wave: (jo, 64 consecutive i, PP_S consecutive t2), loop h1 = do-jo-1 ascending:
@@ -452,7 +343,10 @@ __global__ __launch_bounds__(256) void k_pterm(DevTables T, int sigma, int ngrou
 //       B = level T, block a2, row h2, position l-h2-T-2            (once per h2)
 //       A = level t1, block t1-h2, row a2, position l-T-3-t1 = i    (per t1, valid while h2 <= t1)
 // Both loops visit the terms of one output in ascending (jo, do, ko) order, so a strict < keeps the
-// reference's first minimum within a wave; across waves the 64-bit key atomicMin does (k_pterm).
+// reference's first minimum within a wave; across waves a 64-bit atomicMin on
+// (P + 2^31) << 32 | (j-i, d-i, k-i) key keeps it: T.Pk starts all-ones ("never set"; every
+// candidate is <= 65534 < INF/2, A-Q4), k_diag2d(sigma) takes P from it and the P_P traceback
+// (pseudo_loop.cc:867-896) its first split, without a rescan.
 // ------------------------------------------------------------------------------------------
 
 __device__ __forceinline__ const int16_t *pk_row(const DevTables &T, int t, int a, int h) {
@@ -828,7 +722,7 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
                 // get_PMiloop: d > i, dp < l.  Branch-free (a select of constants): a branch here
                 // splits the loop body, and the compiler then sign-extends the next batch's loads
                 // in the latch, draining every load before the back-edge
-                b1 = imin(b1, c + ((u1 > as - 2) | (u2 > bs - 2) ? INF : 0));
+                b1 = imin(b1, c + (((u1 > as - 2) | (u2 > bs - 2)) ? INF : 0));
             } else {
                 b1 = imin(b1, c);
             }
@@ -921,7 +815,7 @@ __device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__rest
             const int c = il_e(E[u]) + v[u];
             if (PMWIN) {
                 const int u1 = il_u1(E[u]), u2 = il_dt(E[u]) - 2 - u1;
-                b1 = imin(b1, c + ((u1 > as - 2) | (u2 > bs - 2) ? INF : 0));
+                b1 = imin(b1, c + (((u1 > as - 2) | (u2 > bs - 2)) ? INF : 0));
             } else {
                 b1 = imin(b1, c);
             }
@@ -966,11 +860,7 @@ __device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__rest
 // walk).  (Groups of exactly nact lanes, W not a power of two, measured the same.)
 struct ILGroups { int G, W, gq, rl; };
 __device__ __forceinline__ ILGroups il_groups(int nact, int lane) {
-#ifdef CCJ_IL_NOPACK
-    const int W = 64;
-#else
     const int W = nact > 32 ? 64 : nact > 16 ? 32 : nact > 8 ? 16 : 8;
-#endif
     return {64 / W, W, lane / W, lane & (W - 1)};
 }
 
@@ -1152,11 +1042,10 @@ __device__ __forceinline__ void pipe_scan(int s, int step, int last, int mlim, L
         s = sn;
     }
 }
-// The one-buffer loop shape (`cur = nxt`).  The leaders' loops keep it: their ping-pong form
-// needs 241 VGPRs instead of ~150 (2 waves/SIMD) and measured fill +5 ms; CCJ_PIPE_LEAD_NEW builds
-// it, CCJ_PIPE_OLD uses the one-buffer shape for every split loop (fill +0.6 ms).
+// The one-buffer loop shape (`cur = nxt`), kept for the leaders' loops: their ping-pong form needs
+// 241 VGPRs instead of ~150 (2 waves/SIMD) and measured fill +5 ms.
 template <class V, class LD, class ST>
-__device__ __forceinline__ void pipe_scan_old(int s, int step, int last, int mlim, LD ld, ST st) {
+__device__ __forceinline__ void pipe_scan_lead(int s, int step, int last, int mlim, LD ld, ST st) {
     V cur = ld(s);
     for (;;) {
         const int sn = s + step;
@@ -1167,16 +1056,6 @@ __device__ __forceinline__ void pipe_scan_old(int s, int step, int last, int mli
         s = sn;
     }
 }
-#ifdef CCJ_PIPE_OLD
-#define PIPE_SCAN pipe_scan_old
-#define PIPE_SCAN_LEAD pipe_scan_old
-#elif defined(CCJ_PIPE_LEAD_NEW)
-#define PIPE_SCAN pipe_scan
-#define PIPE_SCAN_LEAD pipe_scan
-#else
-#define PIPE_SCAN pipe_scan
-#define PIPE_SCAN_LEAD pipe_scan_old
-#endif
 
 // ------------------------------------------------------------------------------------------
 // 4-D level t: one lane per cell (i,j,k,l); all lanes of a wave share (t, a) so every loop bound
@@ -1204,13 +1083,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     // (step s = part + 1, part + 1 + split, ...) and min-reduce their partial results through LDS.
     extern __shared__ int red[];  // [chunk][part-1][22][64], split > 1 only
     const int n = T.n, rs = T.rs;
-    int bid = blockIdx.x;
-#ifdef CCJ_XCD_MAP
-    {   // workgroups are dealt round-robin to the 8 XCDs: give each XCD a contiguous run of blocks
-        const int nb = gridDim.x, x = bid & 7, q = bid >> 3, per = nb >> 3, rem = nb & 7;
-        bid = x * per + imin(x, rem) + q;
-    }
-#endif
+    const int bid = blockIdx.x;
     const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int part = wib % split;
     const int cpb = (int)(blockDim.x >> 6) / split;  // chunks per block
@@ -1412,7 +1285,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 J[6] = imin(J[6], Kj + wpj + mask);      // PK        :184-187
             }
         };
-        if (s_first + part <= a) PIPE_SCAN_LEAD<LA>(s_first + part, split, a, a, ld, st);
+        if (s_first + part <= a) pipe_scan_lead<LA>(s_first + part, split, a, a, ld, st);
         // slices handed over through the ring: the followers' (r >= 1), and in the prepass scheme
         // the cell's own (r = 0) too; otherwise r = 0 stays in this wave's accumulators
         const int r0 = prem ? 0 : 1;
@@ -1482,7 +1355,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     if (arole == 1 && LEAD) {
         lead_a();
     } else if (s_first + part <= a_stop) {
-        PIPE_SCAN<AV>(s_first + part, split, a_stop, a, load_a, step_a);
+        pipe_scan<AV>(s_first + part, split, a_stop, a, load_a, step_a);
     }
     // the ring record of the a-loop: a follower's leader partial (split points a%R+1 .. a, or
     // a%R+2 .. a in the prepass scheme), and in the prepass scheme the own s >= 2 partial of a
@@ -1616,7 +1489,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 Q[8] = imin(Q[8], fOl + wpl_ + mask);       // PfromO    :429-431
             }
         };
-        if (s_first + part <= b) PIPE_SCAN_LEAD<LB>(s_first + part, split, b, b, ld, st);
+        if (s_first + part <= b) pipe_scan_lead<LB>(s_first + part, split, b, b, ld, st);
         const int r0 = prem ? 0 : 1;
         if (split > 1) {
             int *slot = red + (wib / split) * (split - 1) * LEAD_RED * 64 + lane;
@@ -1690,7 +1563,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     if (brole == 1 && LEAD) {
         lead_b();
     } else if (s_first + part <= b_stop) {
-        PIPE_SCAN<BV>(s_first + part, split, b_stop, b, load_b, step_b);
+        pipe_scan<BV>(s_first + part, split, b_stop, b, load_b, step_b);
     }
     if (prem ? !LEAD : brole == 2) {  // the b-loop's ring record (as for the a-loop)
         const uint4 *ring = T.acc + (long long)((t % SHARE_SLOTS) * SHARE_NACC) * T.accC;
@@ -1905,11 +1778,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 
 // The two launches of a level (ccjk_level4d / ccjk_level4d_lead): the plain cells (short scans)
 // and, on the split-sharing levels, the long-scan cells with their larger register budget.
-__global__ __launch_bounds__(512)
-#ifdef CCJ_WAVES_EU
-__attribute__((amdgpu_waves_per_eu(CCJ_WAVES_EU, CCJ_WAVES_EU)))
-#endif
-void k_level4d(DevTables T, int t, int wavesPerA, int split, int G, int rank, int nblk, int copies) {
+__global__ __launch_bounds__(512) void k_level4d(DevTables T, int t, int wavesPerA, int split, int G, int rank, int nblk, int copies) {
     level4d_body<false>(T, t, wavesPerA, split, G, rank, nblk, copies);
 }
 __global__ __launch_bounds__(512) void k_level4d_lead(DevTables T, int t, int wavesPerA, int split, int G, int rank, int nblk,
@@ -1938,26 +1807,6 @@ extern "C" int ccjk_diag2d(const DevTables *T, int sigma, void *stream) {
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_pterm(const DevTables *T, int sigma, void *stream) {
-#ifdef CCJ_ABLATE_PTERM
-    return 0;
-#endif
-    if (sigma < 3) return 0;
-    const int nint = T->n - sigma;
-    if (nint <= 0) return 0;
-    const int ngroups = (nint + 63) / 64;
-    const int nddc = (sigma - 2 + PT_WAVES - 1) / PT_WAVES;
-    static const int xcd = [] {
-        const char *e = getenv("CCJ_PTERM_XCD");
-        return e ? atoi(e) : 4;  // measured: 15% less traffic than plain dispatch order, same time
-    }();
-    const int gx = nddc * ngroups, total = gx * (sigma - 2);
-    const int blocks = xcd ? 8 * xcd * ((total + 8 * xcd - 1) / (8 * xcd)) : total;
-    hipLaunchKernelGGL(k_pterm, dim3((unsigned)blocks), dim3(64 * PT_WAVES), 0, (hipStream_t)stream, *T, sigma, ngroups, gx,
-                       total, xcd);
-    return (int)hipGetLastError();
-}
-
 // P terms of every span whose operands' highest level is lev (k_ppush); completes P(lev+3).
 extern "C" int ccjk_ppush(const DevTables *T, int lev, void *stream) {
 #ifdef CCJ_ABLATE_PTERM
@@ -1967,27 +1816,15 @@ extern "C" int ccjk_ppush(const DevTables *T, int lev, void *stream) {
     const int nmax = imin(lev, n - 4 - lev) + 1;  // t2 values of part A (part B has one fewer or equal)
     if (nmax <= 0) return 0;
     const int ngrp = (n - lev - 3 + 63) / 64;
-    static const int S = [] {  // spans per wave = partners per reused load (8; CCJ_PP_S=4 / 16)
-        const char *e = getenv("CCJ_PP_S");
-        return e && (atoi(e) == 16 || atoi(e) == 4) ? atoi(e) : 8;
-    }();
+    // spans per wave = partners per reused level-T load (8; 4 and 16 measured slower) and the
+    // inner-loop slice per wave (32; 16 and 64 measured the same)
+    constexpr int S = 8, hs_len = 32;
     const int nch = (nmax + S - 1) / S;
-    static const int hs_len = [] {
-        const char *e = getenv("CCJ_PP_HS");
-        return e && atoi(e) > 0 ? atoi(e) : 32;
-    }();
     int npairs = 0;  // (chunk, inner-loop slice) pairs, as k_ppush enumerates them
     for (int c = 0; c < nch; ++c) npairs += (imin((c + 1) * S, nmax) + hs_len - 1) / hs_len;
     const int blocksA = (npairs * ngrp * (lev + 1) + 3) / 4;
-    if (S == 4)
-        hipLaunchKernelGGL(k_ppush<4>, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp,
-                           npairs, hs_len, blocksA);
-    else if (S == 16)
-        hipLaunchKernelGGL(k_ppush<16>, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp,
-                           npairs, hs_len, blocksA);
-    else
-        hipLaunchKernelGGL(k_ppush<8>, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp,
-                           npairs, hs_len, blocksA);
+    hipLaunchKernelGGL(k_ppush<S>, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp, npairs,
+                       hs_len, blocksA);
     return (int)hipGetLastError();
 }
 
@@ -2166,11 +2003,7 @@ extern "C" int ccjk_level4d_lead(const DevTables *T, int t, int G, int rank, voi
     const long waves = (long)nblk * wavesPerA;
     // each leader chunk's scans are split over `split` waves of one workgroup (the barriers inside
     // the leader scans need every wave of the workgroup on the same chunk)
-    static const int lsplit = [] {
-        const char *e = getenv("CCJ_LEAD_SPLIT");
-        const int v = e ? atoi(e) : 2;
-        return v >= 1 && v <= 8 ? v : 2;
-    }();
+    constexpr int lsplit = 2;  // 1 / 3 / 4 measured +1.1 / +6.5 / +9.4 ms
     // narrow late levels: as many split waves as the plain heuristic would give the rank's blocks
     const int sp = imax(lsplit, ccjk_level_split(T->n, t, own, T->split_target));
     const size_t shmem = sp > 1 ? (size_t)(sp - 1) * (LEAD_RED > 22 ? LEAD_RED : 22) * 64 * sizeof(int) : 0;

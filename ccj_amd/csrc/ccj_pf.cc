@@ -450,6 +450,7 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
 int fill_impl(ccj_pf_ctx *c) {
     const int n = c->n;
     const size_t plane = c->plane();
+    c->filled = false;  // a failed re-fill must not leave the previous fill's tables looking valid
     PFCHK(c, hipSetDevice(c->device));
     PFCHK(c, hipMemsetAsync(c->d_2d, 0, (size_t)CCJ_PF_NMAT2 * plane * sizeof(double), c->st));
     PFCHK(c, hipMemsetAsync(c->d_Pacc, 0, plane * sizeof(long long), c->st));

@@ -92,14 +92,19 @@ int  ccj_create(const ccj_problem *prob, const ccj_options *opts, ccj_ctx **out)
  * options): rebuilds only the sequence tables and the interior-loop work lists and reuses every
  * allocation, so a batch of equal-length sequences pays ccj_create's multi-GB allocation once.
  * The reference has no equivalent (each fold constructs a new W_final, W_final.cc:20-56).
- * CCJ_E_ARG if the length differs or the sequence has characters other than ACGUT. */
+ * Blocking: the interior-loop work-list count pass runs on the context's stream and the call
+ * waits for it (the host sizes the fill's launches from the counts), so it returns only after
+ * the work already queued on that stream; with CCJ_HOST_COUNT=1 the count runs on host threads.
+ * CCJ_E_ARG if the length differs or the sequence has characters other than ACGUT; CCJ_E_STATE
+ * while a fold is in flight. */
 int  ccj_reset(ccj_ctx *ctx, const char *seq);
 
 /* Run the whole DP fill on the GPU (replaces W_final.cc:60-67), then make the host mirror
  * valid (ccj_sync_host is implied). */
 int  ccj_fill(ccj_ctx *ctx);
 
-/* Device-only fill, no host mirror (for timing the kernels alone). */
+/* Device-only fill, no host mirror (for timing the kernels alone).  CCJ_E_STATE while a fold
+ * is in flight (ccj_fill_async without ccj_wait). */
 int  ccj_fill_device(ccj_ctx *ctx);
 /* Copy the device matrices to the host mirror. */
 int  ccj_sync_host(ccj_ctx *ctx);

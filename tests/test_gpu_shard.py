@@ -89,13 +89,22 @@ def _fold_group(seq, params, world):
         except Exception as e:  # noqa: BLE001
             errs.append(repr(e))
 
-    th = [threading.Thread(target=run, args=(wf,)) for wf in ranks]
+    th = [threading.Thread(target=run, args=(wf,), daemon=True) for wf in ranks]
     for x in th:
         x.start()
     for x in th:
         x.join(timeout=300)
+    # a rank still inside ccj_fill owns its context: fail without closing anything it may touch
+    alive = [r for r, x in enumerate(th) if x.is_alive()]
+    assert not alive, f"ranks {alive} did not finish their fill within 300 s (contexts left open)"
     assert not errs, errs
     return g, ranks
+
+
+def _close_group(g, ranks):
+    for wf in ranks:
+        wf.close()
+    g.close()
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -112,9 +121,7 @@ def test_exchange_group_every_rank_holds_the_reference_fold(case, world):
             bad = [k for k in case["hashes"] if got[k] != case["hashes"][k]]
             assert not bad, f"rank {wf.rank if hasattr(wf, 'rank') else '?'}: {bad}"
     finally:
-        for wf in ranks:
-            wf.close()
-        g.close()
+        _close_group(g, ranks)
 
 
 def test_exchange_group_config4_dp09_200():
@@ -129,6 +136,4 @@ def test_exchange_group_config4_dp09_200():
         got = ranks[3].hashes()
         assert {k: got[k] for k in case["hashes"]} == case["hashes"]
     finally:
-        for wf in ranks:
-            wf.close()
-        g.close()
+        _close_group(g, ranks)
