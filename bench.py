@@ -97,6 +97,14 @@ def job_value(cells, steps, elapsed, world, shard):
     return seqs_per_step * steps * cells / elapsed
 
 
+def share_comm_id(rank, dist, make_id):
+    """The band-sharded fold's RCCL unique id: rank 0 makes it (ccj_amd.comm_unique_id), every rank
+    receives the same 128 bytes over torch.distributed (gloo) before any rank calls ccj_comm_init."""
+    obj = [make_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -230,6 +238,12 @@ def main(argv=None):
         return rseq(a.seed if shard else rank_seed(a.seed, rank, world, step, a.distinct), a.n)
 
     if a.dry_run:
+        comm_ok = None
+        if shard:  # the comm-id hand-off of the sharded path, with a stand-in id (no RCCL, no GPU)
+            cid = share_comm_id(rank, dist, lambda: os.urandom(128))
+            ids = [None] * world
+            dist.all_gather_object(ids, cid)
+            comm_ok = len(cid) == 128 and all(x == cid for x in ids)
         barrier()
         t0 = time.perf_counter()
         for _ in range(a.steps):
@@ -239,7 +253,7 @@ def main(argv=None):
         if rank == 0:
             print(json.dumps({"metric": METRIC, "value": job_value(cells, a.steps, elapsed, world, shard),
                               "unit": "DP-cells/s", "n_gpus": world, "ranks_reported": ranks, "steps": a.steps,
-                              "warmup": a.warmup, "dry_run": True,
+                              "warmup": a.warmup, "dry_run": True, "shard": shard, "comm_id_agreed": comm_ok,
                               "seeds": [rank_seed(a.seed, r, world, 0, a.distinct) for r in range(world)]}), flush=True)
         if dist is not None:
             dist.destroy_process_group()
@@ -256,9 +270,8 @@ def main(argv=None):
     inflight = 1 if shard else max(1, min(2, inflight))
     t_c = time.perf_counter()
     if shard:
-        obj = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        ctxs = [W_final(seq_at(0), 2, params=a.params, device=local, shard_world=world, shard_rank=rank, comm_id=obj[0])]
+        cid = share_comm_id(rank, dist, comm_unique_id)
+        ctxs = [W_final(seq_at(0), 2, params=a.params, device=local, shard_world=world, shard_rank=rank, comm_id=cid)]
     else:
         ctxs = [W_final(seq_at(0), 2, params=a.params, device=local) for _ in range(inflight)]
     create_ms = (time.perf_counter() - t_c) * 1e3 / len(ctxs)

@@ -43,6 +43,7 @@ PF_MAT2 = ["V", "VM", "WM", "WMv", "WMp", "WBP", "WPP", "P"]
 CCJ_E_PF_SAMPLE = 8  # include/ccj_pf.h
 
 CCJ_OK, CCJ_E_ARG, CCJ_E_OOM, CCJ_E_HIP, CCJ_E_PARAMS, CCJ_E_BACKTRACK, CCJ_E_STATE, CCJ_E_INTER_EXIT = range(8)
+CCJ_E_COMM = 9  # include/ccj.h: band-sharded exchange failed or timed out
 CCJ_E_PARFILE = 8  # include/ccj_parfile.h
 
 # name -> blob file (the reference's params/*.par sets, dumped to our table format)

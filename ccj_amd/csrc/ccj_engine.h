@@ -34,6 +34,7 @@ constexpr int IL_B = CCJ_ILB;  // interior-loop candidates per load batch (k_ilo
 constexpr int IL_CAP = (IE_U * IE_U + IL_B + 7) / 8 * 8;  // candidate-list capacity per pair (+ IL_B null tail)
 constexpr int IL_SEG = 64;   // per pair: seg[dt] = first list entry of source-level distance dt
 constexpr int IT_TI = 8;     // k_iloop: closing pairs per tile (their partner rows are staged once)
+constexpr int IT_PAD = 256;  // elements of padding before and after d4x / pmx (k_iloop stages whole rows)
 
 struct LevelDesc {
     int16_t *base;  // first element of level t (matrix 0)
@@ -195,8 +196,10 @@ int ccjk_level4d(const ccj::DevTables *T, int t, int G, int rank, int copies, vo
 int ccjk_level_split(int n, int t, int nblk, int split_target);
 int ccjk_level4d_lead(const ccj::DevTables *T, int t, int G, int rank, void *stream);
 int ccjk_pack(const ccj::DevTables *T, int t, int G, int r, int nmax, int16_t *send, void *stream);
-int ccjk_unpack(const ccj::DevTables *T, int t, int G, int r, int nmax, const int16_t *recv, void *stream);
+int ccjk_unpack(const ccj::DevTables *T, int t, int G, int r, int nmax, const int16_t *recv, size_t rstride, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
-int ccjk_ppush(const ccj::DevTables *T, int lev, void *stream);
+int ccjk_ppush(const ccj::DevTables *T, int lev, int G, int rank, void *stream);
+int ccjk_ptail_pack(const ccj::DevTables *T, int sigma, int16_t *tail, void *stream);
+int ccjk_ptail_unpack(const ccj::DevTables *T, int sigma, const int16_t *recv, size_t slice, size_t off, int G, void *stream);
 int ccjk_canon(const ccj::DevTables *T, int x, const long long *offij, int16_t *out, void *stream);
 }

@@ -129,7 +129,8 @@ struct ccj_ctx {
     LevelDesc *d_lv = nullptr;
     long long *d_lb = nullptr;
     LvlDev *d_ld = nullptr;
-    int16_t *d4x = nullptr, *pmx = nullptr;  // interior-loop copies of PL/PR and PM
+    int16_t *d4x = nullptr, *pmx = nullptr;  // interior-loop copies of PL/PR and PM (IT_PAD into the allocations)
+    int16_t *d4x_alloc = nullptr, *pmx_alloc = nullptr;
     uint4 *d_rec = nullptr;                  // AoS loop records
     uint4 *d_acc = nullptr;                  // partial-record ring (split-point sharing)
     int16_t *d_lord = nullptr;               // long-scan a-blocks per sharing level, longest first
@@ -162,6 +163,7 @@ struct ccj_ctx {
     std::vector<hipEvent_t> pre_done;    // prepass launch of level t finished
     bool prepass = false;                // CCJ_PREPASS=1: leader launch of level t beside level t-1 (measured +0.5 ms at n=200)
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
+    std::vector<hipEvent_t> pp_done; // band-sharded: this rank's P-term push of span sigma done (before the exchange)
     std::vector<double> lev_ms_v, diag_ms_v, il_ms_v;
     std::vector<hipEvent_t> il_done, dg_done;  // k_iloop(t) / k_diag2d(sigma) finished
     std::vector<hipEvent_t> lev_done;
@@ -1410,6 +1412,10 @@ extern "C" uint64_t ccj_num_cells(int n) {
 
 static thread_local std::string g_create_err;
 
+// int16 elements of the exchange slice's P tail: one 64-bit (value, first split) word per interval
+// start i = 0..n
+#define PTAIL_ELEMS(n) (4 * ((size_t)(n) + 1))
+
 // The exchange of one level through the in-process group: every member pulls each member's
 // packed slice into its own receive buffer (same device), between two barriers, so no slice is
 // overwritten by the next level's pack before every member has read it.
@@ -1605,6 +1611,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     for (auto &e : c->lev_done) HIPCHK(cp, hipEventCreateWithFlags(&e, fence_fl));
     c->p_done.resize(n + 1);
     for (auto &e : c->p_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
+    c->pp_done.resize(n + 1);
+    for (auto &e : c->pp_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
     c->tev.resize(7 * (size_t)n + 7);
     for (auto &e : c->tev) HIPCHK(cp, hipEventCreate(&e));
 
@@ -1699,12 +1707,16 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
             ox += 2LL * c->lv_host[t].C;
             op += (long long)c->lv_host[t].m * n * (t + 1);
         }
-        const size_t pad = 256;
+        // IT_PAD elements before and after each copy: k_iloop stages whole 66-value rows, whose
+        // lanes outside the row read (and never use) neighbouring elements
+        const size_t pad = 2 * IT_PAD;
         c->nx = ox;
         c->npm = op;
-        if (hipMalloc(&c->d4x, ((size_t)ox + pad) * sizeof(int16_t)) != hipSuccess ||
-            hipMalloc(&c->pmx, ((size_t)op + pad) * sizeof(int16_t)) != hipSuccess)
+        if (hipMalloc(&c->d4x_alloc, ((size_t)ox + pad) * sizeof(int16_t)) != hipSuccess ||
+            hipMalloc(&c->pmx_alloc, ((size_t)op + pad) * sizeof(int16_t)) != hipSuccess)
             return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for interior-loop copies failed", (ox + op) * 2e-9);
+        c->d4x = c->d4x_alloc + IT_PAD;
+        c->pmx = c->pmx_alloc + IT_PAD;
         HIPCHK(cp, hipMalloc(&c->d_ldx, ldx.size() * sizeof(LvlX)));
         HIPCHK(cp, hipMemcpy(c->d_ldx, ldx.data(), ldx.size() * sizeof(LvlX), hipMemcpyHostToDevice));
         const size_t pairs = (size_t)(n + 1) * c->rs;
@@ -1827,7 +1839,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
                 int nm = 0;
                 for (int r = 0; r < G; ++r) nm = std::max(nm, shard_count(t, G, r));
                 c->xnmax[t] = nm;
-                slice = std::max(slice, (size_t)NMAT4 * nm * c->lv_host[t].M);
+                slice = std::max(slice, (((size_t)NMAT4 * nm * c->lv_host[t].M + 3) & ~(size_t)3) + PTAIL_ELEMS(n));
             }
             if (hipMalloc(&c->d_send, std::max<size_t>(slice, 1) * sizeof(int16_t)) != hipSuccess ||
                 hipMalloc(&c->d_recv, std::max<size_t>(slice * G, 1) * sizeof(int16_t)) != hipSuccess)
@@ -1898,8 +1910,15 @@ extern "C" int ccj_reset(ccj_ctx *c, const char *seq) {
 // stream's work of the fill is complete (st waits for the last span, which waits for the last P,
 // and every level waited for its k_iloop / leader launches).
 // The P terms that complete P(lev+3): every term whose operands' highest level is lev (k_ppush,
-// DESIGN.md §4).
-static int pterm_launch(const ccj::DevTables *T, int lev, hipStream_t s) { return ccjk_ppush(T, lev, s); }
+// DESIGN.md §4).  Band-sharded, each rank pushes its share (outer index r, r+G, ...; every share in
+// simulation) and the spans are min-combined in the exchange of level lev+1.
+static int pterm_launch(const ccj_ctx *c, int lev, hipStream_t s) {
+    for (int r = 0; r < c->world; ++r) {
+        if (!c->simulate && r != c->rank) continue;
+        if (const int e = ccjk_ppush(&c->T, lev, c->world, r, s)) return e;
+    }
+    return 0;
+}
 
 static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     if (!c) return CCJ_E_ARG;
@@ -1984,17 +2003,31 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                 // band-sharded exchange: this rank's cells of the level, all 22
                 // matrices, packed into one slice; ONE all-gather of equal slices; the other ranks'
                 // cells unpacked with their loop records and interior-loop copies
+                // The slice's tail carries this rank's partials of P(s+2) (its share of the P terms,
+                // pushed after level s-1), min-combined on arrival: P rides the level exchange, no
+                // extra collective.
                 const int nmax = c->xnmax[s];
-                const size_t slice = (size_t)NMAT4 * nmax * c->lv_host[s].M;
+                const size_t slice4 = ((size_t)NMAT4 * nmax * c->lv_host[s].M + 3) & ~(size_t)3;
+                const size_t slice = slice4 + PTAIL_ELEMS(n);
+                const int sig = s + 2;
+                const bool ptail = s >= 1 && sig <= n - 1;
+                if (ptail) {
+                    HIPCHK(c, hipStreamWaitEvent(st, c->pp_done[sig], 0));
+                    HIPCHK(c, (hipError_t)ccjk_ptail_pack(&c->T, sig, c->d_send + slice4, st));
+                }
                 HIPCHK(c, (hipError_t)ccjk_pack(&c->T, s, G, c->rank, nmax, c->d_send, st));
                 if (c->lgroup) {
                     if (const int rc = local_allgather(c, slice)) return rc;
                 } else {
                     if (!c->comm) return set_err(c, CCJ_E_STATE, "sharded context without ccj_comm_init");
                     if (ncclAllGather(c->d_send, c->d_recv, slice * sizeof(int16_t), ncclInt8, c->comm, st) != ncclSuccess)
-                        return set_err(c, CCJ_E_HIP, "ncclAllGather failed at level %d", s);
+                        return set_err(c, CCJ_E_COMM, "ncclAllGather failed at level %d", s);
                 }
-                HIPCHK(c, (hipError_t)ccjk_unpack(&c->T, s, G, c->rank, nmax, c->d_recv, st));
+                HIPCHK(c, (hipError_t)ccjk_unpack(&c->T, s, G, c->rank, nmax, c->d_recv, slice, st));
+                if (ptail) {
+                    HIPCHK(c, (hipError_t)ccjk_ptail_unpack(&c->T, sig, c->d_recv, slice, slice4, G, st));
+                    HIPCHK(c, hipEventRecord(c->p_done[sig], st));  // P(sig) final on every rank
+                }
             }
             HIPCHK(c, trec(5, st));
             HIPCHK(c, hipEventRecord(c->lev_done[s], st));
@@ -2005,14 +2038,15 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                 HIPCHK(c, hipMemcpyAsync(c->h4 + c->lv_off[s], c->d4 + c->lv_off[s], bytes, hipMemcpyDeviceToHost,
                                          c->st_copy));
             }
-            // P(s+3) only needs PK levels <= s
+            // P(s+3) only needs PK levels <= s; band-sharded, this rank's partials are combined in
+            // the exchange of level s+1, which then records p_done[s+3]
             if (s + 3 < n) {
                 HIPCHK(c, hipStreamWaitEvent(c->st_p, c->lev_done[s], 0));
-                HIPCHK(c, (hipError_t)pterm_launch(&c->T, s, c->st_p));
-                HIPCHK(c, hipEventRecord(c->p_done[s + 3], c->st_p));
+                HIPCHK(c, (hipError_t)pterm_launch(c, s, c->st_p));
+                HIPCHK(c, hipEventRecord((G > 1 && !c->simulate ? c->pp_done : c->p_done)[s + 3], c->st_p));
             }
         } else if (s + 3 < n && s + 3 >= 3) {
-            HIPCHK(c, (hipError_t)pterm_launch(&c->T, s, c->st_p));
+            HIPCHK(c, (hipError_t)pterm_launch(c, s, c->st_p));
             HIPCHK(c, hipEventRecord(c->p_done[s + 3], c->st_p));
         }
     }
@@ -2026,13 +2060,46 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     return CCJ_OK;
 }
 
+// Wait for the fill's end event.  A band-sharded fill over RCCL cannot finish if a peer rank died
+// or hangs (its all-gathers never complete): the wait polls the communicator's asynchronous error
+// state and a deadline (CCJ_COMM_TIMEOUT_S, default 300 s) and, on either, aborts the communicator
+// (ncclCommAbort makes the pending collectives return) and fails with CCJ_E_COMM instead of hanging.
+static int wait_fill_end(ccj_ctx *c) {
+    if (!c->comm) {
+        HIPCHK(c, hipEventSynchronize(c->ev_end));
+        return CCJ_OK;
+    }
+    static const double limit_s = [] {
+        const char *e = getenv("CCJ_COMM_TIMEOUT_S");
+        return e && atof(e) > 0 ? atof(e) : 300.0;
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(c->ev_end);
+        if (q == hipSuccess) return CCJ_OK;
+        if (q != hipErrorNotReady) return set_err(c, CCJ_E_HIP, "fill: %s", hipGetErrorString(q));
+        ncclResult_t ae = ncclSuccess;
+        const ncclResult_t qr = ncclCommGetAsyncError(c->comm, &ae);
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (qr != ncclSuccess || ae != ncclSuccess || el > limit_s) {
+            ncclCommAbort(c->comm);
+            c->comm = nullptr;
+            if (qr != ncclSuccess || ae != ncclSuccess)
+                return set_err(c, CCJ_E_COMM, "band-sharded exchange failed: %s",
+                               ncclGetErrorString(qr != ncclSuccess ? qr : ae));
+            return set_err(c, CCJ_E_COMM, "band-sharded exchange made no progress for %.0f s (a peer rank failed?)", limit_s);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+}
+
 // Wait for an enqueued fill, check the device error word and read its timings.
 static int fill_finish(ccj_ctx *c) {
     if (!c || !c->pending) return c ? set_err(c, CCJ_E_STATE, "no fill in flight") : CCJ_E_ARG;
     c->pending = false;
     HIPCHK(c, hipSetDevice(c->device));
     const int n = c->n;
-    HIPCHK(c, hipEventSynchronize(c->ev_end));
+    if (const int rc = wait_fill_end(c)) return rc;
     int herr = 0;
     HIPCHK(c, hipMemcpy(&herr, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (herr & 1) return set_err(c, CCJ_E_PARAMS, "e_intP table value outside int16 range (flags %d)", herr);
@@ -2625,14 +2692,14 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_lv);
     hipFree(c->d_lb);
     hipFree(c->d_ld);
-    hipFree(c->d4x);
+    hipFree(c->d4x_alloc);
     hipFree(c->d_rec);
     hipFree(c->d_acc);
     hipFree(c->d_wterm);
     hipFree(c->d_lord);
     hipFree(c->d_lord_off);
     hipFree(c->d_wbw);
-    hipFree(c->pmx);
+    hipFree(c->pmx_alloc);
     hipFree(c->d_ldx);
     hipFree(c->d_il);
     hipFree(c->d_ilm);
@@ -2659,6 +2726,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->h4) hipHostFree(c->h4);
     for (auto e : c->lev_done) hipEventDestroy(e);
     for (auto e : c->p_done) hipEventDestroy(e);
+    for (auto e : c->pp_done) hipEventDestroy(e);
     if (c->st_p) hipStreamDestroy(c->st_p);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->st_il) hipStreamDestroy(c->st_il);

@@ -19,7 +19,7 @@ namespace ccj {
 
 inline void level_iloop_items(int n, int t, int G, int r, std::vector<uint32_t> &out) {
     const int m = n - t - 2;
-    if (m <= 0 || t < 6) return;
+    if (m <= 0 || t < 4) return;  // PM from t = 4 (a, b >= 2), PL / PR from t = 6
     auto push = [&](uint32_t role, int f1, int tile, int chunks) {
         for (int c = 0; c < chunks; ++c)
             out.push_back((role << 30) | ((uint32_t)f1 << 20) | ((uint32_t)tile << 10) | (uint32_t)c);

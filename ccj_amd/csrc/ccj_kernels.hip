@@ -375,18 +375,21 @@ __device__ __forceinline__ const int16_t *uni(const int16_t *p) {
 constexpr int PP_OFF = 1 << 30;
 
 template <int PP_S>
-__global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, int npairs, int hs_len, int blocksA) {
+__global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, int npairs, int hs_len, int blocksA, int G,
+                                               int rank, int nout) {
     const int n = T.n, rs = T.rs;
     const int lane = threadIdx.x & 63;
     const int partB = (int)blockIdx.x >= blocksA;
     // wave-uniform (readfirstlane: lets the compiler keep every index below in SGPRs)
     const int item = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - (partB ? blocksA : 0)) * 4 + (int)(threadIdx.x >> 6));
-    // item = (pair * ngrp + g) * (lev+1) + outer; outer = jo (part A) / a2 (part B); pair = one
+    // item = (pair * ngrp + g) * nout + own outer; outer = jo (part A) / a2 (part B), rank r of G
+    // taking outer = r, r+G, ... (band sharding: every rank pushes its share of the terms into its
+    // own T.Pk and the P spans are min-combined in the level exchange); pair = one
     // (chunk c of PP_S spans, slice hs = [hs*hs_len, +hs_len) of the inner loop h1 / h2), so long
     // loops spread over waves.  Chunk c's inner loop runs over h < min((c+1)*PP_S, nmax), so it has
     // ceil(that / hs_len) slices; the pairs are enumerated chunk by chunk (part A's count, nmax).
-    const int outer = item % (lev + 1);
-    int pr = item / (lev + 1);
+    const int outer = rank + G * (item % nout);
+    int pr = item / nout;
     const int g = pr % ngrp;
     pr /= ngrp;
     if (pr >= npairs) return;  // whole wave
@@ -570,65 +573,69 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
 
 // ------------------------------------------------------------------------------------------
 // Interior loops of level t (get_PLiloop / get_PRiloop / get_PMiloop, pseudo_loop.cc:682-773),
-// tiled so that a partner value is loaded from HBM once for every closing pair of a tile that
-// reads it.
+// tiled so that a partner value is loaded once for every closing pair of a tile that reads it.
 //
 // For a fixed source level t' = t - dt the interior loops of one role are a 1-D min-plus sweep:
-//   PL  closing pair (i, i+a), cell (i,j,k,l):   min over u1 of E(i,u1,dt) + PL(i+1+u1, ., k, l)
-// and the partner row d = i+1+u1 (the inner pair (d, d+a-dt)) is read by every closing pair
-// i = d-1-u1 of the same (a, k, l), u1 = 0..min(dt-2, 28).  So a workgroup takes a TILE of
-// IT_TI consecutive closing pairs and 64 lanes of the free index (PL: lanes k; PR: tile along k,
-// lanes i; PM: tile along j at fixed gap g, lanes i), and per source level it
-//   1. stages the partner rows d of the whole tile (IT_TI + 28 at most, only those whose inner
-//      pair can pair: the only ones any candidate reads) from the PLx/PRx/PMx copy into LDS —
-//      one coalesced 128-byte load per row, all of a source level's rows in flight together;
-//   2. walks each closing pair's candidate list for that source level (wave-uniform: the pair's
-//      il/ilm segment for dt, scalar loads) and takes min(energy + LDS[row][lane]).
-// Each lane stages and reads only its own LDS column, so no barrier is needed inside the walk.
-// The four waves of a workgroup take the source levels dt = 3+w, 7+w, ... of the same tile and
-// are min-reduced through LDS at the end.  The candidate (u1, u2) = (0, 0), source level t-2,
-// reads the stack term's inner cell, so k_level4d(t) evaluates it; k_iloop(t) needs levels <= t-3.
-// The minimum (clamped like a store) goes into the cell's own PL / PR / PM slot of level t, where
-// k_level4d(t) picks it up.  (Round 2's form, one wave per closing pair loading every candidate's
-// partner from L2/MALL, moved 1.44x the algorithmic bytes at 0.14 of the HBM roofline.)
+//   PL  closing pair (i, i+a), cell (i,j,k,l):   min over u1 of E(i,u1,u2) + PL(i+1+u1, ., k, l)
+// (u2 = dt-2-u1), and the partner row d = i+1+u1 (inner pair (d, d+a-dt)) is read by every
+// closing pair i = d-1-u1 of the same (a, k, l).  A workgroup takes a TILE of IT_TI consecutive
+// closing pairs and 64 lanes of the free index (PL: lanes k; PR: tile along k, lanes i; PM: tile
+// along j at fixed gap g, lanes i).  Its four waves take the source levels dt = 3+w, 7+w, ... and
+//   1. mark the partner rows whose pair can pair (the only ones a candidate reads: the reference's
+//      can_pair filter), one ballot per source level;
+//   2. stage those rows from the PLx/PRx/PMx copy into LDS with LDS-DMA loads (global_load_lds_dword,
+//      no VGPR destination: 33 lanes move one 64-value row from its dword-aligned start, the parity
+//      kept per slot; the ushort form writes a dword per lane, twice the LDS), the rows of several
+//      source levels in flight together, compacted to the pairable ones;
+//   3. walk every candidate (set bits of the row mask in each pair's window) as
+//      min(E + LDS[row][lane]), E from the tile's interior-loop energies (staged once per
+//      workgroup from the e_intP table), and min-reduce the waves through LDS at the end.
+// The candidate (u1, u2) = (0, 0) (source level t-2) reads the stack term's inner cell, so
+// k_level4d(t) evaluates it; k_iloop(t) needs levels <= t-3 only.  The minimum (clamped like a store)
+// goes into the cell's own PL / PR / PM slot of level t, where k_level4d(t) picks it up.
+// (Round 2's form — one wave per closing pair, every candidate's partner loaded from L2 / MALL —
+// moved 1.44x the algorithmic bytes at 0.14 of the HBM roofline.)
 //
-// Work items (ccj_create, sequence-independent; il_items below): one per (role, a or g, tile,
-// 64-lane chunk) of the rank's own a-blocks, role << 30 | f1 << 20 | tile << 10 | chunk.
+// Work items (ccj_create, sequence-independent; ccj_items.h): one per (role, a or g, tile, 64-lane
+// chunk) of the rank's own a-blocks, role << 30 | f1 << 20 | tile << 10 | chunk.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int il_u1(uint32_t x) { return (int)((x >> 16) & 31u); }
-__device__ __forceinline__ int il_e(uint32_t x) { return (int)(int16_t)(x & 0xffffu); }
-
-constexpr int IT_W = 4;                      // waves per tile: source levels interleaved over them
-constexpr int IT_ROWS = IT_TI + IE_U - 1;    // partner rows of one source level (u1 spans <= 28)
+constexpr int IT_W = 4;                    // waves per tile: source levels interleaved over them
+constexpr int IT_RB = 48;                  // LDS partner-row slots per wave (>= IT_TI + IE_U - 1)
+constexpr int IT_RW = 68;                  // int16 per row slot: 66 staged (33 dwords) + pad to 8 B
+constexpr int IT_NQ = 16;                  // source levels per wave, at most ceil(56 / IT_W)
+constexpr int IT_NE = IE_U * IE_U;         // (u1, u2) energies per closing pair
+static_assert(IT_RB >= IT_TI + IE_U - 1, "one source level's rows must fit");
 
 __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long first, int nitems, int G_SH, int rank) {
-    __shared__ int16_t stage[IT_W][IT_ROWS][64];
+    __shared__ int16_t en_s[IT_NE * IT_TI];             // [(u1*29+u2)*IT_TI + p]
+    __shared__ int16_t rows_s[IT_W][IT_RB][IT_RW];      // staged partner rows, per wave
+    __shared__ unsigned long long msk_s[IT_W][IT_NQ];    // pairable-row mask of each source level
+    typedef const __attribute__((address_space(1))) int16_t gshort;
     const int n = T.n, rs = T.rs, m = n - t - 2;
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     if ((int)blockIdx.x >= nitems) return;  // whole workgroup
     const uint32_t it = T.items[first + blockIdx.x];
     const int role = (int)(it >> 30), f1 = (int)((it >> 20) & 1023u), tx = (int)((it >> 10) & 1023u);
     const int chunk = (int)(it & 1023u);
-    const LvlDev Lt = T.ld[t];
-    int a = 0, b = 0, g = 0, p0 = 0, lv = 0, dtmax = 0;
+    int a = 0, b = 0, g = 0, p0 = 0, lv = 0, dtmax = 0, pw = 0;
     if (role == 0) {         // PL: closing pairs (i, i+a), i = p0+p; lanes k
-        a = f1; b = t - a;
+        a = f1; b = t - a; pw = a;
         p0 = 1 + IT_TI * tx;
         lv = p0 + a + 2 + 64 * chunk + lane;
         dtmax = imin(imin(a - 4, 2 * (IE_U - 1) + 2), t);
     } else if (role == 1) {  // PR: closing pairs (k, k+b), k = p0+p; lanes i
-        a = f1; b = t - a;
+        a = f1; b = t - a; pw = b;
         p0 = a + 3 + IT_TI * tx;
         lv = 1 + 64 * chunk + lane;
         dtmax = imin(imin(b - 4, 2 * (IE_U - 1) + 2), t);
     } else {                 // PM: enclosed pairs (j, j+g), j = p0+p; lanes i
-        g = f1;
+        g = f1; pw = g;
         p0 = 3 + IT_TI * tx;
         lv = imax(1, p0 - t + 2) + 64 * chunk + lane;
         dtmax = imin(t - 2, 2 * (IE_U - 1) + 2);
     }
-    // the tile's closing pairs: valid (some cell) and able to pair; their candidate lists
+    // the tile's pairs with some cell that can pair
     bool pv = false;
     if (lane < IT_TI) {
         const int q = p0 + lane;
@@ -638,6 +645,63 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
     }
     const unsigned pmask = (unsigned)__ballot(pv);
     if (!pmask) return;  // whole workgroup (the ballot is the same in every wave)
+
+    // ---- phase A: the tile's energies (whole workgroup) and this wave's pairable-row masks
+    //   PL: E = IE[u1][u2][a][i];   PR: E = IE[u1][u2][b][k];   PM: E = IE[u1][u2][g+dt][j-1-u1]
+    //   (the outer pair's span and start; k_precompute_ie, pseudo_loop.cc:822-840)
+    constexpr int EPT = (IT_NE * IT_TI + 255) / 256;
+    int ev[EPT];
+#pragma unroll
+    for (int x = 0; x < EPT; ++x) {
+        const int idx = tid + 256 * x;
+        ev[x] = 0;
+        if (idx < IT_NE * IT_TI) {
+            const int uu = idx / IT_TI, p = idx - uu * IT_TI;
+            const int u1 = uu / IE_U, u2 = uu - u1 * IE_U;
+            int ew = pw, ep = p0 + p;
+            if (role == 2) { ew = g + u1 + u2 + 2; ep = p0 + p - 1 - u1; }
+            ew = imin(ew, n);
+            ep = imin(imax(ep, 0), rs - 1);  // outside the tile's valid candidates: any in-range entry
+            ev[x] = T.ie[((size_t)uu * (n + 1) + ew) * rs + ep];
+        }
+    }
+    unsigned long long rmv[IT_NQ];
+    int nq = 0;
+#pragma unroll
+    for (int q = 0; q < IT_NQ; ++q) {
+        const int dt = 3 + w + IT_W * q;
+        bool rv = false;
+        if (dt <= dtmax) {
+            nq = q + 1;
+            const int u1lo = imax(0, dt - 2 - (IE_U - 1)), u1hi = imin(IE_U - 1, dt - 2);
+            if (lane < IT_TI + u1hi - u1lo) {
+                // row r: PL d = p0+1+u1lo+r, pair (d, d+a-dt); PR d = p0+1+u1lo+r, (d, d+b-dt);
+                //        PM d = p0-1-u1hi+r, (d, d+g+dt)
+                if (role == 0) {
+                    const int d = p0 + 1 + u1lo + lane;
+                    rv = d <= m + dt && ptype(T, d, d + a - dt) > 0;
+                } else if (role == 1) {
+                    const int d = p0 + 1 + u1lo + lane;
+                    rv = d + b - dt <= n && ptype(T, d, d + b - dt) > 0;
+                } else {
+                    const int d = p0 - 1 - u1hi + lane;
+                    rv = d >= 1 && d + g + dt <= n && ptype(T, d, d + g + dt) > 0;
+                }
+            }
+        }
+        rmv[q] = __ballot(rv);
+    }
+#pragma unroll
+    for (int x = 0; x < EPT; ++x) {
+        const int idx = tid + 256 * x;
+        if (idx < IT_NE * IT_TI) en_s[idx] = (int16_t)ev[x];
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < IT_NQ; ++q) msk_s[w][q] = rmv[q];
+    }
+    __syncthreads();
+
     // per pair: the lane's cell, its validity and (PM) its loop-window bounds
     int acc[IT_TI];
     bool cv[IT_TI];
@@ -646,11 +710,12 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
     for (int p = 0; p < IT_TI; ++p) {
         acc[p] = INF;
         const int q = p0 + p;
+        pa2[p] = pb2[p] = 0;
         if (role == 0) {
-            const int h = lv - q - a - 2;   // k = j+2+h
+            const int h = lv - q - a - 2;  // k = j+2+h
             cv[p] = h >= 0 && h <= m - q;
         } else if (role == 1) {
-            const int h = q - lv - a - 2;   // k = i+a+2+h
+            const int h = q - lv - a - 2;  // k = i+a+2+h
             cv[p] = lv >= 1 && h >= 0 && lv <= m - h;
         } else {
             const int aa = q - lv, bb = t - aa;  // a = j-i
@@ -659,103 +724,95 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
             pb2[p] = bb - 2;
         }
     }
-    const uint2 *__restrict__ LST = role == 2 ? T.ilm : T.il;
-    const uint32_t *__restrict__ SEG = role == 2 ? T.ilmseg : T.ilseg;
-    const int pw = role == 0 ? a : role == 1 ? b : g;  // list row: pair (p0+p, p0+p+pw)
-    int16_t *col = &stage[w][0][lane];
+    int16_t *const rbase = &rows_s[w][0][0];
+    // ---- phase B: groups of source levels whose compacted rows fit in the wave's IT_RB slots
 #pragma unroll 1
-    for (int dt = 3 + w; dt <= dtmax; dt += IT_W) {
-        const int u1lo = imax(0, dt - 2 - (IE_U - 1)), u1hi = imin(IE_U - 1, dt - 2);
-        const int nrows = IT_TI + u1hi - u1lo;
-        const int ts = t - dt, ms = m + dt;
-        const LvlDev Ls = T.ld[ts];
-        const LvlX Xs = T.ldx[ts];
-        // row r of this source level: the partner rows the tile's candidates can read
-        //   PL: d = p0+1+u1lo+r, inner pair (d, d+a-dt)      PR: d = p0+1+u1lo+r, (d, d+b-dt)
-        //   PM: d = p0-1-u1hi+r, outer pair (d, d+g+dt)
-        bool rv = false;
-        if (lane < nrows) {
-            if (role == 0) {
-                const int d = p0 + 1 + u1lo + lane;
-                rv = d <= ms && ptype(T, d, d + a - dt) > 0;
-            } else if (role == 1) {
-                const int d = p0 + 1 + u1lo + lane;
-                rv = d + b - dt <= n && ptype(T, d, d + b - dt) > 0;
-            } else {
-                const int d = p0 - 1 - u1hi + lane;
-                rv = d >= 1 && d + g + dt <= n && ptype(T, d, d + g + dt) > 0;
-            }
+    for (int q0 = 0; q0 < nq;) {
+        // plan: source levels q0 .. q1-1, slot bases sb
+        int q1 = q0, used = 0;
+        while (q1 < nq) {
+            const int c = __popcll(msk_s[w][q1]);
+            if (used + c > IT_RB) break;
+            used += c;
+            ++q1;
         }
-        unsigned long long rm = __ballot(rv);
-        // stage the rows, 8 loads in flight per batch
-        typedef const __attribute__((address_space(1))) int16_t gshort;
-        while (rm) {
-            int rr[8], v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                rr[u] = -1;
-                v[u] = 0;
-                if (rm) {
-                    const int r = __builtin_ctzll(rm);
-                    rm &= rm - 1;
-                    rr[u] = r;
-                    long long e;
-                    if (role == 0) {
-                        const int d = p0 + 1 + u1lo + r, as = a - dt;
-                        const int hs = imin(imax(lv - d - as - 2, 0), ms - d);
-                        e = Xs.lbx + (long long)as * Ls.M + (long long)(d - 1) * ms - (((long long)(d - 1) * (d - 2)) >> 1) + hs;
-                    } else if (role == 1) {
-                        const int d = p0 + 1 + u1lo + r, qs = d - a - 3;
-                        const int il = imin(imax(lv, 1), qs + 1);
-                        e = Xs.lbx + Ls.C + (long long)a * Ls.M + (((long long)qs * (qs + 1)) >> 1) + il - 1;
-                    } else {
-                        const int d = p0 - 1 - u1hi + r, hs = g + dt - 2;
-                        const int as = imin(imax(d - lv, 0), ts);
-                        e = Xs.pmb + ((long long)hs * n + d - 1) * (ts + 1) + as;
-                    }
+        // issue every row of the group: one LDS-DMA dword load per row (lanes 0..32, the row's
+        // 64 values from its dword-aligned start; LDS gets base + 4*lane), parity bit per slot
+        int slot = 0;
+        unsigned long long odd = 0;
+        const int lv0 = lv - lane;  // lane 0's free index
+#pragma unroll 1
+        for (int q = q0; q < q1; ++q) {
+            const int dt = 3 + w + IT_W * q;
+            const int u1lo = imax(0, dt - 2 - (IE_U - 1)), u1hi = imin(IE_U - 1, dt - 2);
+            const int ts = t - dt, ms = m + dt;
+            const LvlDev Ls = T.ld[ts];
+            const LvlX Xs = T.ldx[ts];
+            unsigned long long rm = msk_s[w][q];
+#pragma unroll 1
+            while (rm) {
+                const int r = __builtin_ctzll(rm);
+                rm &= rm - 1;
+                long long e0;  // element of the row's lowest staged value (lane 0, or lane 63 for PM)
+                if (role == 0) {
+                    const int d = p0 + 1 + u1lo + r, as = a - dt;
+                    e0 = Xs.lbx + (long long)as * Ls.M + (long long)(d - 1) * ms - (((long long)(d - 1) * (d - 2)) >> 1) +
+                         (lv0 - d - as - 2);
+                } else if (role == 1) {
+                    const int d = p0 + 1 + u1lo + r, qs = d - a - 3;
+                    e0 = Xs.lbx + Ls.C + (long long)a * Ls.M + (((long long)qs * (qs + 1)) >> 1) + lv0 - 1;
+                } else {
+                    const int d = p0 - 1 - u1hi + r, hs = g + dt - 2;
+                    e0 = Xs.pmb + ((long long)hs * n + d - 1) * (ts + 1) + (d - lv0) - 63;  // lanes read downwards
+                }
+                const long long ea = e0 & ~1ll;
+                odd |= (unsigned long long)(e0 & 1) << slot;
 #ifdef CCJ_DEBUG_BOUNDS
-                    if (e < 0 || e >= (role == 2 ? T.npm : T.nx)) {
-                        if (atomicOr(T.err, 64) == 0) printf("k_iloop OOB: role %d t %d dt %d r %d e %lld\n", role, t, dt, r, e);
-                        e = 0;
-                    }
+                if (ea < -IT_PAD || ea + 66 > (role == 2 ? T.npm : T.nx) + IT_PAD) {
+                    if (atomicOr(T.err, 64) == 0) printf("k_iloop OOB: role %d t %d dt %d r %d e %lld\n", role, t, dt, r, ea);
+                } else
 #endif
-                    v[u] = (int)*(gshort *)((role == 2 ? T.pmx : T.d4x) + e);
-                }
+                if (lane <= 32)
+                    __builtin_amdgcn_global_load_lds((gshort *)((role == 2 ? T.pmx : T.d4x) + ea + 2 * lane),
+                                                     (__attribute__((address_space(3))) void *)(rbase + slot * IT_RW), 4, 0, 0);
+                ++slot;
             }
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (rr[u] >= 0) col[rr[u] * 64] = (int16_t)v[u];
         }
-        // candidates of each closing pair at this source level, from the staged rows
-#pragma unroll
-        for (int p = 0; p < IT_TI; ++p) {
-            if (!((pmask >> p) & 1u)) continue;
-            const size_t pidx = (size_t)pw * rs + (p0 + p);
-            const int e0 = (int)SEG[pidx * IL_SEG + dt], e1 = (int)SEG[pidx * IL_SEG + dt + 1];
-            const uint2 *ent = LST + pidx * IL_CAP;
-            // row of candidate u1: PL/PR r = p+u1-u1lo, PM r = p+u1hi-u1
-            const int rb = role == 2 ? p + u1hi : p - u1lo;
-            int best = acc[p];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // the group's candidates
+        int sb = 0;
 #pragma unroll 1
-            for (int e = e0; e < e1; e += 4) {
-                uint32_t x4[4];
+        for (int q = q0; q < q1; ++q) {
+            const int dt = 3 + w + IT_W * q;
+            const int u1lo = imax(0, dt - 2 - (IE_U - 1)), u1hi = imin(IE_U - 1, dt - 2);
+            const unsigned long long rm = msk_s[w][q];
+            const unsigned long long cm = (1ull << (u1hi - u1lo + 1)) - 1;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) x4[u] = ent[e + u].x;  // past e1: later entries or the null tail
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int u1 = il_u1(x4[u]);
-                    const int en = e + u < e1 ? il_e(x4[u]) : INF;
-                    const int r = imin(imax(role == 2 ? rb - u1 : rb + u1, 0), IT_ROWS - 1);
-                    int c = en + (int)col[r * 64];
-                    if (role == 2) c += ((u1 > pa2[p]) | (dt - 2 - u1 > pb2[p])) ? INF : 0;  // get_PMiloop: d > i, dp < l
-                    best = imin(best, c);
+            for (int p = 0; p < IT_TI; ++p) {
+                if (!((pmask >> p) & 1u)) continue;
+                unsigned long long cand = (rm >> p) & cm;  // bit c: row p+c
+                int best = acc[p];
+#pragma unroll 1
+                while (cand) {
+                    const int c = __builtin_ctzll(cand);
+                    cand &= cand - 1;
+                    const int r = p + c;
+                    const int u1 = role == 2 ? u1hi - c : u1lo + c, u2 = dt - 2 - u1;
+                    const int sl = sb + __popcll(rm & ((1ull << r) - 1));
+                    const int o = (int)((odd >> sl) & 1ull);
+                    int v = (int)en_s[(u1 * IE_U + u2) * IT_TI + p] + (int)rbase[sl * IT_RW + o + (role == 2 ? 63 - lane : lane)];
+                    if (role == 2) v += ((u1 > pa2[p]) | (u2 > pb2[p])) ? INF : 0;  // get_PMiloop: d > i, dp < l
+                    best = imin(best, v);
                 }
+                acc[p] = best;
             }
-            acc[p] = best;
+            sb += __popcll(rm);
         }
+        q0 = q1;
     }
-    // the waves' partial minima meet in wave 0 (each wave's own staging region holds its values)
-    int *red = (int *)&stage[w][0][0];
+    // the waves' partial minima meet in wave 0 (each wave's own row region holds its values)
+    __syncthreads();  // every wave is done reading its rows
+    int *red = (int *)rbase;
     if (w > 0) {
 #pragma unroll
         for (int p = 0; p < IT_TI; ++p) red[p * 64 + lane] = acc[p];
@@ -764,10 +821,11 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
     if (w > 0) return;
 #pragma unroll
     for (int v = 1; v < IT_W; ++v) {
-        const int *o = (const int *)&stage[v][0][0];
+        const int *o = (const int *)&rows_s[v][0][0];
 #pragma unroll
         for (int p = 0; p < IT_TI; ++p) acc[p] = imin(acc[p], o[p * 64 + lane]);
     }
+    const LvlDev Lt = T.ld[t];
     int16_t *dst = T.d4 + Lt.lb + (long long)(role == 0 ? PL : role == 1 ? PR : PM) * Lt.C;
 #pragma unroll
     for (int p = 0; p < IT_TI; ++p) {
@@ -1614,7 +1672,7 @@ extern "C" int ccjk_diag2d(const DevTables *T, int sigma, void *stream) {
 }
 
 // P terms of every span whose operands' highest level is lev (k_ppush); completes P(lev+3).
-extern "C" int ccjk_ppush(const DevTables *T, int lev, void *stream) {
+extern "C" int ccjk_ppush(const DevTables *T, int lev, int G, int rank, void *stream) {
 #ifdef CCJ_ABLATE_PTERM
     return 0;
 #endif
@@ -1628,9 +1686,11 @@ extern "C" int ccjk_ppush(const DevTables *T, int lev, void *stream) {
     const int nch = (nmax + S - 1) / S;
     int npairs = 0;  // (chunk, inner-loop slice) pairs, as k_ppush enumerates them
     for (int c = 0; c < nch; ++c) npairs += (imin((c + 1) * S, nmax) + hs_len - 1) / hs_len;
-    const int blocksA = (npairs * ngrp * (lev + 1) + 3) / 4;
+    const int nout = rank <= lev ? (lev - rank) / G + 1 : 0;  // this rank's outer indices r, r+G, ... <= lev
+    if (nout <= 0) return 0;
+    const int blocksA = (npairs * ngrp * nout + 3) / 4;
     hipLaunchKernelGGL(k_ppush<S>, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp, npairs,
-                       hs_len, blocksA);
+                       hs_len, blocksA, G, rank, nout);
     return (int)hipGetLastError();
 }
 
@@ -1655,7 +1715,7 @@ extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int n
 // Band-sharded exchange of level t.  k_pack: rank r's own cells, all 22 matrices,
 // into one contiguous slice [x][own index][M] of nmax blocks per matrix (nmax = the largest rank's
 // block count at t), so the exchange is ONE all-gather of equal slices.  k_unpack: every cell of the
-// other ranks' blocks from the gathered slices back into the level layout, plus its loop records and
+// other ranks' blocks from the gathered slices (rank r's at recv + r * rstride) back into the level layout, plus its loop records and
 // interior-loop copies (what k_level4d writes for its own cells).  recv == nullptr: the cells are
 // already in the level layout and only their records and copies are rebuilt.
 // ------------------------------------------------------------------------------------------
@@ -1671,7 +1731,7 @@ __global__ __launch_bounds__(256) void k_pack(DevTables T, int t, int G, int r, 
     for (int x = 0; x < NMAT4; ++x) send[((long long)x * nmax + o) * Mt + c] = src[(long long)x * Lt.C];
 }
 
-__global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r, int nmax, const int16_t *recv) {
+__global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r, int nmax, const int16_t *recv, size_t rstride) {
     const int n = T.n, m = n - t - 2, Mt = (m * (m + 1)) >> 1;
     const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const int a = (int)(gc / Mt);
@@ -1694,7 +1754,7 @@ __global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r
     int v[NMAT4];
     if (recv) {
         const int o = shard_count(a - 1, G, ro);  // a's own index on its rank
-        const int16_t *sl = recv + (long long)ro * NMAT4 * nmax * Mt + (long long)o * Mt + c;
+        const int16_t *sl = recv + (size_t)ro * rstride + (long long)o * Mt + c;
 #pragma unroll
         for (int x = 0; x < NMAT4; ++x) {
             v[x] = sl[(long long)x * nmax * Mt];
@@ -1715,6 +1775,44 @@ __global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r
     if (ptype(T, j, k) > 0) T.pmx[X.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = (int16_t)v[PM];
 }
 
+// The P partials of span sigma (each rank pushed only its share of the terms, k_ppush) ride in the
+// tail of the level exchange: k_ptail_pack copies this rank's (value, first split) words of
+// P(i, i+sigma), k_ptail_unpack takes the minimum over the ranks' tails (the same first minimum the
+// atomicMin of an unsharded fill keeps) into T.Pk.
+__global__ __launch_bounds__(256) void k_ptail_pack(DevTables T, int sigma, unsigned long long *tail) {
+    const int i = 1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i + sigma > T.n) return;
+    tail[i] = T.Pk[sigma * T.rs + i];
+}
+__global__ __launch_bounds__(256) void k_ptail_unpack(DevTables T, int sigma, const int16_t *recv, size_t slice, size_t off,
+                                                      int G) {
+    const int i = 1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i + sigma > T.n) return;
+    unsigned long long v = ~0ull;
+    for (int r = 0; r < G; ++r) {
+        const unsigned long long x = ((const unsigned long long *)(recv + (size_t)r * slice + off))[i];
+        v = x < v ? x : v;
+    }
+    T.Pk[sigma * T.rs + i] = v;
+}
+
+extern "C" int ccjk_ptail_pack(const DevTables *T, int sigma, int16_t *tail, void *stream) {
+    const int cnt = T->n - sigma;
+    if (cnt <= 0) return 0;
+    hipLaunchKernelGGL(k_ptail_pack, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, sigma,
+                       (unsigned long long *)tail);
+    return (int)hipGetLastError();
+}
+
+extern "C" int ccjk_ptail_unpack(const DevTables *T, int sigma, const int16_t *recv, size_t slice, size_t off, int G,
+                                 void *stream) {
+    const int cnt = T->n - sigma;
+    if (cnt <= 0) return 0;
+    hipLaunchKernelGGL(k_ptail_unpack, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, sigma, recv,
+                       slice, off, G);
+    return (int)hipGetLastError();
+}
+
 extern "C" int ccjk_pack(const DevTables *T, int t, int G, int r, int nmax, int16_t *send, void *stream) {
     const int m = T->n - t - 2;
     if (m <= 0) return 0;
@@ -1724,11 +1822,13 @@ extern "C" int ccjk_pack(const DevTables *T, int t, int G, int r, int nmax, int1
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_unpack(const DevTables *T, int t, int G, int r, int nmax, const int16_t *recv, void *stream) {
+extern "C" int ccjk_unpack(const DevTables *T, int t, int G, int r, int nmax, const int16_t *recv, size_t rstride,
+                           void *stream) {
     const int m = T->n - t - 2;
     if (m <= 0) return 0;
     const long long cells = (long long)(t + 1) * (m * (m + 1) / 2);
-    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, G, r, nmax, recv);
+    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, G, r, nmax, recv,
+                       rstride);
     return (int)hipGetLastError();
 }
 

@@ -32,6 +32,10 @@ extern "C" {
 #define CCJ_E_BACKTRACK  5   /* reference backtrack would exit(EXIT_FAILURE); message in ccj_last_error() */
 #define CCJ_E_STATE      6   /* call out of order (e.g. ccj_result before ccj_fill) */
 #define CCJ_E_INTER_EXIT 7   /* reference "NOT GOOD RESTR INTER" path: it prints and exit(0) */
+#define CCJ_E_COMM       9   /* band-sharded exchange failed: an RCCL error on the communicator, or no
+                                progress within CCJ_COMM_TIMEOUT_S seconds (default 300; a peer rank
+                                died or hung); the communicator is aborted and the context must be
+                                destroyed */
 
 /* 4-D gap matrices, reference pseudo_loop.hh:62-108 / allocation order pseudo_loop.cc:37-62 */
 enum ccj_mat4 {

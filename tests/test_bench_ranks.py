@@ -85,3 +85,17 @@ def test_gpus_mismatch_fails():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0
+
+
+def test_shard_dry_run_shares_comm_id():
+    """`bench.py --gpus 2 --shard --dry-run`: the sharded path's comm-id hand-off (rank 0 makes the
+    128-byte id, every rank receives it over gloo before ccj_comm_init), with no GPU; one fold per
+    step for the whole job (strong scaling)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--shard", "--steps", "2",
+                        "--dry-run"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["shard"] is True and out["comm_id_agreed"] is True and out["ranks_reported"] == 2
