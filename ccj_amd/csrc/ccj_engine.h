@@ -33,8 +33,6 @@ constexpr int IE_U = 29;  // u1,u2 in [0,28] for pseudoknot interior loops (pseu
 constexpr int IL_B = CCJ_ILB;  // interior-loop candidates per load batch (k_iloop)
 constexpr int IL_CAP = (IE_U * IE_U + IL_B + 7) / 8 * 8;  // candidate-list capacity per pair (+ IL_B null tail)
 constexpr int IL_SEG = 64;   // per pair: seg[dt] = first list entry of source-level distance dt
-constexpr int IT_TI = 8;     // k_iloop: closing pairs per tile (their partner rows are staged once)
-constexpr int IT_PAD = 256;  // elements of padding before and after d4x / pmx (k_iloop stages whole rows)
 
 struct LevelDesc {
     int16_t *base;  // first element of level t (matrix 0)
@@ -160,7 +158,7 @@ struct DevTables {
     // .y = 2*u1*dt (the address cross term); IL_B null entries (dt 63) follow the last one
     uint2 *il, *ilm;               // il: pair (p,p+w) closes the loop (PL, PR); ilm: pair encloses (PM)
     int16_t *dummy;                // n+64 values 32767: target of the null entries
-    const uint32_t *items;         // k_iloop work items (role << 30 | f1 << 20 | tile << 10 | chunk)
+    const uint32_t *items;         // k_iloop work items (role << 30 | f1 << 20 | f2 << 10 | chunk)
     uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
     int *err;                      // device error word
     // split-point sharing (above): levels [g_lo, g_hi) share; partial-record ring of SHARE_R
@@ -201,5 +199,7 @@ int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
 int ccjk_ppush(const ccj::DevTables *T, int lev, int G, int rank, void *stream);
 int ccjk_ptail_pack(const ccj::DevTables *T, int sigma, int16_t *tail, void *stream);
 int ccjk_ptail_unpack(const ccj::DevTables *T, int sigma, const int16_t *recv, size_t slice, size_t off, int G, void *stream);
+int ccjk_items(const ccj::DevTables *T, int G, int rank, int simulate, long long *counts, const long long *offs,
+               uint32_t *items, int pass, void *stream);
 int ccjk_canon(const ccj::DevTables *T, int x, const long long *offij, int16_t *out, void *stream);
 }

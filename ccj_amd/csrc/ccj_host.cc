@@ -143,11 +143,14 @@ struct ccj_ctx {
     uint2 *d_il = nullptr, *d_ilm = nullptr;
     int16_t *d_dummy = nullptr;
     uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
+    size_t items_cap = 0;
     int16_t *d_send = nullptr, *d_recv = nullptr;  // band-sharded exchange: own slice, world slices
     std::vector<int> xnmax;               // per level: the largest rank's block count (slice = 22 x nmax x M)
     ccj_group *lgroup = nullptr;          // in-process exchange between contexts (tests), else RCCL
+    long long *d_icount = nullptr, *d_ioff = nullptr;  // k_items: items per (t, r), first item
+    long long *h_ioff = nullptr;          // pinned staging of it_off
     void *h_stage = nullptr;              // pinned staging of the sequence tables
-    hipEvent_t ev_stage = nullptr;        // the uploads from the staging are done
+    hipEvent_t ev_stage = nullptr;        // the uploads from the staging (and h_ioff) are done
     std::vector<long long> it_off;        // first item of (level t, shard r) at t*world + r
     uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
@@ -1504,6 +1507,78 @@ static int seq_setup(ccj_ctx *c) {
         return e;
     };
     HIPCHK(cp, up(c->d_pt, pt.data(), plane));
+    // ---- k_iloop work items (one per wave), counted per (level, shard), then written by k_items
+    // on the GPU at the prefix offsets.  By default the count pass runs on the GPU too (k_items
+    // pass 0 on st) and the host WAITS for it (hipStreamSynchronize): the offsets are needed on
+    // the host to size the k_iloop launches, so ccj_reset blocks until the context's stream has
+    // run it.  CCJ_HOST_COUNT=1 counts on host threads instead (the same enumeration, ccj_items.h;
+    // slower, ~1.3 ms at n=200, but no device round trip).
+    {
+        if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
+        const int G = c->world;
+        const int nb = n * G;
+        const int rs = c->rs;
+        struct HostPT {
+            const int8_t *pt;
+            int rs;
+            int operator()(int i, int j) const { return pt[(size_t)(j - i) * rs + i]; }
+        } hpt{pt.data(), rs};
+        std::vector<long long> cnt((size_t)nb, 0);
+        // default: counted on the GPU by k_items (0.2 ms + one round trip; 0.5 ms setup at n=200);
+        // CCJ_HOST_COUNT=1: on host threads (≈1 ms, but no device round trip, so a reset never
+        // waits behind another context's fill on a shared hardware queue)
+        static const bool host_count = getenv("CCJ_HOST_COUNT") && atoi(getenv("CCJ_HOST_COUNT")) != 0;
+        if (!host_count) {
+            HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, nullptr, nullptr, 0, c->st));
+            HIPCHK(cp, hipMemcpyAsync(cnt.data(), c->d_icount, nb * sizeof(long long), hipMemcpyDeviceToHost, c->st));
+            HIPCHK(cp, hipStreamSynchronize(c->st));
+        }
+        std::atomic<int> next{0};
+        static const bool check = getenv("CCJ_CHECK_ITEMS") && atoi(getenv("CCJ_CHECK_ITEMS")) != 0;
+        std::atomic<bool> bad{false};
+        auto worker = [&]() {
+            for (int b; (b = next.fetch_add(1)) < nb;) {
+                const int t = b / G, r = b % G;
+                if (!(c->simulate || r == c->rank) || t < 4 || t >= c->nlev) continue;
+                const long long hc = count_level_items(pt.data(), rs, n, t, G, r);
+                if (!host_count && hc != cnt[b]) bad = true;  // check mode: host and GPU counts agree
+                cnt[b] = hc;
+                if (check) {  // CCJ_CHECK_ITEMS=1: the generic enumeration must agree
+                    const ItemRows R = item_rows(n, t, G, r);
+                    long long sum = 0;
+                    uint32_t it0;
+                    for (int x = 0; x < R.nPL + R.nPR + R.nPM; ++x) sum += item_row(hpt, n, t, R, x, G, r, it0);
+                    if (sum != cnt[b]) bad = true;
+                }
+            }
+        };
+        if (host_count || check) {
+            if (!host_count) next = nb;  // check mode only: the GPU counts stay
+            if (check) next = 0;
+            const int nth = std::max(1, std::min<int>(8, (int)std::thread::hardware_concurrency()));
+            std::vector<std::thread> pool;
+            for (int x = 1; x < nth; ++x) pool.emplace_back(worker);
+            worker();
+            for (auto &th : pool) th.join();
+        }
+        if (bad) return set_err(cp, CCJ_E_STATE, "k_iloop item count pass disagrees with the enumeration");
+        c->it_off.assign((size_t)nb + 1, 0);
+        for (int x = 0; x < nb; ++x) c->it_off[x + 1] = c->it_off[x] + cnt[x];
+        const size_t total = (size_t)c->it_off[nb];
+        lap("count");
+        if (total > c->items_cap || !c->d_items) {  // ccj_reset: grow only
+            if (c->d_items) HIPCHK(cp, hipFree(c->d_items));
+            c->d_items = nullptr;
+            c->items_cap = std::max<size_t>(total, 1);
+            HIPCHK(cp, hipMalloc(&c->d_items, c->items_cap * sizeof(uint32_t)));
+        }
+        c->T.items = c->d_items;
+        // pinned staging so the upload is asynchronous on st (the fill's first launches follow it)
+        if (!c->h_ioff) HIPCHK(cp, hipHostMalloc(&c->h_ioff, ((size_t)nb + 1) * sizeof(long long), hipHostMallocDefault));
+        memcpy(c->h_ioff, c->it_off.data(), ((size_t)nb + 1) * sizeof(long long));
+        HIPCHK(cp, hipMemcpyAsync(c->d_ioff, c->h_ioff, (nb + 1) * sizeof(long long), hipMemcpyHostToDevice, c->st));
+        HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, c->d_ioff, c->d_items, 1, c->st));
+    }
     HIPCHK(cp, up(c->d_hp, hp.data(), plane * sizeof(int)));
     HIPCHK(cp, up(c->d_est, est.data(), plane * sizeof(int16_t)));
     HIPCHK(cp, up(c->d_S, c->S.data(), (n + 2) * sizeof(short)));
@@ -1707,16 +1782,14 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
             ox += 2LL * c->lv_host[t].C;
             op += (long long)c->lv_host[t].m * n * (t + 1);
         }
-        // IT_PAD elements before and after each copy: k_iloop stages whole 66-value rows, whose
-        // lanes outside the row read (and never use) neighbouring elements
-        const size_t pad = 2 * IT_PAD;
+        const size_t pad = 256;
         c->nx = ox;
         c->npm = op;
         if (hipMalloc(&c->d4x_alloc, ((size_t)ox + pad) * sizeof(int16_t)) != hipSuccess ||
             hipMalloc(&c->pmx_alloc, ((size_t)op + pad) * sizeof(int16_t)) != hipSuccess)
             return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for interior-loop copies failed", (ox + op) * 2e-9);
-        c->d4x = c->d4x_alloc + IT_PAD;
-        c->pmx = c->pmx_alloc + IT_PAD;
+        c->d4x = c->d4x_alloc;
+        c->pmx = c->pmx_alloc;
         HIPCHK(cp, hipMalloc(&c->d_ldx, ldx.size() * sizeof(LvlX)));
         HIPCHK(cp, hipMemcpy(c->d_ldx, ldx.data(), ldx.size() * sizeof(LvlX), hipMemcpyHostToDevice));
         const size_t pairs = (size_t)(n + 1) * c->rs;
@@ -1831,6 +1904,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.prepass = c->prepass && g_hi > g_lo;
     {
         const int G = c->world;
+        HIPCHK(cp, hipMalloc(&c->d_icount, (size_t)n * G * sizeof(long long)));
+        HIPCHK(cp, hipMalloc(&c->d_ioff, ((size_t)n * G + 1) * sizeof(long long)));
         if (G > 1 && !c->simulate) {
             // exchange slices: per level, 22 matrices x the largest rank's blocks x M
             c->xnmax.assign(n, 0);
@@ -1846,23 +1921,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
                 return set_err(cp, CCJ_E_OOM, "device allocation of the exchange buffers (%.2f GB) failed",
                                slice * (G + 1) * 2e-9);
         }
-    }
-    {
-        // k_iloop work items of every (level, rank) this context launches (ccj_items.h): they depend
-        // only on n and the shard, so they are built once here, not per sequence
-        const int G = c->world;
-        std::vector<uint32_t> items;
-        c->it_off.assign((size_t)n * G + 1, 0);
-        for (int tr = 0; tr < n * G; ++tr) {
-            const int t = tr / G, r = tr % G;
-            c->it_off[tr] = (long long)items.size();
-            if ((c->simulate || r == c->rank) && t < c->nlev) level_iloop_items(n, t, G, r, items);
-        }
-        c->it_off[(size_t)n * G] = (long long)items.size();
-        HIPCHK(cp, hipMalloc(&c->d_items, std::max<size_t>(items.size(), 1) * sizeof(uint32_t)));
-        if (!items.empty())
-            HIPCHK(cp, hipMemcpy(c->d_items, items.data(), items.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        c->T.items = c->d_items;
     }
     if (const int rc = seq_setup(cp)) return rc;
     *out = c.release();
@@ -2693,6 +2751,8 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_lb);
     hipFree(c->d_ld);
     hipFree(c->d4x_alloc);
+    hipFree(c->d_icount);
+    hipFree(c->d_ioff);
     hipFree(c->d_rec);
     hipFree(c->d_acc);
     hipFree(c->d_wterm);
@@ -2708,6 +2768,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_send);
     hipFree(c->d_recv);
     if (c->h_stage) hipHostFree(c->h_stage);
+    if (c->h_ioff) hipHostFree(c->h_ioff);
     if (c->ev_stage) hipEventDestroy(c->ev_stage);
     if (c->hr_W) hipHostFree(c->hr_W);
     if (c->hr_fp) hipHostFree(c->hr_fp);

@@ -1,47 +1,100 @@
-// ccj_items.h — the k_iloop work items of one level and shard.  They depend only
-// on n, the level and the shard (not on the sequence), so ccj_create builds them once.
+// ccj_items.h — enumeration of the k_iloop work items of one level and shard, shared
+// by the GPU builder (k_items, ccj_kernels.hip) and the host's count pass (ccj_host.cc): both must
+// produce the same per-level counts, since the host sizes the k_iloop launches from them.
 //
-// One item = one workgroup = a tile of IT_TI consecutive closing pairs x one 64-lane chunk of the
-// free index (ccj_kernels.hip k_iloop), role << 30 | f1 << 20 | tile << 10 | chunk:
-//   PL (role 0): own a in [6, t]:   pairs (i, i+a), i = 1+IT_TI*tile ... <= m; lanes k from i0+a+2
-//   PR (role 1): own a in [0, t-6]: pairs (k, k+t-a), k = a+3+IT_TI*tile ... <= m+a+2; lanes i from 1
-//   PM (role 2): g in [4, m+1]:     pairs (j, j+g), j = 3+IT_TI*tile ... <= n-g-2; lanes i from
-//                                   max(1, j0-t+2); every rank walks them and stores its own a only
-// with m = n-t-2.  PL/PR with a or b = 6 have no candidates (source levels >= 3 need a, b >= 7)
-// but still store the "no interior loop" value k_level4d reads.
+// A "row" is one closing pair; its items are the 64-lane chunks of the cells that share it:
+//   PL (role 0): for own a in [6, t], i in [1, m]:   pair (i, i+a),  chunks over h <= m-i
+//   PR (role 1): for own a in [0, t-6], q < m:        pair (k, k+t-a), k = q+a+3, chunks over i <= q+1
+//   PM (role 2): for h in [2, m-1], j in [1, n]:      pair (j, k = j+h+2), chunks over the own a in [alo, ahi]
+// ("own": the rank's a-blocks, ccj_engine.h shard_a; every a when unsharded).  An item is
+// role << 30 | f1 << 20 | f2 << 10 | chunk.  pt(i, j) is the pair type of (i, j), 0 = cannot pair.
 #pragma once
-#include <stdint.h>
-#include <vector>
 #include "ccj_energy.h"
 #include "ccj_engine.h"
 
 namespace ccj {
 
-inline void level_iloop_items(int n, int t, int G, int r, std::vector<uint32_t> &out) {
-    const int m = n - t - 2;
-    if (m <= 0 || t < 4) return;  // PM from t = 4 (a, b >= 2), PL / PR from t = 6
-    auto push = [&](uint32_t role, int f1, int tile, int chunks) {
-        for (int c = 0; c < chunks; ++c)
-            out.push_back((role << 30) | ((uint32_t)f1 << 20) | ((uint32_t)tile << 10) | (uint32_t)c);
-    };
-    const int nown = shard_count(t, G, r);
-    for (int o = 0; o < nown; ++o) {  // PL: own a >= 6
-        const int a = shard_a(o, G, r);
-        if (a < 6) continue;
-        for (int x = 0; 1 + IT_TI * x <= m; ++x) push(0, a, x, (m - IT_TI * x + 63) / 64);
+struct ItemRows {
+    int m, oPL0, nPLa, nPRa, nPL, nPR, nPM;
+};
+
+// rows of level t for rank r of G
+CCJ_HD ItemRows item_rows(int n, int t, int G, int r) {
+    ItemRows R;
+    R.m = n - t - 2;
+    R.oPL0 = shard_ceil(6, G, r);
+    R.nPLa = imax(0, shard_count(t, G, r) - R.oPL0);
+    R.nPRa = t >= 6 ? shard_count(t - 6, G, r) : 0;
+    R.nPL = R.nPLa * R.m;
+    R.nPR = R.nPRa * R.m;
+    R.nPM = imax(0, R.m - 2) * n;
+    return R;
+}
+
+// rank r's a-blocks of a PM pair (j, k = j+h+2) at level t: own indices [o0, o1]
+CCJ_HD void pm_own_range(int n, int t, int j, int k, int G, int r, int &o0, int &o1) {
+    const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, j - 1);
+    o0 = shard_ceil(alo, G, r);
+    o1 = ahi >= alo ? shard_count(ahi, G, r) - 1 : o0 - 1;
+}
+
+// items of row x and the first of them (chunk 0); 0 when the pair cannot pair
+template <class PT>
+CCJ_HD int item_row(const PT &pt, int n, int t, const ItemRows &R, int x, int G, int r, uint32_t &it0) {
+    const int m = R.m;
+    if (x < R.nPL) {
+        const int a = shard_a(R.oPL0 + x / m, G, r), i = 1 + x % m;
+        it0 = (0u << 30) | ((uint32_t)a << 20) | ((uint32_t)i << 10);
+        return pt(i, i + a) > 0 ? (m - i) / 64 + 1 : 0;
     }
-    for (int o = 0; o < nown; ++o) {  // PR: own a with b = t-a >= 6
-        const int a = shard_a(o, G, r);
-        if (t - a < 6) continue;
-        for (int x = 0; IT_TI * x < m; ++x) push(1, a, x, (imin(IT_TI * (x + 1), m) + 63) / 64);
+    x -= R.nPL;
+    if (x < R.nPR) {
+        const int a = shard_a(x / m, G, r), q = x % m;
+        const int k = q + a + 3, b = t - a;
+        it0 = (1u << 30) | ((uint32_t)a << 20) | ((uint32_t)q << 10);
+        return pt(k, k + b) > 0 ? q / 64 + 1 : 0;
     }
-    for (int g = 4; g <= m + 1; ++g) {  // PM
-        for (int x = 0; 3 + IT_TI * x <= n - g - 2; ++x) {
-            const int j0 = 3 + IT_TI * x;
-            const int ilo = imax(1, j0 - t + 2), ihi = imin(j0 + IT_TI - 3, n - g - t);
-            if (ihi >= ilo) push(2, g, x, (ihi - ilo + 1 + 63) / 64);
+    x -= R.nPR;
+    const int h = 2 + x / n, j = 1 + x % n;
+    const int k = j + h + 2;
+    if (k > n) return 0;
+    int o0, o1;
+    pm_own_range(n, t, j, k, G, r, o0, o1);
+    if (o0 > o1 || pt(j, k) <= 0) return 0;
+    it0 = (2u << 30) | ((uint32_t)h << 20) | ((uint32_t)j << 10);
+    return (o1 - o0) / 64 + 1;
+}
+
+// The same count as summing item_row over every row of the level, with the rows walked in tight
+// loops over contiguous pair-type rows (host count pass of ccj_reset: ~10x faster).  pt is the
+// [w][p] pair-type table with row stride rs.
+inline long long count_level_items(const int8_t *pt, int rs, int n, int t, int G, int r) {
+    const ItemRows R = item_rows(n, t, G, r);
+    const int m = R.m;
+    long long cnt = 0;
+    for (int o = R.oPL0; o < R.oPL0 + R.nPLa; ++o) {  // PL: pair (i, i+a)
+        const int a = shard_a(o, G, r);
+        const int8_t *row = pt + (size_t)a * rs;
+        for (int i = 1; i <= m; ++i)
+            if (row[i] > 0) cnt += (m - i) / 64 + 1;
+    }
+    for (int o = 0; o < R.nPRa; ++o) {  // PR: pair (k, k+b), k = q+a+3
+        const int a = shard_a(o, G, r), b = t - a;
+        const int8_t *row = pt + (size_t)b * rs + a + 3;
+        for (int q = 0; q < m; ++q)
+            if (row[q] > 0) cnt += q / 64 + 1;
+    }
+    for (int h = 2; h <= m - 1; ++h) {  // PM: pair (j, k = j+h+2)
+        const int g = h + 2;
+        const int8_t *row = pt + (size_t)g * rs;
+        for (int j = 1; j + g <= n; ++j) {
+            if (row[j] <= 0) continue;
+            int o0, o1;
+            pm_own_range(n, t, j, j + g, G, r, o0, o1);
+            if (o0 <= o1) cnt += (o1 - o0) / 64 + 1;
         }
     }
+    return cnt;
 }
 
 }  // namespace ccj

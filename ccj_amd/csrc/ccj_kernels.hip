@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include "ccj_engine.h"
 #include "ccj_energy.h"
+#include "ccj_items.h"
 
 using namespace ccj;
 
@@ -319,6 +320,13 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
     }
 }
 
+// readlane of a 64-bit value (two 32-bit readlanes)
+__device__ __forceinline__ unsigned long long rdl64(unsigned long long v, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 // ------------------------------------------------------------------------------------------
 // P(i, i+sigma) = min over i<=j<d<k<l of PK(i,j,d+1,k) + PK(j+1,d,k+1,l)   (pseudo_loop.cc:166-179),
 // pushed by level.  A term of P(i, i+sigma) reads A = PK(i,j,d+1,k) at level t1 = jo+(ko-do-1) and
@@ -572,276 +580,407 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Interior loops of level t (get_PLiloop / get_PRiloop / get_PMiloop, pseudo_loop.cc:682-773),
-// tiled so that a partner value is loaded once for every closing pair of a tile that reads it.
-//
-// For a fixed source level t' = t - dt the interior loops of one role are a 1-D min-plus sweep:
-//   PL  closing pair (i, i+a), cell (i,j,k,l):   min over u1 of E(i,u1,u2) + PL(i+1+u1, ., k, l)
-// (u2 = dt-2-u1), and the partner row d = i+1+u1 (inner pair (d, d+a-dt)) is read by every
-// closing pair i = d-1-u1 of the same (a, k, l).  A workgroup takes a TILE of IT_TI consecutive
-// closing pairs and 64 lanes of the free index (PL: lanes k; PR: tile along k, lanes i; PM: tile
-// along j at fixed gap g, lanes i).  Its four waves take the source levels dt = 3+w, 7+w, ... and
-//   1. mark the partner rows whose pair can pair (the only ones a candidate reads: the reference's
-//      can_pair filter), one ballot per source level;
-//   2. stage those rows from the PLx/PRx/PMx copy into LDS with LDS-DMA loads (global_load_lds_dword,
-//      no VGPR destination: 33 lanes move one 64-value row from its dword-aligned start, the parity
-//      kept per slot; the ushort form writes a dword per lane, twice the LDS), the rows of several
-//      source levels in flight together, compacted to the pairable ones;
-//   3. walk every candidate (set bits of the row mask in each pair's window) as
-//      min(E + LDS[row][lane]), E from the tile's interior-loop energies (staged once per
-//      workgroup from the e_intP table), and min-reduce the waves through LDS at the end.
-// The candidate (u1, u2) = (0, 0) (source level t-2) reads the stack term's inner cell, so
-// k_level4d(t) evaluates it; k_iloop(t) needs levels <= t-3 only.  The minimum (clamped like a store)
-// goes into the cell's own PL / PR / PM slot of level t, where k_level4d(t) picks it up.
-// (Round 2's form — one wave per closing pair, every candidate's partner loaded from L2 / MALL —
-// moved 1.44x the algorithmic bytes at 0.14 of the HBM roofline.)
-//
-// Work items (ccj_create, sequence-independent; ccj_items.h): one per (role, a or g, tile, 64-lane
-// chunk) of the rank's own a-blocks, role << 30 | f1 << 20 | tile << 10 | chunk.
+// k_iloop work items, built on the GPU once per sequence (ccj_create / ccj_reset).  One wave of
+// k_iloop per item; an item is a closing pair that can pair plus a 64-lane chunk of the cells that
+// share it (role << 30 | f1 << 20 | f2 << 10 | chunk):
+//   PL (role 0): for own a in [6, t], i in [1, m]:   pair (i, i+a),  chunks over h <= m-i
+//   PR (role 1): for own a in [0, t-6], q < m:        pair (k, k+t-a), k = q+a+3, chunks over i <= q+1
+//   PM (role 2): for h in [2, m-1], j in [1, n]:      pair (j, k = j+h+2), chunks over the own a in [alo, ahi]
+// ("own": the rank's a-blocks, ccj_engine.h shard_a; every a when unsharded)
+// in this enumeration order (measured no slower than heaviest-list-first).  One workgroup per
+// (level t, shard r) walks its "rows" (one closing pair each) 256 at a time; pass 0 counts the
+// items, pass 1 writes them at offs[t*G+r] + an exclusive scan of the row counts.
 // ------------------------------------------------------------------------------------------
-constexpr int IT_W = 4;                    // waves per tile: source levels interleaved over them
-constexpr int IT_RB = 48;                  // LDS partner-row slots per wave (>= IT_TI + IE_U - 1)
-constexpr int IT_RW = 68;                  // int16 per row slot: 66 staged (33 dwords) + pad to 8 B
-constexpr int IT_NQ = 16;                  // source levels per wave, at most ceil(56 / IT_W)
-constexpr int IT_NE = IE_U * IE_U;         // (u1, u2) energies per closing pair
-static_assert(IT_RB >= IT_TI + IE_U - 1, "one source level's rows must fit");
+// the row enumeration (ItemRows, item_row) is shared with the host's count pass: ccj_items.h
+struct DevPT {
+    const DevTables *T;
+    __device__ int operator()(int i, int j) const { return ptype(*T, i, j); }
+};
 
+__global__ __launch_bounds__(256) void k_items(DevTables T, int G, int rank, int simulate,
+                                               long long *counts, const long long *__restrict__ offs, uint32_t *items,
+                                               int pass) {
+    __shared__ int wsum[4];
+    __shared__ long long tot;
+    const int b = blockIdx.x, t = b / G, r = b - t * G;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const bool mine = simulate || r == rank;
+    if (!mine || t < 4 || t >= T.nlev) {
+        if (pass == 0 && tid == 0) counts[b] = 0;
+        return;  // whole workgroup
+    }
+    const ItemRows R = item_rows(T.n, t, G, r);
+    const DevPT pt{&T};
+    const int nrows = R.nPL + R.nPR + R.nPM;
+    long long base = pass ? offs[b] : 0;
+    for (int c0 = 0; c0 < nrows; c0 += 256) {
+        const int x = c0 + tid;
+        uint32_t it0 = 0;
+        const int cnt = x < nrows ? item_row(pt, T.n, t, R, x, G, r, it0) : 0;
+        // exclusive scan of cnt over the workgroup: wave scan, then the wave totals
+        int inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        int before = 0;
+        for (int v = 0; v < w; ++v) before += wsum[v];
+        const int chunk_total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (pass) {
+            const long long pos = base + before + inc - cnt;
+            for (int c = 0; c < cnt; ++c) items[pos + c] = it0 | (uint32_t)c;
+        }
+        base += chunk_total;
+        __syncthreads();  // wsum is rewritten by the next chunk
+    }
+    if (pass == 0 && tid == 0) {
+        tot = base;
+        counts[b] = tot;
+    }
+}
+
+extern "C" int ccjk_items(const DevTables *T, int G, int rank, int simulate, long long *counts, const long long *offs,
+                          uint32_t *items, int pass, void *stream) {
+    const int blocks = T->n * G;
+    if (blocks <= 0) return 0;
+    hipLaunchKernelGGL(k_items, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *T, G, rank, simulate, counts,
+                       offs, items, pass);
+    return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Interior loops of level t (get_PLiloop / get_PRiloop / get_PMiloop, pseudo_loop.cc:682-773).
+// One wave per closing pair and run of cells sharing it, so the pair test, the candidate list and
+// the loop energies are wave-uniform (scalar loads) and only candidates whose inner pair can pair
+// are visited; the partner value comes from the PLx/PRx/PMx copy, contiguous along the lanes.
+//   PL: wave = (a, i, h-chunk), lanes h  — closing pair (i, j)
+//   PR: wave = (a, q, i-chunk), lanes i  — closing pair (k, l), q = i+h-1 = k-a-3
+//   PM: wave = (h, j, a-chunk), lanes a  — pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
+// The minimum (clamped like a store) goes into the cell's PL/PR/PM slot of level t, where
+// k_level4d(t) picks it up.  The candidate with no unpaired base (u1 = u2 = 0, source level t-2)
+// reads the same inner cell as the stack term, so k_level4d(t) evaluates it there; k_iloop(t)
+// walks the lists from dt = 3 on and needs levels <= t-3 only, a whole level of slack.
+// ------------------------------------------------------------------------------------------
+// Each list entry's partner address is A[dt] + B[u1] (+ 2*u1*dt for PL/PM) bytes + the lane's
+// offset: A (64-bit, per source level) and B (per u1) are per-wave tables held one value per lane
+// and fetched with readlane, so an entry costs a few scalar ops and one load on a uniform base.
+// IL_B entries are loaded together (one s_load burst), then IL_B partner values, then reduced.
+// Null tail entries (dt 63) hit T.dummy, so the last batch needs no masking (PL/PR: cnt is the
+// whole list; PM stops early and substitutes null entries).
+__device__ __forceinline__ int il_u1(uint32_t x) { return (int)((x >> 16) & 31u); }
+__device__ __forceinline__ int il_dt(uint32_t x) { return (int)(x >> 21); }
+__device__ __forceinline__ int il_e(uint32_t x) { return (int)(int16_t)(x & 0xffffu); }
+
+// min over the wave's candidate list of energy + partner value (PL/PR/PM interior loops).
+// Software-pipelined one batch deep: the entries and partner loads of batch k+1 are issued before
+// batch k is reduced, so a wave keeps 2*IL_B partner loads in flight.
+template <bool CROSS, bool PMWIN>
+__device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restrict__ ent, int cnt,
+                                       unsigned long long Atab, int Btab, unsigned lofs2, int as, int bs) {
+    int b1 = INF;
+    if (cnt <= 0) return b1;
+    auto fetch = [&](int e0, uint2 *E) {
+        const uint2 *ep = ent + e0;
+#pragma unroll
+        for (int u = 0; u < IL_B; ++u) {
+            E[u] = ep[u];
+            // PM stops at dt <= t-2, before the list's null tail: past cnt, substitute a null entry
+            if (PMWIN && e0 + u >= cnt) E[u] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0u);
+        }
+    };
+    auto issue = [&](const uint2 *E, int *v) {
+#pragma unroll
+        for (int u = 0; u < IL_B; ++u) {
+            const int dt = il_dt(E[u].x), u1 = il_u1(E[u].x);
+            unsigned off = (unsigned)__builtin_amdgcn_readlane(Btab, u1);
+            if (CROSS) off += E[u].y;
+            const char *p = (const char *)(rdl64(Atab, dt) + off);
+#ifdef CCJ_DEBUG_BOUNDS
+            {   // the partner must lie inside its copy (or be the null target)
+                const int16_t *q = (const int16_t *)(p + lofs2);
+                const bool in = (q >= T.d4x && q < T.d4x + T.nx) || (q >= T.pmx && q < T.pmx + T.npm) ||
+                                (q >= T.dummy && q < T.dummy + T.n + 64);
+                if (!in || (dt != 63 && (dt < 2 || dt > 2 * MAXLOOP - 2))) {
+                    if (atomicOr(T.err, 64) == 0)
+                        printf("k_iloop OOB: dt %d u1 %d off %u lofs2 %u p-d4x %lld p-pmx %lld p-dummy %lld\n", dt, u1,
+                               off, lofs2, (long long)(q - T.d4x), (long long)(q - T.pmx), (long long)(q - T.dummy));
+                    v[u] = 0;
+                    continue;
+                }
+            }
+#endif
+            // global address space: a plain pointer rebuilt from an integer would become a flat load
+            v[u] = *(const __attribute__((address_space(1))) int16_t *)(p + lofs2);
+        }
+    };
+    auto reduce = [&](const uint2 *E, const int *v) {
+#pragma unroll
+        for (int u = 0; u < IL_B; ++u) {
+            const int c = il_e(E[u].x) + v[u];
+            if (PMWIN) {
+                const int u1 = il_u1(E[u].x), u2 = il_dt(E[u].x) - 2 - u1;
+                // get_PMiloop: d > i, dp < l.  Branch-free (a select of constants): a branch here
+                // splits the loop body, and the compiler then sign-extends the next batch's loads
+                // in the latch, draining every load before the back-edge
+                b1 = imin(b1, c + (((u1 > as - 2) | (u2 > bs - 2)) ? INF : 0));
+            } else {
+                b1 = imin(b1, c);
+            }
+        }
+    };
+    // Ping-pong buffers, two batches per trip: a batch's registers are written only after the
+    // batch they replace was reduced, so the loop carries no register copies.  (With one buffer
+    // and a copy per trip, the copy of a just-issued load made the compiler wait for every load
+    // before the back-edge: one full memory latency per batch instead of overlapped batches.)
+    uint2 Ea[IL_B], Eb[IL_B];
+    int va[IL_B], vb[IL_B];
+    fetch(0, Ea);
+    issue(Ea, va);
+    int e0 = IL_B;
+#pragma unroll 1
+    while (true) {
+        if (e0 >= cnt) {
+            reduce(Ea, va);
+            break;
+        }
+        fetch(e0, Eb);
+        issue(Eb, vb);
+        reduce(Ea, va);
+        e0 += IL_B;
+        if (e0 >= cnt) {
+            reduce(Eb, vb);
+            break;
+        }
+        fetch(e0, Ea);
+        issue(Ea, va);
+        reduce(Eb, vb);
+        e0 += IL_B;
+    }
+    return b1;
+}
+
+// The same minimum for a wave whose row has at most 32 cells: the wave is G groups of W lanes
+// (il_groups), each group holding the whole row and walking every G-th list entry (entry
+// e0+g+G*u), so the list takes 1/G of the iterations; the groups are min-reduced at the end
+// (lanes rl, rl+W, ..., rl+(G-1)W; rl unused with power-of-two W).  The
+// entry is per lane here, so the A/B tables are read with ds_bpermute instead of readlane.  All 64
+// lanes run the scan (bpermute sources must be live).
+__device__ __forceinline__ int bperm(int v, int l) { return __builtin_amdgcn_ds_bpermute(l << 2, v); }
+
+#ifndef CCJ_ILG_B
+#define CCJ_ILG_B 4
+#endif
+constexpr int ILG_B = CCJ_ILG_B;  // entries per lane per batch in the grouped walk (registers: 8 waves/SIMD)
+template <bool CROSS, bool PMWIN>
+__device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__restrict__ ent, int cnt, unsigned long long Atab, int Btab,
+                                         unsigned lofs2, int as, int bs, int G, int W, int g, int rl) {
+    int b1 = INF;
+    if (cnt <= 0) return b1;
+    const int alo = (int)(unsigned)Atab, ahi = (int)(unsigned)(Atab >> 32);
+    // only the packed word is loaded (the cross term 2*u1*dt is recomputed): half the registers
+    const uint32_t nul = (63u << 21) | (uint32_t)INTERN_INF;
+    auto fetch = [&](int e0, uint32_t *E) {
+#pragma unroll
+        for (int u = 0; u < ILG_B; ++u) {
+            const int e = e0 + g + G * u;
+            E[u] = ent[imin(e, cnt - 1)].x;
+            if (e >= cnt) E[u] = nul;
+        }
+    };
+    auto issue = [&](const uint32_t *E, int *v) {
+#pragma unroll
+        for (int u = 0; u < ILG_B; ++u) {
+            const int dt = il_dt(E[u]), u1 = il_u1(E[u]);
+            unsigned off = (unsigned)bperm(Btab, u1);
+            if (CROSS) off += (unsigned)(2 * u1 * dt);
+            const unsigned long long A = ((unsigned long long)(unsigned)bperm(ahi, dt) << 32) | (unsigned)bperm(alo, dt);
+#ifdef CCJ_DEBUG_BOUNDS
+            {
+                const int16_t *q = (const int16_t *)((const char *)(A + off) + lofs2);
+                const bool in = (q >= T.d4x && q < T.d4x + T.nx) || (q >= T.pmx && q < T.pmx + T.npm) ||
+                                (q >= T.dummy && q < T.dummy + T.n + 64);
+                if (!in || (dt != 63 && (dt < 2 || dt > 2 * MAXLOOP - 2))) {
+                    if (atomicOr(T.err, 64) == 0) printf("k_iloop (grouped, G %d) OOB: dt %d u1 %d\n", G, dt, u1);
+                    v[u] = 0;
+                    continue;
+                }
+            }
+#endif
+            v[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)(A + off) + lofs2);
+        }
+    };
+    auto reduce = [&](const uint32_t *E, const int *v) {
+#pragma unroll
+        for (int u = 0; u < ILG_B; ++u) {
+            const int c = il_e(E[u]) + v[u];
+            if (PMWIN) {
+                const int u1 = il_u1(E[u]), u2 = il_dt(E[u]) - 2 - u1;
+                b1 = imin(b1, c + (((u1 > as - 2) | (u2 > bs - 2)) ? INF : 0));
+            } else {
+                b1 = imin(b1, c);
+            }
+        }
+    };
+    // Ping-pong as in il_scan, with the (per-lane, vector-memory) entries loaded one batch ahead:
+    // loads return in order, so waiting for batch k+1's entries also waits for batch k's partners;
+    // issuing k+1's partners together with k+2's entries keeps two loads per lane in flight
+    // across each wait instead of one.
+    uint32_t Ea[ILG_B], Eb[ILG_B];
+    int va[ILG_B], vb[ILG_B];
+    const int stepE = G * ILG_B;
+    fetch(0, Ea);
+    issue(Ea, va);
+    fetch(stepE, Eb);
+    int e0 = stepE;
+#pragma unroll 1
+    while (true) {
+        if (e0 >= cnt) {
+            reduce(Ea, va);
+            break;
+        }
+        issue(Eb, vb);
+        reduce(Ea, va);
+        fetch(e0 + stepE, Ea);
+        e0 += stepE;
+        if (e0 >= cnt) {
+            reduce(Eb, vb);
+            break;
+        }
+        issue(Ea, va);
+        reduce(Eb, vb);
+        fetch(e0 + stepE, Eb);
+        e0 += stepE;
+    }
+    for (int off = W; off < 64; off <<= 1) b1 = imin(b1, __shfl_xor(b1, off));
+    return b1;
+}
+
+// Lane groups for a row of nact cells: W lanes per group (one per cell, W >= nact, a power of two
+// >= 8), G = 64/W groups; lane = gq*W + rl.  Rows above 32 cells keep one group (the scalar list
+// walk).  (Groups of exactly nact lanes, W not a power of two, measured the same.)
+struct ILGroups { int G, W, gq, rl; };
+__device__ __forceinline__ ILGroups il_groups(int nact, int lane) {
+    const int W = nact > 32 ? 64 : nact > 16 ? 32 : nact > 8 ? 16 : 8;
+    return {64 / W, W, lane / W, lane & (W - 1)};
+}
+
+// one wave per work item (host-built list for level t: closing pairs that can pair, heaviest first)
 __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long first, int nitems, int G_SH, int rank) {
-    __shared__ int16_t en_s[IT_NE * IT_TI];             // [(u1*29+u2)*IT_TI + p]
-    __shared__ int16_t rows_s[IT_W][IT_RB][IT_RW];      // staged partner rows, per wave
-    __shared__ unsigned long long msk_s[IT_W][IT_NQ];    // pairable-row mask of each source level
-    typedef const __attribute__((address_space(1))) int16_t gshort;
     const int n = T.n, rs = T.rs, m = n - t - 2;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if ((int)blockIdx.x >= nitems) return;  // whole workgroup
-    const uint32_t it = T.items[first + blockIdx.x];
-    const int role = (int)(it >> 30), f1 = (int)((it >> 20) & 1023u), tx = (int)((it >> 10) & 1023u);
-    const int chunk = (int)(it & 1023u);
-    int a = 0, b = 0, g = 0, p0 = 0, lv = 0, dtmax = 0, pw = 0;
-    if (role == 0) {         // PL: closing pairs (i, i+a), i = p0+p; lanes k
-        a = f1; b = t - a; pw = a;
-        p0 = 1 + IT_TI * tx;
-        lv = p0 + a + 2 + 64 * chunk + lane;
-        dtmax = imin(imin(a - 4, 2 * (IE_U - 1) + 2), t);
-    } else if (role == 1) {  // PR: closing pairs (k, k+b), k = p0+p; lanes i
-        a = f1; b = t - a; pw = b;
-        p0 = a + 3 + IT_TI * tx;
-        lv = 1 + 64 * chunk + lane;
-        dtmax = imin(imin(b - 4, 2 * (IE_U - 1) + 2), t);
-    } else {                 // PM: enclosed pairs (j, j+g), j = p0+p; lanes i
-        g = f1; pw = g;
-        p0 = 3 + IT_TI * tx;
-        lv = imax(1, p0 - t + 2) + 64 * chunk + lane;
-        dtmax = imin(t - 2, 2 * (IE_U - 1) + 2);
-    }
-    // the tile's pairs with some cell that can pair
-    bool pv = false;
-    if (lane < IT_TI) {
-        const int q = p0 + lane;
-        if (role == 0) pv = q <= m && ptype(T, q, q + a) > 0;
-        else if (role == 1) pv = q <= m + a + 2 && ptype(T, q, q + b) > 0;
-        else pv = q <= n - g - 2 && ptype(T, q, q + g) > 0;
-    }
-    const unsigned pmask = (unsigned)__ballot(pv);
-    if (!pmask) return;  // whole workgroup (the ballot is the same in every wave)
-
-    // ---- phase A: the tile's energies (whole workgroup) and this wave's pairable-row masks
-    //   PL: E = IE[u1][u2][a][i];   PR: E = IE[u1][u2][b][k];   PM: E = IE[u1][u2][g+dt][j-1-u1]
-    //   (the outer pair's span and start; k_precompute_ie, pseudo_loop.cc:822-840)
-    constexpr int EPT = (IT_NE * IT_TI + 255) / 256;
-    int ev[EPT];
-#pragma unroll
-    for (int x = 0; x < EPT; ++x) {
-        const int idx = tid + 256 * x;
-        ev[x] = 0;
-        if (idx < IT_NE * IT_TI) {
-            const int uu = idx / IT_TI, p = idx - uu * IT_TI;
-            const int u1 = uu / IE_U, u2 = uu - u1 * IE_U;
-            int ew = pw, ep = p0 + p;
-            if (role == 2) { ew = g + u1 + u2 + 2; ep = p0 + p - 1 - u1; }
-            ew = imin(ew, n);
-            ep = imin(imax(ep, 0), rs - 1);  // outside the tile's valid candidates: any in-range entry
-            ev[x] = T.ie[((size_t)uu * (n + 1) + ew) * rs + ep];
-        }
-    }
-    unsigned long long rmv[IT_NQ];
-    int nq = 0;
-#pragma unroll
-    for (int q = 0; q < IT_NQ; ++q) {
-        const int dt = 3 + w + IT_W * q;
-        bool rv = false;
-        if (dt <= dtmax) {
-            nq = q + 1;
-            const int u1lo = imax(0, dt - 2 - (IE_U - 1)), u1hi = imin(IE_U - 1, dt - 2);
-            if (lane < IT_TI + u1hi - u1lo) {
-                // row r: PL d = p0+1+u1lo+r, pair (d, d+a-dt); PR d = p0+1+u1lo+r, (d, d+b-dt);
-                //        PM d = p0-1-u1hi+r, (d, d+g+dt)
-                if (role == 0) {
-                    const int d = p0 + 1 + u1lo + lane;
-                    rv = d <= m + dt && ptype(T, d, d + a - dt) > 0;
-                } else if (role == 1) {
-                    const int d = p0 + 1 + u1lo + lane;
-                    rv = d + b - dt <= n && ptype(T, d, d + b - dt) > 0;
-                } else {
-                    const int d = p0 - 1 - u1hi + lane;
-                    rv = d >= 1 && d + g + dt <= n && ptype(T, d, d + g + dt) > 0;
-                }
-            }
-        }
-        rmv[q] = __ballot(rv);
-    }
-#pragma unroll
-    for (int x = 0; x < EPT; ++x) {
-        const int idx = tid + 256 * x;
-        if (idx < IT_NE * IT_TI) en_s[idx] = (int16_t)ev[x];
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < IT_NQ; ++q) msk_s[w][q] = rmv[q];
-    }
-    __syncthreads();
-
-    // per pair: the lane's cell, its validity and (PM) its loop-window bounds
-    int acc[IT_TI];
-    bool cv[IT_TI];
-    int pa2[IT_TI], pb2[IT_TI];  // PM: u1 <= a-2, u2 <= b-2
-#pragma unroll
-    for (int p = 0; p < IT_TI; ++p) {
-        acc[p] = INF;
-        const int q = p0 + p;
-        pa2[p] = pb2[p] = 0;
-        if (role == 0) {
-            const int h = lv - q - a - 2;  // k = j+2+h
-            cv[p] = h >= 0 && h <= m - q;
-        } else if (role == 1) {
-            const int h = q - lv - a - 2;  // k = i+a+2+h
-            cv[p] = lv >= 1 && h >= 0 && lv <= m - h;
-        } else {
-            const int aa = q - lv, bb = t - aa;  // a = j-i
-            cv[p] = lv >= 1 && aa >= 2 && bb >= 2 && g + t + lv <= n && (G_SH == 1 || shard_owner(aa, G_SH) == rank);
-            pa2[p] = aa - 2;
-            pb2[p] = bb - 2;
-        }
-    }
-    int16_t *const rbase = &rows_s[w][0][0];
-    // ---- phase B: groups of source levels whose compacted rows fit in the wave's IT_RB slots
-#pragma unroll 1
-    for (int q0 = 0; q0 < nq;) {
-        // plan: source levels q0 .. q1-1, slot bases sb
-        int q1 = q0, used = 0;
-        while (q1 < nq) {
-            const int c = __popcll(msk_s[w][q1]);
-            if (used + c > IT_RB) break;
-            used += c;
-            ++q1;
-        }
-        // issue every row of the group: one LDS-DMA dword load per row (lanes 0..32, the row's
-        // 64 values from its dword-aligned start; LDS gets base + 4*lane), parity bit per slot
-        int slot = 0;
-        unsigned long long odd = 0;
-        const int lv0 = lv - lane;  // lane 0's free index
-#pragma unroll 1
-        for (int q = q0; q < q1; ++q) {
-            const int dt = 3 + w + IT_W * q;
-            const int u1lo = imax(0, dt - 2 - (IE_U - 1)), u1hi = imin(IE_U - 1, dt - 2);
-            const int ts = t - dt, ms = m + dt;
-            const LvlDev Ls = T.ld[ts];
-            const LvlX Xs = T.ldx[ts];
-            unsigned long long rm = msk_s[w][q];
-#pragma unroll 1
-            while (rm) {
-                const int r = __builtin_ctzll(rm);
-                rm &= rm - 1;
-                long long e0;  // element of the row's lowest staged value (lane 0, or lane 63 for PM)
-                if (role == 0) {
-                    const int d = p0 + 1 + u1lo + r, as = a - dt;
-                    e0 = Xs.lbx + (long long)as * Ls.M + (long long)(d - 1) * ms - (((long long)(d - 1) * (d - 2)) >> 1) +
-                         (lv0 - d - as - 2);
-                } else if (role == 1) {
-                    const int d = p0 + 1 + u1lo + r, qs = d - a - 3;
-                    e0 = Xs.lbx + Ls.C + (long long)a * Ls.M + (((long long)qs * (qs + 1)) >> 1) + lv0 - 1;
-                } else {
-                    const int d = p0 - 1 - u1hi + r, hs = g + dt - 2;
-                    e0 = Xs.pmb + ((long long)hs * n + d - 1) * (ts + 1) + (d - lv0) - 63;  // lanes read downwards
-                }
-                const long long ea = e0 & ~1ll;
-                odd |= (unsigned long long)(e0 & 1) << slot;
-#ifdef CCJ_DEBUG_BOUNDS
-                if (ea < -IT_PAD || ea + 66 > (role == 2 ? T.npm : T.nx) + IT_PAD) {
-                    if (atomicOr(T.err, 64) == 0) printf("k_iloop OOB: role %d t %d dt %d r %d e %lld\n", role, t, dt, r, ea);
-                } else
-#endif
-                if (lane <= 32)
-                    __builtin_amdgcn_global_load_lds((gshort *)((role == 2 ? T.pmx : T.d4x) + ea + 2 * lane),
-                                                     (__attribute__((address_space(3))) void *)(rbase + slot * IT_RW), 4, 0, 0);
-                ++slot;
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // the group's candidates
-        int sb = 0;
-#pragma unroll 1
-        for (int q = q0; q < q1; ++q) {
-            const int dt = 3 + w + IT_W * q;
-            const int u1lo = imax(0, dt - 2 - (IE_U - 1)), u1hi = imin(IE_U - 1, dt - 2);
-            const unsigned long long rm = msk_s[w][q];
-            const unsigned long long cm = (1ull << (u1hi - u1lo + 1)) - 1;
-#pragma unroll
-            for (int p = 0; p < IT_TI; ++p) {
-                if (!((pmask >> p) & 1u)) continue;
-                unsigned long long cand = (rm >> p) & cm;  // bit c: row p+c
-                int best = acc[p];
-#pragma unroll 1
-                while (cand) {
-                    const int c = __builtin_ctzll(cand);
-                    cand &= cand - 1;
-                    const int r = p + c;
-                    const int u1 = role == 2 ? u1hi - c : u1lo + c, u2 = dt - 2 - u1;
-                    const int sl = sb + __popcll(rm & ((1ull << r) - 1));
-                    const int o = (int)((odd >> sl) & 1ull);
-                    int v = (int)en_s[(u1 * IE_U + u2) * IT_TI + p] + (int)rbase[sl * IT_RW + o + (role == 2 ? 63 - lane : lane)];
-                    if (role == 2) v += ((u1 > pa2[p]) | (u2 > pb2[p])) ? INF : 0;  // get_PMiloop: d > i, dp < l
-                    best = imin(best, v);
-                }
-                acc[p] = best;
-            }
-            sb += __popcll(rm);
-        }
-        q0 = q1;
-    }
-    // the waves' partial minima meet in wave 0 (each wave's own row region holds its values)
-    __syncthreads();  // every wave is done reading its rows
-    int *red = (int *)rbase;
-    if (w > 0) {
-#pragma unroll
-        for (int p = 0; p < IT_TI; ++p) red[p * 64 + lane] = acc[p];
-    }
-    __syncthreads();
-    if (w > 0) return;
-#pragma unroll
-    for (int v = 1; v < IT_W; ++v) {
-        const int *o = (const int *)&rows_s[v][0][0];
-#pragma unroll
-        for (int p = 0; p < IT_TI; ++p) acc[p] = imin(acc[p], o[p * 64 + lane]);
-    }
+    const int lane = threadIdx.x & 63;
+    const int w = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (w >= nitems) return;
+    const uint32_t it = T.items[first + w];
+    const int role = (int)(it >> 30), f1 = (int)((it >> 20) & 1023u), f2 = (int)((it >> 10) & 1023u);
+    const int zc = (int)(it & 1023u);
     const LvlDev Lt = T.ld[t];
-    int16_t *dst = T.d4 + Lt.lb + (long long)(role == 0 ? PL : role == 1 ? PR : PM) * Lt.C;
-#pragma unroll
-    for (int p = 0; p < IT_TI; ++p) {
-        if (!((pmask >> p) & 1u) || !cv[p]) continue;
-        const int q = p0 + p;
-        int ca, ch, ci;  // cell (a, h, i) of level t
-        if (role == 0) { ca = a; ch = lv - q - a - 2; ci = q; }
-        else if (role == 1) { ca = a; ch = q - lv - a - 2; ci = lv; }
-        else { ca = q - lv; ch = g - 2; ci = lv; }
+    const int tl = t - lane;  // A-table lane L describes source level t-L (dt = L)
+    const bool lvl_ok = lane >= 2 && lane <= 2 * MAXLOOP - 2 && tl >= 0;
+    const long long BIAS = (long long)(n + 64) * (n + 64);  // keeps B >= 0
+    if (role == 0) {
+        // PL: wave = (a, i, h-chunk), lanes h; closing pair (i, j)
+        const int a = f1, i = f2;
+        const ILGroups lg = il_groups(imin(64, m - i - zc * 64 + 1), lane);
+        const int G = lg.G, gq = lg.gq;
+        const int h = zc * 64 + lg.rl;
+        const bool act = h <= m - i;
+        const unsigned lofs2 = 2u * (unsigned)(act ? h : m - i);  // idle lanes re-read a valid cell
+        const size_t pidx = (size_t)a * rs + i;
+        // PLx(t-dt, a-dt, h+dt-1-u1, i+1+u1) = lbx + (a-dt)M + x(m+dt) - x(x-1)/2 + dt-1-u1 + h, x = i+u1
+        //   = [lbx + (a-dt)M + i*m + i*dt + dt-1] + [u1*m - x(x-1)/2 - u1] + u1*dt
+        const int x = i + lane;
+        const int Btab = (int)(2 * ((long long)lane * m - ((long long)x * (x - 1) >> 1) - lane + BIAS));
+        unsigned long long Atab = 0;
+        if (lvl_ok && a >= lane)
+            Atab = (unsigned long long)T.d4x +
+                   2 * (T.ldx[tl].lbx + (long long)(a - lane) * T.ld[tl].M + (long long)i * m + (long long)i * lane + lane - 1 - BIAS);
+        const int B0 = __builtin_amdgcn_readlane(Btab, 0);
+        if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
+        const int e0 = (int)T.ilseg[pidx * IL_SEG + 3];
+        const uint2 *le = T.il + pidx * IL_CAP + e0;
+        const int lc = (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0;
+        const int b1 = G == 1 ? il_scan<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0)
+                              : il_scan_g<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl);
 #ifdef CCJ_DEBUG_BOUNDS
-        if (ca < 0 || ca > t || ch < 0 || ch >= m || ci < 1 || ci > m - ch) {
+        if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
             atomicOr(T.err, 128);
-            continue;
+            return;
         }
 #endif
-        dst[(long long)ca * Lt.M + ch * m - ((ch * (ch - 1)) >> 1) + ci - 1] = (int16_t)clamp_store(acc[p]);
+        if (act && gq == 0) T.d4[Lt.lb + (long long)PL * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
+    } else if (role == 1) {
+        // PR: wave = (a, q, i-chunk), lanes i; closing pair (k, l), q = i+h-1 = k-a-3
+        const int a = f1, q = f2;
+        const int b = t - a;
+        const int k = q + a + 3;
+        const ILGroups lg = il_groups(imin(64, q + 1 - zc * 64), lane);
+        const int G = lg.G, gq = lg.gq;
+        const int i = zc * 64 + lg.rl + 1;
+        const bool act = i <= q + 1;
+        const unsigned lofs2 = 2u * (unsigned)((act ? i : q + 1) - 1);
+        const int h = q + 1 - i;
+        const size_t pidx = (size_t)b * rs + k;
+        // PRx(t-dt, a, h+1+u1, i) = lbx + C + a*M + qq(qq+1)/2 + i-1, qq = q+1+u1
+        const int qq = q + 1 + lane;
+        const int Btab = qq * (qq + 1);  // bytes
+        unsigned long long Atab = 0;
+        if (lvl_ok) Atab = (unsigned long long)T.d4x + 2 * (T.ldx[tl].lbx + T.ld[tl].C + (long long)a * T.ld[tl].M);
+        const int B0 = __builtin_amdgcn_readlane(Btab, 0);
+        if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
+        const int e0 = (int)T.ilseg[pidx * IL_SEG + 3];
+        const uint2 *le = T.il + pidx * IL_CAP + e0;
+        const int lc = (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0;
+        const int b1 = G == 1 ? il_scan<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0)
+                              : il_scan_g<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl);
+#ifdef CCJ_DEBUG_BOUNDS
+        if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
+            atomicOr(T.err, 128);
+            return;
+        }
+#endif
+        if (act && gq == 0) T.d4[Lt.lb + (long long)PR * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
+    } else {
+        // PM: wave = (h, j, a-chunk), lanes a; pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
+        const int h = f1, j = f2;
+        const int g = h + 2, k = j + g;
+        // the rank's own a-blocks in the window (all of [alo, ahi] when unsharded): lanes = own index
+        int o0, o1;
+        pm_own_range(n, t, j, k, G_SH, rank, o0, o1);  // ccj_items.h
+        const ILGroups lg = il_groups(imin(64, o1 - o0 - zc * 64 + 1), lane);
+        const int G = lg.G, gq = lg.gq;
+        const int o = o0 + zc * 64 + lg.rl;
+        const bool act = o <= o1;
+        const int a = shard_a(imin(o, o1), G_SH, rank);
+        const int as = a;
+        const unsigned lofs2 = 2u * (unsigned)as;
+        const size_t pidx = (size_t)g * rs + j;
+        // PMx(t-dt, a-1-u1, h+dt, j-1-u1) = pmb + (h+dt)*n*(t+1-dt) + (j-2-u1)(t+1-dt) - 1-u1 + a
+        //   = [pmb + (h+dt)*n*(t+1-dt) + (j-2)(t+1-dt) - 1] + [-u1(t+2)] + u1*dt
+        // Lanes outside the get_PMiloop window read another cell of the same level (h+dt >= 4:
+        // in bounds) and are masked.
+        const int Btab = (int)(2 * (-(long long)lane * (t + 2) + BIAS));
+        unsigned long long Atab = 0;
+        if (lvl_ok)
+            Atab = (unsigned long long)T.pmx +
+                   2 * (T.ldx[tl].pmb + ((long long)(h + lane) * n + (j - 2)) * (tl + 1) - 1 - BIAS);
+        const int B0 = __builtin_amdgcn_readlane(Btab, 0);
+        if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
+        // entries with dt > t-2 fit no cell of this level
+        const int cnt = (int)T.ilmseg[pidx * IL_SEG + imin(t - 1, IL_SEG - 1)];
+        const int e0 = (int)T.ilmseg[pidx * IL_SEG + 3];
+        const uint2 *le = T.ilm + pidx * IL_CAP + e0;
+        const int b1 = G == 1 ? il_scan<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as)
+                              : il_scan_g<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl);
+#ifdef CCJ_DEBUG_BOUNDS
+        if (act && (a < 0 || a > t || h < 0 || h >= m || (j - a) < 1 || (j - a) > m - h)) {
+            atomicOr(T.err, 128);
+            return;
+        }
+#endif
+        if (act && gq == 0) T.d4[Lt.lb + (long long)PM * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + (j - a) - 1] = (int16_t)clamp_store(b1);
     }
 }
 
@@ -1706,8 +1845,8 @@ extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int n
     return 0;
 #endif
     if (nitems <= 0) return 0;
-    hipLaunchKernelGGL(k_iloop, dim3((unsigned)nitems), dim3(64 * IT_W), 0, (hipStream_t)stream, *T, t, first_item, nitems, G,
-                       rank);
+    hipLaunchKernelGGL(k_iloop, dim3((unsigned)((nitems + 3) / 4)), dim3(256), 0, (hipStream_t)stream, *T, t, first_item,
+                       nitems, G, rank);
     return (int)hipGetLastError();
 }
 

@@ -93,12 +93,12 @@ typedef struct ccj_options {
 int  ccj_create(const ccj_problem *prob, const ccj_options *opts, ccj_ctx **out);
 
 /* Rebind a context to another sequence of the same length n (same tables, dangles, noGU,
- * options): rebuilds only the sequence tables and reuses every
+ * options): rebuilds only the sequence tables and the interior-loop work lists and reuses every
  * allocation, so a batch of equal-length sequences pays ccj_create's multi-GB allocation once.
  * The reference has no equivalent (each fold constructs a new W_final, W_final.cc:20-56).
- * Non-blocking: the sequence tables go up asynchronously on the context's stream (the interior-
- * loop work items depend only on n and are built once by ccj_create); the call waits only for
- * the previous reset's uploads to have left the pinned staging buffer.
+ * Blocking: the interior-loop work-list count pass runs on the context's stream and the call
+ * waits for it (the host sizes the fill's launches from the counts), so it returns only after
+ * the work already queued on that stream; with CCJ_HOST_COUNT=1 the count runs on host threads.
  * CCJ_E_ARG if the length differs or the sequence has characters other than ACGUT; CCJ_E_STATE
  * while a fold is in flight. */
 int  ccj_reset(ccj_ctx *ctx, const char *seq);

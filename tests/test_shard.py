@@ -8,6 +8,10 @@
   (nmax = the largest rank's block count), the slices are all-gathered as ONE collective per level
   (the RCCL path does the same on the GPU), and unpacking the other ranks' slices must rebuild the
   level exactly as one process writes it.
+* P terms: each rank pushes only its share of the terms of P(i, i+sigma) (k_ppush outer index
+  jo / d-j-1 taken r, r+G, ...), as (value + 2^31) << 32 | first-split key words; the tail of the
+  exchange of level sigma-2 carries them and the minimum over the ranks must be the reference's P
+  (pseudo_loop.cc:166-179) with its first minimum.
 """
 import os
 import random
@@ -107,6 +111,34 @@ def _gloo_rank(rank, world, port, n, seq, q):
         q.put((rank, repr(e)))
 
 
+def p_term_rank(jo, do, ko, sigma, world):
+    """The rank that pushes term (j-i, d-i, k-i) of P(i, i+sigma) (k_ppush: part A, t1 = max level,
+    by outer index jo; part B, t2 = max level > t1, by outer index d-j-1)."""
+    t1 = jo + (ko - do - 1)
+    t2 = (do - jo - 1) + (sigma - ko - 1)
+    return (jo if t1 >= t2 else do - jo - 1) % world
+
+
+def _p_partials(fold, n, sigma, world, rank):
+    """This rank's (value + 2^31) << 32 | key word of P(i, i+sigma) for i = 0..n (~0: no term)."""
+    out = np.full(n + 1, np.iinfo(np.uint64).max, dtype=np.uint64)
+    for i in range(1, n - sigma + 1):
+        l = i + sigma
+        best = None
+        for j in range(i, l):
+            for d in range(j + 1, l):
+                for k in range(d + 1, l):
+                    jo, do, ko = j - i, d - i, k - i
+                    if p_term_rank(jo, do, ko, sigma, world) != rank:
+                        continue
+                    v = fold.get4(0, i, j, d + 1, k) + fold.get4(0, j + 1, d, k + 1, l)
+                    w = ((v + 2 ** 31) << 32) | ((jo * sigma + do) * sigma + ko)
+                    best = w if best is None or w < best else best
+        if best is not None:
+            out[i] = best
+    return out
+
+
 def _gloo_body(rank, world, n, seq, torch, dist):
     from ccj_amd import shard_blocks
     fold = OracleFold(seq, blob("Turner04"), 2, 0)
@@ -115,13 +147,24 @@ def _gloo_body(rank, world, n, seq, torch, dist):
         mine = shard_blocks(n, t, world, rank)
         nmax = max(len(shard_blocks(n, t, world, r)) for r in range(world))
         level, C, M = _level(n, t, fold, mine)
-        own = torch.from_numpy(_pack(level, C, M, mine, nmax)).view(torch.uint8)  # bytes, like ncclInt8
+        sig = t + 2  # the P span whose partials ride this exchange (pushed after level t-1)
+        tail = _p_partials(fold, n, sig, world, rank) if 1 <= t and sig <= n - 1 else np.zeros(n + 1, np.uint64)
+        body = _pack(level, C, M, mine, nmax).view(np.uint8)
+        own = torch.from_numpy(np.concatenate([body, np.zeros((-len(body)) % 8, np.uint8), tail.view(np.uint8)]))
         parts = [torch.empty_like(own) for _ in range(world)]
-        dist.all_gather(parts, own)  # ONE collective per level
-        slices = [p.view(torch.int16).numpy() for p in parts]
+        dist.all_gather(parts, own)  # ONE collective per level: cells + P tail
+        nb = len(body) + (-len(body)) % 8
+        slices = [p[:len(body)].numpy().view(np.int16) for p in parts]
         _unpack(level, C, M, slices, world, rank, t, nmax, shard_blocks, n)
         full, _, _ = _level(n, t, fold, range(t + 1))
         ok &= bool(np.array_equal(level, full))
+        if 1 <= t and sig <= n - 1:
+            comb = np.minimum.reduce([p[nb:].numpy().view(np.uint64) for p in parts])
+            for i in range(1, n - sig + 1):
+                ref = fold.get2(0, i, i + sig)  # reference P (INF+1 when no term)
+                got = int(comb[i])
+                val = None if got == (1 << 64) - 1 else (got >> 32) - 2 ** 31
+                ok &= (val is None and ref == 10000001) or (val == ref)
     fold.close()
     return ok
 
@@ -129,7 +172,7 @@ def _gloo_body(rank, world, n, seq, torch, dist):
 def test_level_allgather_rebuilds_levels_gloo():
     pytest.importorskip("torch")
     import torch.multiprocessing as mp
-    n, world = 18, 2
+    n, world = 16, 2
     seq = _rseq(11, n)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -141,3 +184,20 @@ def test_level_allgather_rebuilds_levels_gloo():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_p_term_partition_covers_every_term_once(world):
+    """k_ppush's per-rank outer indices r, r+G, ... <= lev partition [0, lev]; every term of P lands
+    on exactly one rank."""
+    for lev in range(0, 40):
+        seen = []
+        for r in range(world):
+            nout = (lev - r) // world + 1 if r <= lev else 0
+            seen += [r + world * x for x in range(nout)]
+        assert sorted(seen) == list(range(lev + 1))
+    sigma = 12
+    for jo in range(sigma):
+        for do in range(jo + 1, sigma):
+            for ko in range(do + 1, sigma):
+                assert 0 <= p_term_rank(jo, do, ko, sigma, world) < world
