@@ -165,6 +165,7 @@ struct ccj_ctx {
     hipStream_t st_pre = nullptr;        // prepass leader launches (level t beside level t-1)
     std::vector<hipEvent_t> pre_done;    // prepass launch of level t finished
     bool prepass = false;                // CCJ_PREPASS=1: leader launch of level t beside level t-1 (measured +0.5 ms at n=200)
+    bool join_diag = true;               // k_diag2d(t-1) after k_iloop(t) on st_il (one cross-stream wait per level)
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<hipEvent_t> pp_done; // band-sharded: this rank's P-term push of span sigma done (before the exchange)
     std::vector<double> lev_ms_v, diag_ms_v, il_ms_v;
@@ -1608,6 +1609,10 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         if (lt) c->level_timing = std::max(0, std::min(2, atoi(lt)));
         const char *pp = getenv("CCJ_PREPASS");
         c->prepass = pp && atoi(pp) != 0;
+        // k_diag2d(t-1) behind k_iloop(t) on one side stream, so each level waits on one event
+        // (fill -0.25 ms at n=200 in 3/3 alternating runs); not with the prepass scheme, which waits
+        // on dg_done[t-1] before it would be recorded
+        c->join_diag = !c->prepass;
         const char *g = getenv("CCJ_SHARE_SPLITS");
         c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
     }
@@ -1682,7 +1687,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipEventCreate(&c->ev_end));
     HIPCHK(cp, hipEventCreate(&c->ev_pre));
     c->lev_done.resize(n + 1);
-    // timed: the level durations (mode 1)
+    // timed: the level durations (mode 1; recording them untimed measured the same)
     for (auto &e : c->lev_done) HIPCHK(cp, hipEventCreateWithFlags(&e, fence_fl));
     c->p_done.resize(n + 1);
     for (auto &e : c->p_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
@@ -2023,11 +2028,24 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
         hipEvent_t *ev = &c->tev[7 * (size_t)s];
         // timing markers (ev[0..6]) only when per-kernel timing is on
         auto trec = [&](int x, hipStream_t q) { return c->level_timing == 2 ? hipEventRecord(ev[x], q) : hipSuccess; };
-        if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_d, c->p_done[s], 0));
-        HIPCHK(c, trec(0, c->st_d));
-        HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, s, c->st_d));
-        HIPCHK(c, trec(1, c->st_d));
-        HIPCHK(c, hipEventRecord(c->dg_done[s], c->st_d));
+        // k_diag2d(sigma) on st_d; or, joined (c->join_diag), on st_il right after k_iloop(sigma+1),
+        // so that level sigma+1 waits on one event that covers both
+        auto enqueue_diag = [&](int sg, hipStream_t q) -> int {
+            hipEvent_t *evd = &c->tev[7 * (size_t)sg];
+            if (sg >= 3) HIPCHK(c, hipStreamWaitEvent(q, c->p_done[sg], 0));
+            if (c->level_timing == 2) HIPCHK(c, hipEventRecord(evd[0], q));
+            HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, sg, q));
+            if (c->level_timing == 2) HIPCHK(c, hipEventRecord(evd[1], q));
+            HIPCHK(c, hipEventRecord(c->dg_done[sg], q));
+            return CCJ_OK;
+        };
+        const bool joined = c->join_diag && s >= 1 && s < c->nlev;  // diag(s-1) follows iloop(s)
+        if (!c->join_diag || s >= c->nlev) {
+            if (c->join_diag && s == c->nlev && s >= 1 && s - 1 < c->nlev) {
+                if (const int rc = enqueue_diag(s - 1, c->st_il)) return rc;  // last one behind iloop
+            }
+            if (const int rc = enqueue_diag(s, c->join_diag ? c->st_il : c->st_d)) return rc;
+        }
         if (const int rc = enqueue_pre(s + 1)) return rc;  // its inputs: lev_done[s-1], dg_done[s]
         if (s < c->nlev) {
             if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 3], 0));
@@ -2040,9 +2058,12 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                                                  c->st_il));
             }
             HIPCHK(c, trec(3, c->st_il));
+            if (joined) {
+                if (const int rc = enqueue_diag(s - 1, c->st_il)) return rc;
+            }
             HIPCHK(c, hipEventRecord(c->il_done[s], c->st_il));
             HIPCHK(c, hipStreamWaitEvent(st, c->il_done[s], 0));
-            if (s >= 1) HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s - 1], 0));
+            if (s >= 1 && !c->join_diag) HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s - 1], 0));
             if (c->T.prepass && s >= c->T.g_lo && s < c->T.g_hi) HIPCHK(c, hipStreamWaitEvent(st, c->pre_done[s], 0));
             HIPCHK(c, trec(4, st));
             // the level: its plain launch, then (sharing levels) the leaders on the same stream, no
