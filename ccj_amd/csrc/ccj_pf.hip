@@ -70,123 +70,177 @@ struct PfG {  // getters with the reference's semantics
 // the product in int.  Lanes take 64 consecutive i; a workgroup takes one (j-i, d-i) and loops k.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_pf_pterm(PfDev D, int s) {
-    const PfG G{D};
     const int jo = blockIdx.y, dd = blockIdx.z;  // j = i+jo, d = i+dd
     if (dd <= jo || dd > s - 2) return;
     const int i = blockIdx.x * 64 + threadIdx.x + 1;
     if (i + s > D.n) return;
-    const int l = i + s, j = i + jo, d = i + dd;
+    // PK(i, j, d+1, k): level jo + (ko-dd-1), block jo, row dd-jo-1, position i;
+    // PK(j+1, d, k+1, l): level (dd-jo-1) + (s-ko-1), block dd-jo-1, row ko-dd-1, position i+jo+1
+    // (ko = k-i): wave-uniform level descriptors, lanes at consecutive positions
+    const int n = D.n, a1 = jo, h1 = dd - jo - 1, a2 = dd - jo - 1;
+    typedef const __attribute__((address_space(1))) int gint;
     long long acc = 0;
-    for (int k = d + 1; k < l; ++k) acc += imul_wrap(G.g4(PF_PK, i, j, d + 1, k), G.g4(PF_PK, j + 1, d, k + 1, l));
+    for (int ko = dd + 1; ko < s; ++ko) {
+        const int h2 = ko - dd - 1, t1 = a1 + h2, t2 = a2 + (s - ko - 1);
+        const int m1 = n - t1 - 2, m2 = n - t2 - 2;
+        const PfLvl L1 = D.ld[t1], L2 = D.ld[t2];
+        const long long U1 = L1.lb + PF_PK * L1.C + (long long)a1 * L1.M + (long long)h1 * m1 - (((long long)h1 * (h1 - 1)) >> 1) - 1;
+        const long long U2 = L2.lb + PF_PK * L2.C + (long long)a2 * L2.M + (long long)h2 * m2 - (((long long)h2 * (h2 - 1)) >> 1) + jo;
+        acc += imul_wrap(*(gint *)(D.d4 + U1 + i), *(gint *)(D.d4 + U2 + i));
+    }
     if (acc) atomicAdd((unsigned long long *)&D.Pacc[s * D.rs + i], (unsigned long long)acc);
 }
 
 // ---------------------------------------------------------------------------------------------
-// The 2-D values of span s, one thread per interval (i, j = i+s), in the reference's order.
+// The 2-D values of span s, one wave per interval (i, j = i+s).  Every sum keeps the reference's
+// term order and association: the lanes evaluate up to 64 terms at once (the products, each as
+// written), then the sum adds them one after another in the reference's order (lane u's term
+// read back with readlane), so the bits equal the reference's serial loop.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double rdlane(double x, int u) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, u);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), u);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// acc += term(0) + term(1) + ... + term(N-1), added in that order; term(q) evaluated by lane q % 64
+template <class F>
+__device__ __forceinline__ double ordered_sum(double acc, int N, int lane, F term) {
+    for (int q0 = 0; q0 < N; q0 += 64) {
+        const int q = q0 + lane;
+        const double x = q < N ? term(q) : 0.0;
+        const int cnt = imin(64, N - q0);
+        for (int u = 0; u < cnt; ++u) acc += rdlane(x, u);
+    }
+    return acc;
+}
+
 __global__ __launch_bounds__(64) void k_pf_diag(PfDev D, int s) {
     const PfG G{D};
     const PfExp &E = *D.E;
-    const int i = blockIdx.x * 64 + threadIdx.x + 1, j = i + s, n = D.n;
-    if (j > n) return;
+    const int i = blockIdx.x + 1, j = i + s, n = D.n;
+    if (j > n) return;  // whole wave
+    const int lane = threadIdx.x;
     const int rs = D.rs;
     const int ij = s * rs + i;
     const int dang = D.dangles == 1 || D.dangles == 2;
     const short *S = D.S, *S1 = D.S1;
 
     // compute_energy (part_func.cc:290-300): V = hairpin + interior loops + VM
+    double v_ij;
     {
-        double vi = 0;  // compute_internal :222-240
+        double vi = 0;  // compute_internal :222-240: k = i+1..max_k, l = j-1 down to min_l
         const int max_k = imin(j - TURN - 2, i + MAXLOOP + 1);
         const int tc = G.pt(i, j);
         for (int k = i + 1; k <= max_k; ++k) {
             const int min_l = imax(k + TURN + 1 + MAXLOOP + 2, k + j - i) - MAXLOOP - 2;
-            for (int l = j - 1; l >= min_l; --l) {
+            vi = ordered_sum(vi, j - min_l, lane, [&](int u) {
+                const int l = j - 1 - u;
                 double x = G.d2(D.V, k, l) *
                            exp_E_IntLoop_pf(E, k - i - 1, j - l - 1, tc, D.rtype[G.pt(k, l)], S1[i + 1], S1[j - 1], S1[k - 1], S1[l + 1]);
                 x *= 1.0;  // scale[u1+u2+2]
-                vi += x;
-            }
+                return x;
+            });
         }
-        // compute_energy_VM :276-288, exp_Mbloop :203-212
+        // compute_energy_VM :276-288, exp_Mbloop :203-212; three terms per k, in order
         const int tt = D.pair[S[j] * 8 + S[i]];
         const double mb = dang ? exp_E_MLstem_pf(E, tt, j < n ? S[j - 1] : -1, i > 1 ? S[i + 1] : -1) : exp_E_MLstem_pf(E, tt, -1, -1);
-        double vm = 0;
-        for (int k = i + 1; k <= j - TURN - 1; ++k) {
-            const double wm = G.g2(D.WM, i + 1, k - 1), wmv = G.g2(D.WMv, k, j - 1), wmp = G.g2(D.WMp, k, j - 1);
-            vm += wm * wmv * mb * E.MLclosing;
-            vm += wm * wmp * mb * E.MLclosing;
-            vm += D.mlb[k - i - 1] * wmp * mb * E.MLclosing;
-        }
+        const int nk = imax(0, j - TURN - 1 - i);  // k = i+1 .. j-TURN-1
+        double vm = ordered_sum(0.0, 3 * nk, lane, [&](int q) {
+            const int k = i + 1 + q / 3, w = q % 3;
+            const double wmp = G.g2(D.WMp, k, j - 1);
+            if (w == 0) return G.g2(D.WM, i + 1, k - 1) * G.g2(D.WMv, k, j - 1) * mb * E.MLclosing;
+            if (w == 1) return G.g2(D.WM, i + 1, k - 1) * wmp * mb * E.MLclosing;
+            return D.mlb[k - i - 1] * wmp * mb * E.MLclosing;
+        });
         vm *= 1.0;  // scale[2]
-        D.VM[ij] = vm;
         double v = 0;
         v += D.hp[ij];
         v += vi;
         v += vm;
-        D.V[ij] = v;
+        if (lane == 0) {
+            D.VM[ij] = vm;
+            D.V[ij] = v;
+        }
+        v_ij = v;
     }
     // compute_pk_energies (:302-309): P (summed by k_pf_pterm), WBP, WPP
     const double p = (double)D.Pacc[ij];
-    D.P[ij] = p;
-    {
-        double c = 0;  // compute_WBP :361-370
-        for (int d = i; d < j; ++d) {
-            c += G.d2(D.V, d, j) * E.bp * E.PPS;
-            c += (d == i ? p : G.d2(D.P, d, j)) * E.PSM * E.PPS;
-        }
+    if (lane == 0) D.P[ij] = p;
+    const int nd = j - i;  // d = i .. j-1, two terms each
+    double wbp;
+    {   // compute_WBP :361-370
+        double c = ordered_sum(0.0, 2 * nd, lane, [&](int q) {
+            const int d = i + q / 2;
+            if ((q & 1) == 0) return (d == i ? v_ij : G.d2(D.V, d, j)) * E.bp * E.PPS;
+            return (d == i ? p : G.d2(D.P, d, j)) * E.PSM * E.PPS;
+        });
         c += G.g2(D.WBP, i, j - 1) * D.cpp[1];
-        D.WBP[ij] = c;
-        double w = 0;  // compute_WPP :372-381 (its last term reads WBP)
-        for (int d = i; d < j; ++d) {
-            const double wp = G.WP(i, d - 1);
-            w += wp * G.d2(D.V, d, j) * 1.0 * E.PPS;
-            w += wp * (d == i ? p : G.d2(D.P, d, j)) * E.PSP * E.PPS;
-        }
-        w += G.g2(D.WBP, i, j - 1) * D.pup[1];
-        D.WPP[ij] = w;
+        wbp = c;
+        if (lane == 0) D.WBP[ij] = c;
     }
+    {   // compute_WPP :372-381 (its last term reads WBP)
+        double w = ordered_sum(0.0, 2 * nd, lane, [&](int q) {
+            const int d = i + q / 2;
+            const double wp = G.WP(i, d - 1);
+            if ((q & 1) == 0) return wp * (d == i ? v_ij : G.d2(D.V, d, j)) * 1.0 * E.PPS;
+            return wp * (d == i ? p : G.d2(D.P, d, j)) * E.PSP * E.PPS;
+        });
+        w += G.g2(D.WBP, i, j - 1) * D.pup[1];
+        if (lane == 0) D.WPP[ij] = w;
+    }
+    (void)wbp;
     // compute_WMv_WMp (:242-256), exp_MLstem :192-201
     const int tij = G.pt(i, j);
     const double mls_ij = dang ? exp_E_MLstem_pf(E, tij, i > 1 ? S[i - 1] : -1, j < n ? S[j + 1] : -1) : exp_E_MLstem_pf(E, tij, -1, -1);
-    if (!(j - i - 1 < TURN)) {
+    if (!(j - i - 1 < TURN) && lane == 0) {
         double wv = 0, wp = 0;
-        wv += D.V[ij] * mls_ij;
+        wv += v_ij * mls_ij;
         wp += p * E.PSM * E.b;
         wv += G.d2(D.WMv, i, j - 1) * D.mlb[1];
         wp += G.d2(D.WMp, i, j - 1) * D.mlb[1];
         D.WMv[ij] = wv;
         D.WMp[ij] = wp;
     }
-    // compute_energy_WM (:258-274)
+    // compute_energy_WM (:258-274): k = i .. j-TURN-1, four terms each
     if (!(j - i + 1 < 4)) {
-        double c = 0;
-        for (int k = i; k < j - TURN; ++k) {
+        const int nk = j - TURN - i;
+        double c = ordered_sum(0.0, 4 * nk, lane, [&](int q) {
+            const int k = i + q / 4, w = q % 4;
             const int tk = G.pt(k, j);
             const double mls = k == i ? mls_ij
                                       : (dang ? exp_E_MLstem_pf(E, tk, k > 1 ? S[k - 1] : -1, j < n ? S[j + 1] : -1)
                                               : exp_E_MLstem_pf(E, tk, -1, -1));
-            const double q1 = (k == i ? D.V[ij] : G.d2(D.V, k, j)) * mls;
+            const double q1 = (k == i ? v_ij : G.d2(D.V, k, j)) * mls;
             const double q2 = (k == i ? p : G.d2(D.P, k, j)) * E.PSM * E.b;
-            c += D.mlb[k - i] * q1;
-            c += D.mlb[k - i] * q2;
             const double wm = G.g2(D.WM, i, k - 1);
-            c += wm * q1;
-            c += wm * q2;
-        }
+            if (w == 0) return D.mlb[k - i] * q1;
+            if (w == 1) return D.mlb[k - i] * q2;
+            if (w == 2) return wm * q1;
+            return wm * q2;
+        });
         c += G.d2(D.WM, i, j - 1) * D.mlb[1];
-        D.WM[ij] = c;
+        if (lane == 0) D.WM[ij] = c;
     }
 }
 
 // ---------------------------------------------------------------------------------------------
 // The 21 recurrences of one 4-D cell, in the reference's order (compute_pk_energies :315-355).
-// One thread per cell of level t; blockIdx.y = a = j-i (every loop bound is block-uniform).
+// One lane per cell of level t; blockIdx.y = a = j-i, so every loop bound and every neighbour's
+// level / block is wave-uniform.  A neighbour X at (level t-dt, block a-da, row h+dh, position
+// i+di) is, as in the MFE level kernel,
+//     d4[ lb' + x C' + (a-da) M' + dh m' - dh(dh-1)/2 + di ]      (uniform: one scalar descriptor)
+//        [ off + h (dt-dh) ]                                      (per lane; off = the cell's own offset)
+// so each term costs one coalesced load on a scalar base instead of a per-lane descriptor gather.
+// Each sum is still one lane's serial sum in the reference's term order and association (bits).
+// The split loops run over s = d - i (or d - k):
+//   X1(s) = X(i+s, j, k, l)   X2(s) = X(i, i+s, k, l)   X3(s) = X(i, j, k+s, l)   X4(s) = X(i, j, k, k+s)
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     const PfG G{D};
     const PfExp &E = *D.E;
-    const int n = D.n, a = blockIdx.y, b = t - a, m = n - t - 2;
+    const int n = D.n, a = blockIdx.y, b = t - a, m = n - t - 2, rs = D.rs;
     const PfLvl L = D.ld[t];
     const int off = blockIdx.x * 256 + threadIdx.x;
     if (off >= L.M) return;
@@ -204,195 +258,228 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         cell[x * C] = r;
         return r;
     };
+    // matrix x at (t-dt, a-da, h+dh, i+di); the caller checks that the cell exists (a-da, b-db >= 0)
+    typedef const __attribute__((address_space(1))) int gint;
+    auto X = [&](int x, int dt, int da, int dh, int di) -> int {
+        const int tp = t - dt, mp = m + dt;
+        const PfLvl Lp = D.ld[tp];
+        const long long U = Lp.lb + (long long)x * Lp.C + (long long)(a - da) * Lp.M + (long long)dh * mp -
+                            (((long long)dh * (dh - 1)) >> 1) + di;
+        return *(gint *)(D.d4 + U + (off + h * (dt - dh)));
+    };
+    auto X1 = [&](int x, int s) { return X(x, s, s, 0, s); };              // X(i+s, j, k, l)
+    auto X2 = [&](int x, int s) { return X(x, a - s, a - s, a - s, 0); };  // X(i, i+s, k, l)
+    auto X3 = [&](int x, int s) { return X(x, s, 0, s, 0); };              // X(i, j, k+s, l)
+    auto X4 = [&](int x, int s) { return X(x, b - s, 0, 0, 0); };          // X(i, j, k, k+s)
+    // get_WB / get_WP (part_func.cc:701-715) of in-range intervals: expcp_pen[len] + WBP
+    const double *cpp = D.cpp, *pup = D.pup, *WBP = D.WBP, *WPP = D.WPP;
+    auto WBi = [&](int s) { return cpp[s] + WBP[(s - 1) * rs + i]; };                   // WB(i, i+s-1)
+    auto WBj = [&](int s) { return cpp[a - s] + WBP[(a - s - 1) * rs + i + s + 1]; };   // WB(i+s+1, j)
+    auto WBk = [&](int s) { return cpp[s] + WBP[(s - 1) * rs + k]; };                   // WB(k, k+s-1)
+    auto WBl = [&](int s) { return cpp[b - s] + WBP[(b - s - 1) * rs + k + s + 1]; };   // WB(k+s+1, l)
+    auto WPi = [&](int s) { return pup[s] + WPP[(s - 1) * rs + i]; };
+    auto WPj = [&](int s) { return pup[a - s] + WPP[(a - s - 1) * rs + i + s + 1]; };
+    auto WPk = [&](int s) { return pup[s] + WPP[(s - 1) * rs + k]; };
+    auto WPl = [&](int s) { return pup[b - s] + WPP[(b - s - 1) * rs + k + s + 1]; };
+    auto BPi = [&](int s) { return WBP[(s - 1) * rs + i]; };                            // WBP(i, i+s-1)
+    auto BPj = [&](int s) { return WBP[(a - s - 1) * rs + i + s + 1]; };                // WBP(i+s+1, j)
+    auto BPk = [&](int s) { return WBP[(s - 1) * rs + k]; };
+    auto BPl = [&](int s) { return WBP[(b - s - 1) * rs + k + s + 1]; };
     const double bp = E.bp, ap = E.ap, cp1 = D.cpp[1], PB = E.PB;
 
-    // PLmloop00 (:554-568); the seed PL(i,j,k,l) is not computed yet: 0 * beta2P
-    {
+    {  // PLmloop00 (:554-568); the seed PL(i,j,k,l) is not computed yet: 0 * beta2P
         double c = 0;
         c += 0.0 * bp;
-        for (int d = i; d <= j; ++d) {
-            if (d > i) c += G.WB(i, d - 1) * G.g4(PF_PLmloop00, d, j, k, l);
-            if (d < j) c += G.g4(PF_PLmloop00, i, d, k, l) * G.WB(d + 1, j);
+        for (int s = 0; s <= a; ++s) {
+            if (s > 0) c += WBi(s) * X1(PF_PLmloop00, s);
+            if (s < a) c += X2(PF_PLmloop00, s) * WBj(s);
         }
         put(PF_PLmloop00, c);
     }
     {  // PLmloop01 (:570-578)
         double c = 0;
-        for (int d = i; d < j; ++d) c += G.g4(PF_PLmloop00, i, d, k, l) * G.g2(D.WBP, d + 1, j);
+        for (int s = 0; s < a; ++s) c += X2(PF_PLmloop00, s) * BPj(s);
         put(PF_PLmloop01, c);
     }
     {  // PLmloop10 (:580-590)
         double c = 0;
-        for (int d = i + 1; d <= j; ++d) {
-            c += G.g2(D.WBP, i, d - 1) * G.g4(PF_PLmloop00, d, j, k, l);
-            if (d < j) c += G.g4(PF_PLmloop10, i, d, k, l) * G.WB(d + 1, j);
+        for (int s = 1; s <= a; ++s) {
+            c += BPi(s) * X1(PF_PLmloop00, s);
+            if (s < a) c += X2(PF_PLmloop10, s) * WBj(s);
         }
         put(PF_PLmloop10, c);
     }
     {  // PRmloop00 (:592-605)
         double c = 0;
         c += 0.0 * bp;
-        for (int d = k; d <= l; ++d) {
-            if (d > k) c += G.WB(k, d - 1) * G.g4(PF_PRmloop00, i, j, d, l);
-            if (d < l) c += G.g4(PF_PRmloop00, i, j, k, d) * G.WB(d + 1, l);
+        for (int s = 0; s <= b; ++s) {
+            if (s > 0) c += WBk(s) * X3(PF_PRmloop00, s);
+            if (s < b) c += X4(PF_PRmloop00, s) * WBl(s);
         }
         put(PF_PRmloop00, c);
     }
-    {  // PRmloop01 (:608-616)
+    {  // PRmloop01 (:608-616): PRmloop01(i,j,k,l-1) * expcp_pen[1] (0 when k = l: outside the matrix)
         double c = 0;
-        c += G.g4(PF_PRmloop01, i, j, k, l - 1) * cp1;
-        for (int d = k; d < l; ++d) c += G.g4(PF_PRmloop00, i, j, k, d) * G.g2(D.WBP, d + 1, l);
+        c += (b >= 1 ? X(PF_PRmloop01, 1, 0, 0, 0) : 0) * cp1;
+        for (int s = 0; s < b; ++s) c += X4(PF_PRmloop00, s) * BPl(s);
         put(PF_PRmloop01, c);
     }
-    {  // PRmloop10 (:618-626)
+    {  // PRmloop10 (:618-626): PRmloop10(i,j,k+1,l) * expcp_pen[1]
         double c = 0;
-        c += G.g4(PF_PRmloop10, i, j, k + 1, l) * cp1;
-        for (int d = k + 1; d <= l; ++d) c += G.g2(D.WBP, k, d - 1) * G.g4(PF_PRmloop00, i, j, d, l);
+        c += (b >= 1 ? X(PF_PRmloop10, 1, 0, 1, 0) : 0) * cp1;
+        for (int s = 1; s <= b; ++s) c += BPk(s) * X3(PF_PRmloop00, s);
         put(PF_PRmloop10, c);
     }
     {  // PMmloop00 (:628-639)
         double c = 0;
         c += 0.0 * bp;
-        for (int d = i; d < j; ++d) c += G.g4(PF_PMmloop00, i, d, k, l) * G.WB(d + 1, j);
-        for (int d = k + 1; d <= l; ++d) c += G.g4(PF_PMmloop00, i, j, d, l) * G.WB(k, d - 1);
+        for (int s = 0; s < a; ++s) c += X2(PF_PMmloop00, s) * WBj(s);
+        for (int s = 1; s <= b; ++s) c += X3(PF_PMmloop00, s) * WBk(s);
         put(PF_PMmloop00, c);
     }
     {  // PMmloop01 (:642-650): "+ expcp_pen[1]"
         double c = 0;
-        c += G.g4(PF_PMmloop01, i, j, k + 1, l) + cp1;
-        for (int d = k; d < l; ++d) c += G.g4(PF_PMmloop00, i, j, k, d) * G.g2(D.WBP, d + 1, l);
+        c += (b >= 1 ? X(PF_PMmloop01, 1, 0, 1, 0) : 0) + cp1;
+        for (int s = 0; s < b; ++s) c += X4(PF_PMmloop00, s) * BPl(s);
         put(PF_PMmloop01, c);
     }
-    {  // PMmloop10 (:652-663)
+    {  // PMmloop10 (:652-663): PMmloop10(i,j-1,k,l) * expcp_pen[1]
         double c = 0;
-        c += G.g4(PF_PMmloop10, i, j - 1, k, l) * cp1;
-        for (int d = i + 1; d <= j; ++d) c += G.g2(D.WBP, i, d - 1) * G.g4(PF_PMmloop00, d, j, k, l);
-        for (int d = k + 1; d < l; ++d) c += G.g4(PF_POmloop10, i, j, k, d) * G.WB(d + 1, l);
+        c += (a >= 1 ? X(PF_PMmloop10, 1, 1, 1, 0) : 0) * cp1;
+        for (int s = 1; s <= a; ++s) c += BPi(s) * X1(PF_PMmloop00, s);
+        for (int s = 1; s < b; ++s) c += X4(PF_POmloop10, s) * WBl(s);
         put(PF_PMmloop10, c);
     }
     {  // POmloop00 (:665-676): the second loop assigns, so only its last term survives
         double c = 0;
         c += 0.0 * bp;
-        for (int d = i + 1; d <= j; ++d) c += G.WB(i, d - 1) * G.g4(PF_POmloop00, d, j, k, l);
-        if (k < l) c = G.g4(PF_POmloop00, i, j, k, l - 1) * G.WB(l, l);
+        for (int s = 1; s <= a; ++s) c += WBi(s) * X1(PF_POmloop00, s);
+        if (b >= 1) c = X(PF_POmloop00, 1, 0, 0, 0) * (cpp[1] + WBP[l]);  // POmloop00(i,j,k,l-1) * WB(l,l)
         put(PF_POmloop00, c);
     }
     {  // POmloop01 (:679-686)
         double c = 0;
-        for (int d = k; d < l; ++d) c += G.g4(PF_POmloop00, i, j, k, d) * G.g2(D.WBP, d + 1, l);
+        for (int s = 0; s < b; ++s) c += X4(PF_POmloop00, s) * BPl(s);
         put(PF_POmloop01, c);
     }
     {  // POmloop10 (:688-699): "+ get_WB"
         double c = 0;
-        for (int d = i + 1; d <= j; ++d) c += G.g2(D.WBP, i, d - 1) * G.g4(PF_POmloop00, d, j, k, l);
-        for (int d = k + 1; d < l; ++d) c += G.g4(PF_POmloop10, i, j, k, d) + G.WB(d + 1, l);
+        for (int s = 1; s <= a; ++s) c += BPi(s) * X1(PF_POmloop00, s);
+        for (int s = 1; s < b; ++s) c += X4(PF_POmloop10, s) + WBl(s);
         put(PF_POmloop10, c);
     }
 
-    const int rs = D.rs;
-    // PL (:414-430) with get_PLiloop (:736-756) and get_PLmloop (:758-768)
+    // PL (:414-430) with get_PLiloop (:736-756) and get_PLmloop (:758-768); the inner cell
+    // (i+1, j-1, k, l) is (t-2, a-2, h+1, i+1), outside the matrix (0) when a < 2
     int PL = 0;
     {
         double c = 0;
         if (G.pt(i, j) > 0) {
+            const bool in = a >= 2;
             double r = 0;
-            r += G.g4(PF_PL, i + 1, j - 1, k, l) * D.est[a * rs + i];
-            const int dmax = PF_ILOOP_ON ? imin(j, i + MAXLOOP) : 0;
-            for (int d = i + 1; d < dmax; ++d) {
-                const int u1 = d - i - 1;
-                const int dpmin = imax(d + TURN, j - MAXLOOP);
-                for (int dp = j - 1; dp > dpmin; --dp) {
-                    const int u2 = j - dp - 1;
+            r += (in ? X(PF_PL, 2, 2, 1, 1) : 0) * D.est[a * rs + i];
+            // d = i+1+u1 < min(j, i+30); dp = j-1-u2 > max(d+3, j-30): u1 <= min(a,30)-2, u2 <= min(a-u1-6, 28)
+            const int u1m = PF_ILOOP_ON ? imin(a, MAXLOOP) - 2 : -1;
+            for (int u1 = 0; u1 <= u1m; ++u1) {
+                const int u2m = imin(a - u1 - 6, PF_IEW - 1);
+                for (int u2 = 0; u2 <= u2m; ++u2) {
                     const double e = D.ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + a) * rs + i];
-                    if (e != 0.0) r += e * G.g4(PF_PL, d, dp, k, l) * 1.0;
+                    const int dt = 2 + u1 + u2;
+                    if (e != 0.0) r += e * X(PF_PL, dt, dt, 1 + u2, 1 + u1) * 1.0;
                 }
             }
             c += r;
             double q = 0;
-            q += G.g4(PF_PLmloop10, i + 1, j - 1, k, l) * ap * bp;
-            q += (double)imul_wrap(G.g4(PF_PLmloop01, i + 1, j - 1, k, l), D.ap_int) * bp;
+            q += (in ? X(PF_PLmloop10, 2, 2, 1, 1) : 0) * ap * bp;
+            q += (double)imul_wrap(in ? X(PF_PLmloop01, 2, 2, 1, 1) : 0, D.ap_int) * bp;
             c += q * bp;
-            if (j >= i + TURN + 1) c += G.g4(PF_PfromL, i + 1, j - 1, k, l) * 1.0;
+            if (j >= i + TURN + 1) c += (in ? X(PF_PfromL, 2, 2, 1, 1) : 0) * 1.0;
         }
         PL = put(PF_PL, c);
     }
-    // PR (:432-447), get_PRiloop (:770-790), get_PRmloop (:792-802)
+    // PR (:432-447), get_PRiloop (:770-790), get_PRmloop (:792-802); (i, j, k+1, l-1) is
+    // (t-2, a, h+1, i), outside when b < 2
     int PR = 0;
     {
         double c = 0;
         if (G.pt(k, l) > 0) {
+            const bool in = b >= 2;
             double r = 0;
-            r += G.g4(PF_PR, i, j, k + 1, l - 1) * D.est[b * rs + k];
-            const int dmax = PF_ILOOP_ON ? imin(l, k + MAXLOOP) : 0;
-            for (int d = k + 1; d < dmax; ++d) {
-                const int u1 = d - k - 1;
-                const int dpmin = imax(d + TURN, l - MAXLOOP);
-                for (int dp = l - 1; dp > dpmin; --dp) {
-                    const int u2 = l - dp - 1;
+            r += (in ? X(PF_PR, 2, 0, 1, 0) : 0) * D.est[b * rs + k];
+            const int u1m = PF_ILOOP_ON ? imin(b, MAXLOOP) - 2 : -1;
+            for (int u1 = 0; u1 <= u1m; ++u1) {
+                const int u2m = imin(b - u1 - 6, PF_IEW - 1);
+                for (int u2 = 0; u2 <= u2m; ++u2) {
                     const double e = D.ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + b) * rs + k];
-                    if (e != 0.0) r += e * G.g4(PF_PR, i, j, d, dp) * 1.0;
+                    const int dt = 2 + u1 + u2;
+                    if (e != 0.0) r += e * X(PF_PR, dt, 0, 1 + u1, 0) * 1.0;
                 }
             }
             c += r;
             double q = 0;
-            q += G.g4(PF_PRmloop10, i, j, k + 1, l - 1) * ap * bp;
-            q += G.g4(PF_PRmloop01, i, j, k + 1, l - 1) * ap * bp;
+            q += (in ? X(PF_PRmloop10, 2, 0, 1, 0) : 0) * ap * bp;
+            q += (in ? X(PF_PRmloop01, 2, 0, 1, 0) : 0) * ap * bp;
             c += q * bp;
-            if (l >= k + TURN + 1) c += G.g4(PF_PfromR, i, j, k + 1, l - 1) * 1.0;
+            if (l >= k + TURN + 1) c += (in ? X(PF_PfromR, 2, 0, 1, 0) : 0) * 1.0;
         }
         PR = put(PF_PR, c);
     }
-    // PM (:449-467), get_PMiloop (:804-824), get_PMmloop (:826-836)
+    // PM (:449-467), get_PMiloop (:804-824), get_PMmloop (:826-836); (i, j-1, k+1, l) is
+    // (t-2, a-1, h+2, i), outside when a < 1 or b < 1
     int PM = 0;
     {
         double c = 0;
         if (G.pt(j, k) > 0) {
+            const bool in = a >= 1 && b >= 1;
             double r = 0;
             // get_e_stP(j-1, k+1): for j == 1 or k == n the reference indexes pair[][] with S[0] (= n)
             // or S[n+1]; the factor multiplies PM(i, j-1, k+1, l), which is then outside the matrix
             // (0), so any finite value gives 0 — use 0 instead of reading past the table
             const double est_m = (j > 1 && k < n) ? D.est[(h + 4) * rs + (j - 1)] : 0.0;
-            r += G.g4(PF_PM, i, j - 1, k + 1, l) * est_m;
-            const int dmin = PF_ILOOP_ON ? imax(i, j - MAXLOOP) : j, dpmax = imin(l, k + MAXLOOP);
-            for (int d = j - 1; d > dmin; --d) {
-                const int u1 = j - d - 1;
-                for (int dp = k + 1; dp < dpmax; ++dp) {
-                    const int u2 = dp - k - 1;
-                    const double e = D.ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + (dp - d)) * rs + d];
-                    if (e != 0.0) r += e * G.g4(PF_PM, i, d, dp, l) * 1.0;
+            r += (in ? X(PF_PM, 2, 1, 2, 0) : 0) * est_m;
+            // d = j-1-u1 > max(i, j-30), dp = k+1+u2 < min(l, k+30): u1 <= min(a-2, 28), u2 <= min(b-2, 28)
+            const int u1m = PF_ILOOP_ON ? imin(a - 2, PF_IEW - 1) : -1, u2m = imin(b - 2, PF_IEW - 1);
+            for (int u1 = 0; u1 <= u1m; ++u1) {
+                const int d = j - 1 - u1;
+                for (int u2 = 0; u2 <= u2m; ++u2) {
+                    const double e = D.ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + (h + 4 + u1 + u2)) * rs + d];
+                    const int dt = 2 + u1 + u2;
+                    if (e != 0.0) r += e * X(PF_PM, dt, 1 + u1, dt, 0) * 1.0;
                 }
             }
             c += r;
             double q = 0;
-            q += G.g4(PF_PMmloop10, i, j - 1, k + 1, l) * ap * bp;
-            q += G.g4(PF_PMmloop01, i, j - 1, k + 1, l) * ap * bp;
+            q += (in ? X(PF_PMmloop10, 2, 1, 2, 0) : 0) * ap * bp;
+            q += (in ? X(PF_PMmloop01, 2, 1, 2, 0) : 0) * ap * bp;
             c += q * bp;
-            if (k >= j + TURN - 1) c += G.g4(PF_PfromM, i, j - 1, k + 1, l) * 1.0;
+            if (k >= j + TURN - 1) c += (in ? X(PF_PfromM, 2, 1, 2, 0) : 0) * 1.0;
             if (i == j && k == l) c += 1.0;
         }
         PM = put(PF_PM, c);
     }
-    // PO (:469-486), get_POiloop (:838-858: reads PO(d,j,dp,k) with dp > k, always 0), get_POmloop
+    // PO (:469-486), get_POiloop (:838-858: reads PO(d,j,dp,k) with dp > k, always 0), get_POmloop;
+    // (i+1, j, k, l-1) is (t-2, a-1, h, i+1), outside when a < 1 or b < 1
     int PO = 0;
     {
         double c = 0;
         if (G.pt(i, l) > 0) {
+            const bool in = a >= 1 && b >= 1;
             double r = 0;
-            r += G.g4(PF_PO, i + 1, j, k, l - 1) * D.est[(t + h + 2) * rs + i];
+            r += (in ? X(PF_PO, 2, 1, 0, 1) : 0) * D.est[(t + h + 2) * rs + i];
             c += r;
             double q = 0;
-            q += G.g4(PF_POmloop10, i + 1, j, k, l - 1) * ap * bp;
-            q += G.g4(PF_POmloop01, i + 1, j, k, l - 1) * ap * bp;
+            q += (in ? X(PF_POmloop10, 2, 1, 0, 1) : 0) * ap * bp;
+            q += (in ? X(PF_POmloop01, 2, 1, 0, 1) : 0) * ap * bp;
             c += q * bp;
-            if (l >= i + TURN + 1) c += G.g4(PF_PfromO, i + 1, j, k, l - 1) * 1.0;
+            if (l >= i + TURN + 1) c += (in ? X(PF_PfromO, 2, 1, 0, 1) : 0) * 1.0;
         }
         PO = put(PF_PO, c);
     }
     {  // PfromL (:488-503)
         double c = 0;
-        for (int d = i + 1; d < j; ++d) {
-            c += G.g4(PF_PfromL, d, j, k, l) * G.WP(i, d - 1);
-            c += G.g4(PF_PfromL, i, d, k, l) * G.WP(d + 1, j);
+        for (int s = 1; s < a; ++s) {
+            c += X1(PF_PfromL, s) * WPi(s);
+            c += X2(PF_PfromL, s) * WPj(s);
         }
         c += PR * 1.0 * PB;
         c += PM * 1.0 * PB;
@@ -401,9 +488,9 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     }
     {  // PfromR (:505-518)
         double c = 0;
-        for (int d = k + 1; d < l; ++d) {
-            c += G.g4(PF_PfromR, i, j, d, l) * G.WP(k, d - 1);
-            c += G.g4(PF_PfromR, i, j, k, d) * G.WP(d + 1, l);
+        for (int s = 1; s < b; ++s) {
+            c += X3(PF_PfromR, s) * WPk(s);
+            c += X4(PF_PfromR, s) * WPl(s);
         }
         c += PM * 1.0 * PB;
         c += PO * 1.0 * PB;
@@ -411,24 +498,24 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     }
     {  // PfromM (:520-535)
         double c = 0;
-        for (int d = i + 1; d < j; ++d) c += G.g4(PF_PfromM, i, d, k, l) * G.WP(d + 1, j);
-        for (int d = k + 1; d < l; ++d) c += G.g4(PF_PfromM, i, j, d, l) * G.WP(k, d - 1);
+        for (int s = 1; s < a; ++s) c += X2(PF_PfromM, s) * WPj(s);
+        for (int s = 1; s < b; ++s) c += X3(PF_PfromM, s) * WPk(s);
         c += PL * 1.0 * PB;
         c += PR * 1.0 * PB;
         put(PF_PfromM, c);
     }
     {  // PfromO (:537-552)
         double c = 0;
-        for (int d = i + 1; d < j; ++d) c += G.g4(PF_PfromO, d, j, k, l) * G.WP(i, d - 1);
-        for (int d = k + 1; d < l; ++d) c += G.g4(PF_PfromO, i, j, k, d) * G.WP(d + 1, l);
+        for (int s = 1; s < a; ++s) c += X1(PF_PfromO, s) * WPi(s);
+        for (int s = 1; s < b; ++s) c += X4(PF_PfromO, s) * WPl(s);
         c += PL * 1.0 * PB;
         c += PR * 1.0 * PB;
         put(PF_PfromO, c);
     }
     {  // PK (:395-412)
         double c = 0;
-        for (int d = i + 1; d < j; ++d) c += G.g4(PF_PK, i, d, k, l) * G.WP(d + 1, j);
-        for (int d = k + 1; d < l; ++d) c += G.g4(PF_PK, i, j, d, l) * G.WP(k, d - 1);
+        for (int s = 1; s < a; ++s) c += X2(PF_PK, s) * WPj(s);
+        for (int s = 1; s < b; ++s) c += X3(PF_PK, s) * WPk(s);
         c += PL * 1.0 * PB;
         c += PM * 1.0 * PB;
         c += PR * 1.0 * PB;
@@ -461,7 +548,7 @@ extern "C" int ccjk_pf_pterm(const PfDev *D, int s, void *stream) {
 extern "C" int ccjk_pf_diag(const PfDev *D, int s, void *stream) {
     const int ni = D->n - s;
     if (ni <= 0) return 0;
-    hipLaunchKernelGGL(k_pf_diag, dim3((unsigned)((ni + 63) / 64)), dim3(64), 0, (hipStream_t)stream, *D, s);
+    hipLaunchKernelGGL(k_pf_diag, dim3((unsigned)ni), dim3(64), 0, (hipStream_t)stream, *D, s);
     return (int)hipGetLastError();
 }
 

@@ -3,7 +3,9 @@ import random
 import sys
 import time
 
-import ccj_amd
+import os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import ccj_amd  # noqa: E402
 
 for n in [int(x) for x in sys.argv[1:]] or [100]:
     r = random.Random(5)
