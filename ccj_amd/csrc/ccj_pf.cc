@@ -175,6 +175,7 @@ struct ccj_pf_ctx {
     double *d_hp = nullptr, *d_est = nullptr, *d_ie = nullptr, *d_mlb = nullptr, *d_cpp = nullptr, *d_pup = nullptr;
     double *d_2d = nullptr;  // CCJ_PF_NMAT2 planes of (n+1)*rs
     long long *d_Pacc = nullptr;
+    unsigned long long *d_Pabs = nullptr;
     int *d_d4 = nullptr;
     PfLvl *d_ld = nullptr;
     hipStream_t st = nullptr;
@@ -278,7 +279,7 @@ void run_threads(int total, int nthr, const std::function<void(int, int)> &f) {
 
 void free_dev(ccj_pf_ctx *c) {
     void *ptrs[] = {c->d_E, c->d_S, c->d_S1, c->d_pt, c->d_pair, c->d_rtype, c->d_hp, c->d_est, c->d_ie,
-                    c->d_mlb, c->d_cpp, c->d_pup, c->d_2d, c->d_Pacc, c->d_d4, c->d_ld};
+                    c->d_mlb, c->d_cpp, c->d_pup, c->d_2d, c->d_Pacc, c->d_Pabs, c->d_d4, c->d_ld};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (c->e0) hipEventDestroy(c->e0);
@@ -294,7 +295,7 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     c->n = (int)c->seq.size();
     const int n = c->n;
     if (n < 1) return pf_err(c, CCJ_E_ARG, "empty sequence");
-    if (n > 295) return pf_err(c, CCJ_E_ARG, "n > 295: P sums may leave the exact integer range of a double");
+    if (n > 1023) return pf_err(c, CCJ_E_ARG, "sequence longer than 1023");
     for (char ch : c->seq)
         if (!(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'U' || ch == 'T'))
             return pf_err(c, CCJ_E_ARG, "sequence must be A/C/G/U/T");
@@ -412,6 +413,7 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     PFCHK(c, up((void **)&c->d_ld, c->lv.data(), c->lv.size() * sizeof(PfLvl)));
     PFCHK(c, hipMalloc((void **)&c->d_2d, (size_t)CCJ_PF_NMAT2 * plane * sizeof(double)));
     PFCHK(c, hipMalloc((void **)&c->d_Pacc, plane * sizeof(long long)));
+    PFCHK(c, hipMalloc((void **)&c->d_Pabs, plane * sizeof(unsigned long long)));
     PFCHK(c, hipMalloc((void **)&c->d_d4, (size_t)std::max(off, 1LL) * sizeof(int)));
 
     PfDev &D = c->D;
@@ -442,6 +444,7 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     D.WPP = pl[CCJ_PF_WPP];
     D.P = pl[CCJ_PF_P];
     D.Pacc = c->d_Pacc;
+    D.Pabs = c->d_Pabs;
     D.d4 = c->d_d4;
     D.ld = c->d_ld;
     return CCJ_OK;
@@ -454,6 +457,7 @@ int fill_impl(ccj_pf_ctx *c) {
     PFCHK(c, hipSetDevice(c->device));
     PFCHK(c, hipMemsetAsync(c->d_2d, 0, (size_t)CCJ_PF_NMAT2 * plane * sizeof(double), c->st));
     PFCHK(c, hipMemsetAsync(c->d_Pacc, 0, plane * sizeof(long long), c->st));
+    PFCHK(c, hipMemsetAsync(c->d_Pabs, 0, plane * sizeof(unsigned long long), c->st));
     PFCHK(c, hipEventRecord(c->e0, c->st));
     // level t needs the 2-D spans <= t-1; span s needs P(s), i.e. the levels <= s-3
     if (n >= 3) PFCHK(c, (hipError_t)ccjk_pf_level(&c->D, c->lv.data(), 0, c->st));
@@ -465,7 +469,18 @@ int fill_impl(ccj_pf_ctx *c) {
     PFCHK(c, hipEventRecord(c->e1, c->st));
     c->h2d.assign((size_t)CCJ_PF_NMAT2 * plane, 0.0);
     PFCHK(c, hipMemcpyAsync(c->h2d.data(), c->d_2d, c->h2d.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));
+    std::vector<unsigned long long> pabs(plane, 0);
+    PFCHK(c, hipMemcpyAsync(pabs.data(), c->d_Pabs, plane * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->st));
     PFCHK(c, hipStreamSynchronize(c->st));
+    // the exact int64 P sums equal the reference's serial double sums only while every partial sum
+    // is an exactly representable integer: guaranteed by sum |term| < 2^53 (part_func.cc:383-393)
+    for (int w = 0; w < n; ++w)
+        for (int p = 1; p + w <= n; ++p)
+            if (pabs[(size_t)w * c->rs + p] >= (1ull << 53)) {
+                char msg[160];
+                snprintf(msg, sizeof msg, "P(%d,%d): sum of |terms| >= 2^53, the reference's double sum may round", p, p + w);
+                return pf_err(c, CCJ_E_PF_RANGE, msg);
+            }
     PFCHK(c, hipEventElapsedTime(&c->fill_ms, c->e0, c->e1));
 
     // W (part_func.cc:163-172)

@@ -14,11 +14,15 @@
 //   * every double sum is accumulated by one thread in the reference's term order, with the
 //     reference's association, and this file is compiled without contraction;
 //   * the 4-D matrices hold what Matrix4DPF keeps: the x86 int truncation of the sum (int32);
-//   * P sums int products made in 32-bit int arithmetic; each partial sum is an integer below
-//     2^53 for n <= 295, so it is accumulated exactly in int64 across threads and converted once;
+//   * P sums int products made in 32-bit int arithmetic, accumulated exactly in int64 across
+//     threads and converted once; that equals the reference's serial double sum whenever the sum
+//     of |terms| stays below 2^53 (always for n <= 295), which the fill checks (Pabs) and
+//     otherwise reports CCJ_E_PF_RANGE instead of a result;
 //   * table values (Boltzmann weights, pow(), the hairpin strstr cases) come from the host libm.
-// A term whose Boltzmann factor is exactly 0.0 adds a signed zero to a sum that is truncated to
-// int (interior-loop windows): such terms are skipped.
+// An interior-loop term whose Boltzmann factor is exactly 0.0 (a pair that cannot pair; the
+// reference skips it) adds a signed zero here: it changes no bit of a nonzero partial sum, and
+// every 4-D sum ends in an int truncation, where the sign of a zero is lost.  So the iloop terms
+// are added branch-free, which lets the loads of consecutive terms overlap.
 #pragma clang fp contract(off)
 
 // CCJ_PF_ABLATE_ILOOP (timing experiments only, wrong results): skip the interior-loop windows
@@ -80,15 +84,19 @@ __global__ __launch_bounds__(64) void k_pf_pterm(PfDev D, int s) {
     const int n = D.n, a1 = jo, h1 = dd - jo - 1, a2 = dd - jo - 1;
     typedef const __attribute__((address_space(1))) int gint;
     long long acc = 0;
+    unsigned long long aabs = 0;
     for (int ko = dd + 1; ko < s; ++ko) {
         const int h2 = ko - dd - 1, t1 = a1 + h2, t2 = a2 + (s - ko - 1);
         const int m1 = n - t1 - 2, m2 = n - t2 - 2;
         const PfLvl L1 = D.ld[t1], L2 = D.ld[t2];
         const long long U1 = L1.lb + PF_PK * L1.C + (long long)a1 * L1.M + (long long)h1 * m1 - (((long long)h1 * (h1 - 1)) >> 1) - 1;
         const long long U2 = L2.lb + PF_PK * L2.C + (long long)a2 * L2.M + (long long)h2 * m2 - (((long long)h2 * (h2 - 1)) >> 1) + jo;
-        acc += imul_wrap(*(gint *)(D.d4 + U1 + i), *(gint *)(D.d4 + U2 + i));
+        const long long x = imul_wrap(*(gint *)(D.d4 + U1 + i), *(gint *)(D.d4 + U2 + i));
+        acc += x;
+        aabs += (unsigned long long)(x < 0 ? -x : x);
     }
     if (acc) atomicAdd((unsigned long long *)&D.Pacc[s * D.rs + i], (unsigned long long)acc);
+    if (aabs) atomicAdd(&D.Pabs[s * D.rs + i], aabs);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -287,87 +295,93 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     auto BPl = [&](int s) { return WBP[(b - s - 1) * rs + k + s + 1]; };
     const double bp = E.bp, ap = E.ap, cp1 = D.cpp[1], PB = E.PB;
 
-    {  // PLmloop00 (:554-568); the seed PL(i,j,k,l) is not computed yet: 0 * beta2P
-        double c = 0;
-        c += 0.0 * bp;
-        for (int s = 0; s <= a; ++s) {
-            if (s > 0) c += WBi(s) * X1(PF_PLmloop00, s);
-            if (s < a) c += X2(PF_PLmloop00, s) * WBj(s);
+    // The split loops of all 20 non-interior recurrences fused into one loop over the (i,j) gap
+    // (s = d-i) and one over the (k,l) gap (s = d-k): each neighbour value is loaded once for every
+    // sum that reads it.  Each sum is its own accumulator and receives its terms in exactly the
+    // reference's order (a sum's (i,j)-gap terms all precede its (k,l)-gap terms, as in its code).
+    double cLm00 = 0, cLm01 = 0, cLm10 = 0, cMm00 = 0, cMm10 = 0, cOm00 = 0, cOm10 = 0;
+    double cFL = 0, cFM = 0, cFO = 0, cK = 0;
+    double cRm00 = 0, cRm01 = 0, cRm10 = 0, cMm01 = 0, cOm01 = 0, cFR = 0;
+    cLm00 += 0.0 * bp;  // PLmloop00 (:554-568): the seed PL(i,j,k,l) is not computed yet: 0 * beta2P
+    cRm00 += 0.0 * bp;  // PRmloop00 (:592-605)
+    cMm00 += 0.0 * bp;  // PMmloop00 (:628-639)
+    cOm00 += 0.0 * bp;  // POmloop00 (:665-676)
+    cRm01 += (b >= 1 ? X(PF_PRmloop01, 1, 0, 0, 0) : 0) * cp1;  // PRmloop01(i,j,k,l-1) * expcp_pen[1] (:608-616)
+    cRm10 += (b >= 1 ? X(PF_PRmloop10, 1, 0, 1, 0) : 0) * cp1;  // PRmloop10(i,j,k+1,l) * expcp_pen[1] (:618-626)
+    cMm01 += (b >= 1 ? X(PF_PMmloop01, 1, 0, 1, 0) : 0) + cp1;  // PMmloop01(i,j,k+1,l) "+ expcp_pen[1]" (:642-650)
+    cMm10 += (a >= 1 ? X(PF_PMmloop10, 1, 1, 1, 0) : 0) * cp1;  // PMmloop10(i,j-1,k,l) * expcp_pen[1] (:652-663)
+    // (i,j) gap, d = i+s
+#pragma unroll 2
+    for (int s = 0; s <= a; ++s) {
+        if (s > 0) {  // X1 = X(i+s, j, k, l), WB(i, i+s-1) / WBP(i, i+s-1)
+            const double bpi = BPi(s), wbi = cpp[s] + bpi;
+            const int lm00 = X1(PF_PLmloop00, s), mm00 = X1(PF_PMmloop00, s), om00 = X1(PF_POmloop00, s);
+            cLm00 += wbi * lm00;  // :558-560
+            cLm10 += bpi * lm00;  // :582-584
+            cMm10 += bpi * mm00;  // :656-658
+            cOm00 += wbi * om00;  // :669-670
+            cOm10 += bpi * om00;  // :690-692
         }
-        put(PF_PLmloop00, c);
-    }
-    {  // PLmloop01 (:570-578)
-        double c = 0;
-        for (int s = 0; s < a; ++s) c += X2(PF_PLmloop00, s) * BPj(s);
-        put(PF_PLmloop01, c);
-    }
-    {  // PLmloop10 (:580-590)
-        double c = 0;
-        for (int s = 1; s <= a; ++s) {
-            c += BPi(s) * X1(PF_PLmloop00, s);
-            if (s < a) c += X2(PF_PLmloop10, s) * WBj(s);
+        if (s < a) {  // X2 = X(i, i+s, k, l), WB(i+s+1, j) / WBP(i+s+1, j)
+            const double bpj = BPj(s), wbj = cpp[a - s] + bpj;
+            const int lm00 = X2(PF_PLmloop00, s);
+            cLm00 += lm00 * wbj;                      // :561-562
+            cLm01 += lm00 * bpj;                      // :574-576
+            if (s > 0) cLm10 += X2(PF_PLmloop10, s) * wbj;  // :585-587
+            cMm00 += X2(PF_PMmloop00, s) * wbj;       // :632-633
+            if (s > 0) {  // PfromL / PfromM / PfromO / PK: d = i+1 .. j-1, WP(i, d-1), WP(d+1, j)
+                const double wpi = WPi(s), wpj = WPj(s);
+                cFL += X1(PF_PfromL, s) * wpi;  // :491-493
+                cFL += X2(PF_PfromL, s) * wpj;
+                cFM += X2(PF_PfromM, s) * wpj;  // :523-524
+                cFO += X1(PF_PfromO, s) * wpi;  // :540-541
+                cK += X2(PF_PK, s) * wpj;       // :398-399
+            }
         }
-        put(PF_PLmloop10, c);
     }
-    {  // PRmloop00 (:592-605)
-        double c = 0;
-        c += 0.0 * bp;
-        for (int s = 0; s <= b; ++s) {
-            if (s > 0) c += WBk(s) * X3(PF_PRmloop00, s);
-            if (s < b) c += X4(PF_PRmloop00, s) * WBl(s);
+    if (b >= 1) cOm00 = X(PF_POmloop00, 1, 0, 0, 0) * (cpp[1] + WBP[l]);  // :671-673: assigns POmloop00(i,j,k,l-1) * WB(l,l)
+    // (k,l) gap, d = k+s
+#pragma unroll 2
+    for (int s = 0; s <= b; ++s) {
+        if (s > 0) {  // X3 = X(i, j, k+s, l), WB(k, k+s-1) / WBP(k, k+s-1)
+            const double bpk = BPk(s), wbk = cpp[s] + bpk;
+            const int rm00 = X3(PF_PRmloop00, s);
+            cRm00 += wbk * rm00;                   // :596-598
+            cRm10 += bpk * rm00;                   // :622-624
+            cMm00 += X3(PF_PMmloop00, s) * wbk;    // :634-636
         }
-        put(PF_PRmloop00, c);
+        if (s < b) {  // X4 = X(i, j, k, k+s), WB(k+s+1, l) / WBP(k+s+1, l)
+            const double bpl = BPl(s), wbl = cpp[b - s] + bpl;
+            const int rm00 = X4(PF_PRmloop00, s);
+            cRm00 += rm00 * wbl;                   // :599-600
+            cRm01 += rm00 * bpl;                   // :612-614
+            cMm01 += X4(PF_PMmloop00, s) * bpl;    // :646-648
+            cOm01 += X4(PF_POmloop00, s) * bpl;    // :682-684
+            if (s > 0) {  // d = k+1 .. l-1
+                const int om10 = X4(PF_POmloop10, s);
+                const double wpk = WPk(s), wpl = WPl(s);
+                cMm10 += om10 * wbl;               // :659-661
+                cOm10 += om10 + wbl;               // :693-695 ("+ get_WB")
+                cFR += X3(PF_PfromR, s) * wpk;     // :508-510
+                cFR += X4(PF_PfromR, s) * wpl;
+                cFM += X3(PF_PfromM, s) * wpk;     // :526-527
+                cFO += X4(PF_PfromO, s) * wpl;     // :544-545
+                cK += X3(PF_PK, s) * wpk;          // :401-402
+            }
+        }
     }
-    {  // PRmloop01 (:608-616): PRmloop01(i,j,k,l-1) * expcp_pen[1] (0 when k = l: outside the matrix)
-        double c = 0;
-        c += (b >= 1 ? X(PF_PRmloop01, 1, 0, 0, 0) : 0) * cp1;
-        for (int s = 0; s < b; ++s) c += X4(PF_PRmloop00, s) * BPl(s);
-        put(PF_PRmloop01, c);
-    }
-    {  // PRmloop10 (:618-626): PRmloop10(i,j,k+1,l) * expcp_pen[1]
-        double c = 0;
-        c += (b >= 1 ? X(PF_PRmloop10, 1, 0, 1, 0) : 0) * cp1;
-        for (int s = 1; s <= b; ++s) c += BPk(s) * X3(PF_PRmloop00, s);
-        put(PF_PRmloop10, c);
-    }
-    {  // PMmloop00 (:628-639)
-        double c = 0;
-        c += 0.0 * bp;
-        for (int s = 0; s < a; ++s) c += X2(PF_PMmloop00, s) * WBj(s);
-        for (int s = 1; s <= b; ++s) c += X3(PF_PMmloop00, s) * WBk(s);
-        put(PF_PMmloop00, c);
-    }
-    {  // PMmloop01 (:642-650): "+ expcp_pen[1]"
-        double c = 0;
-        c += (b >= 1 ? X(PF_PMmloop01, 1, 0, 1, 0) : 0) + cp1;
-        for (int s = 0; s < b; ++s) c += X4(PF_PMmloop00, s) * BPl(s);
-        put(PF_PMmloop01, c);
-    }
-    {  // PMmloop10 (:652-663): PMmloop10(i,j-1,k,l) * expcp_pen[1]
-        double c = 0;
-        c += (a >= 1 ? X(PF_PMmloop10, 1, 1, 1, 0) : 0) * cp1;
-        for (int s = 1; s <= a; ++s) c += BPi(s) * X1(PF_PMmloop00, s);
-        for (int s = 1; s < b; ++s) c += X4(PF_POmloop10, s) * WBl(s);
-        put(PF_PMmloop10, c);
-    }
-    {  // POmloop00 (:665-676): the second loop assigns, so only its last term survives
-        double c = 0;
-        c += 0.0 * bp;
-        for (int s = 1; s <= a; ++s) c += WBi(s) * X1(PF_POmloop00, s);
-        if (b >= 1) c = X(PF_POmloop00, 1, 0, 0, 0) * (cpp[1] + WBP[l]);  // POmloop00(i,j,k,l-1) * WB(l,l)
-        put(PF_POmloop00, c);
-    }
-    {  // POmloop01 (:679-686)
-        double c = 0;
-        for (int s = 0; s < b; ++s) c += X4(PF_POmloop00, s) * BPl(s);
-        put(PF_POmloop01, c);
-    }
-    {  // POmloop10 (:688-699): "+ get_WB"
-        double c = 0;
-        for (int s = 1; s <= a; ++s) c += BPi(s) * X1(PF_POmloop00, s);
-        for (int s = 1; s < b; ++s) c += X4(PF_POmloop10, s) + WBl(s);
-        put(PF_POmloop10, c);
-    }
+    put(PF_PLmloop00, cLm00);
+    put(PF_PLmloop01, cLm01);
+    put(PF_PLmloop10, cLm10);
+    put(PF_PRmloop00, cRm00);
+    put(PF_PRmloop01, cRm01);
+    put(PF_PRmloop10, cRm10);
+    put(PF_PMmloop00, cMm00);
+    put(PF_PMmloop01, cMm01);
+    put(PF_PMmloop10, cMm10);
+    put(PF_POmloop00, cOm00);
+    put(PF_POmloop01, cOm01);
+    put(PF_POmloop10, cOm10);
 
     // PL (:414-430) with get_PLiloop (:736-756) and get_PLmloop (:758-768); the inner cell
     // (i+1, j-1, k, l) is (t-2, a-2, h+1, i+1), outside the matrix (0) when a < 2
@@ -382,10 +396,11 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
             const int u1m = PF_ILOOP_ON ? imin(a, MAXLOOP) - 2 : -1;
             for (int u1 = 0; u1 <= u1m; ++u1) {
                 const int u2m = imin(a - u1 - 6, PF_IEW - 1);
+#pragma unroll 4
                 for (int u2 = 0; u2 <= u2m; ++u2) {
                     const double e = D.ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + a) * rs + i];
                     const int dt = 2 + u1 + u2;
-                    if (e != 0.0) r += e * X(PF_PL, dt, dt, 1 + u2, 1 + u1) * 1.0;
+                    r += e * X(PF_PL, dt, dt, 1 + u2, 1 + u1) * 1.0;
                 }
             }
             c += r;
@@ -409,10 +424,11 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
             const int u1m = PF_ILOOP_ON ? imin(b, MAXLOOP) - 2 : -1;
             for (int u1 = 0; u1 <= u1m; ++u1) {
                 const int u2m = imin(b - u1 - 6, PF_IEW - 1);
+#pragma unroll 4
                 for (int u2 = 0; u2 <= u2m; ++u2) {
                     const double e = D.ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + b) * rs + k];
                     const int dt = 2 + u1 + u2;
-                    if (e != 0.0) r += e * X(PF_PR, dt, 0, 1 + u1, 0) * 1.0;
+                    r += e * X(PF_PR, dt, 0, 1 + u1, 0) * 1.0;
                 }
             }
             c += r;
@@ -441,10 +457,11 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
             const int u1m = PF_ILOOP_ON ? imin(a - 2, PF_IEW - 1) : -1, u2m = imin(b - 2, PF_IEW - 1);
             for (int u1 = 0; u1 <= u1m; ++u1) {
                 const int d = j - 1 - u1;
+#pragma unroll 4
                 for (int u2 = 0; u2 <= u2m; ++u2) {
                     const double e = D.ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + (h + 4 + u1 + u2)) * rs + d];
                     const int dt = 2 + u1 + u2;
-                    if (e != 0.0) r += e * X(PF_PM, dt, 1 + u1, dt, 0) * 1.0;
+                    r += e * X(PF_PM, dt, 1 + u1, dt, 0) * 1.0;
                 }
             }
             c += r;
@@ -475,47 +492,33 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         }
         PO = put(PF_PO, c);
     }
-    {  // PfromL (:488-503)
-        double c = 0;
-        for (int s = 1; s < a; ++s) {
-            c += X1(PF_PfromL, s) * WPi(s);
-            c += X2(PF_PfromL, s) * WPj(s);
-        }
+    {  // PfromL (:488-503): split terms above, then the same-cell P* terms
+        double c = cFL;
         c += PR * 1.0 * PB;
         c += PM * 1.0 * PB;
         c += PO * 1.0 * PB;
         put(PF_PfromL, c);
     }
     {  // PfromR (:505-518)
-        double c = 0;
-        for (int s = 1; s < b; ++s) {
-            c += X3(PF_PfromR, s) * WPk(s);
-            c += X4(PF_PfromR, s) * WPl(s);
-        }
+        double c = cFR;
         c += PM * 1.0 * PB;
         c += PO * 1.0 * PB;
         put(PF_PfromR, c);
     }
     {  // PfromM (:520-535)
-        double c = 0;
-        for (int s = 1; s < a; ++s) c += X2(PF_PfromM, s) * WPj(s);
-        for (int s = 1; s < b; ++s) c += X3(PF_PfromM, s) * WPk(s);
+        double c = cFM;
         c += PL * 1.0 * PB;
         c += PR * 1.0 * PB;
         put(PF_PfromM, c);
     }
     {  // PfromO (:537-552)
-        double c = 0;
-        for (int s = 1; s < a; ++s) c += X1(PF_PfromO, s) * WPi(s);
-        for (int s = 1; s < b; ++s) c += X4(PF_PfromO, s) * WPl(s);
+        double c = cFO;
         c += PL * 1.0 * PB;
         c += PR * 1.0 * PB;
         put(PF_PfromO, c);
     }
     {  // PK (:395-412)
-        double c = 0;
-        for (int s = 1; s < a; ++s) c += X2(PF_PK, s) * WPj(s);
-        for (int s = 1; s < b; ++s) c += X3(PF_PK, s) * WPk(s);
+        double c = cK;
         c += PL * 1.0 * PB;
         c += PM * 1.0 * PB;
         c += PR * 1.0 * PB;

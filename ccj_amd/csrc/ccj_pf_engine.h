@@ -47,6 +47,7 @@ struct PfDev {
     const double *mlb, *cpp, *pup;  // expMLbase[], expcp_pen[], expPUP_pen[] (n+2)
     double *V, *VM, *WM, *WMv, *WMp, *WBP, *WPP, *P;  // [w][p]
     long long *Pacc;      // [w][p] exact integer P sums
+    unsigned long long *Pabs;  // [w][p] sum of |term| (exactness check: < 2^53 => the reference's double sum is exact)
     int *d4;
     const PfLvl *ld;
 };

