@@ -36,6 +36,7 @@
 #include "../../include/ccj_pf.h"
 #include "ccj_pf_energy.h"
 #include "ccj_pf_engine.h"
+#include "ccj_items.h"
 
 using namespace ccj;
 
@@ -172,11 +173,15 @@ struct ccj_pf_ctx {
     PfExp *d_E = nullptr;
     short *d_S = nullptr, *d_S1 = nullptr;
     int8_t *d_pt = nullptr, *d_pair = nullptr, *d_rtype = nullptr;
-    double *d_hp = nullptr, *d_est = nullptr, *d_ie = nullptr, *d_mlb = nullptr, *d_cpp = nullptr, *d_pup = nullptr;
+    double *d_hp = nullptr, *d_est = nullptr, *d_ieO = nullptr, *d_ieI = nullptr, *d_mlb = nullptr, *d_cpp = nullptr, *d_pup = nullptr;
     double *d_2d = nullptr;  // CCJ_PF_NMAT2 planes of (n+1)*rs
     long long *d_Pacc = nullptr;
     unsigned long long *d_Pabs = nullptr;
     int *d_d4 = nullptr;
+    int *d_cx = nullptr, *d_pmx = nullptr;  // k_pf_iloop's copies of PL / PR and PM (ccj_pf_engine.h)
+    double *d_R = nullptr;                  // k_pf_iloop's sums of one level, 3 planes of max C_t
+    uint32_t *d_items = nullptr;
+    std::vector<long long> ifirst;          // k_pf_iloop items of level t: [ifirst[t], ifirst[t+1])
     PfLvl *d_ld = nullptr;
     hipStream_t st = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -278,8 +283,9 @@ void run_threads(int total, int nthr, const std::function<void(int, int)> &f) {
 }
 
 void free_dev(ccj_pf_ctx *c) {
-    void *ptrs[] = {c->d_E, c->d_S, c->d_S1, c->d_pt, c->d_pair, c->d_rtype, c->d_hp, c->d_est, c->d_ie,
-                    c->d_mlb, c->d_cpp, c->d_pup, c->d_2d, c->d_Pacc, c->d_Pabs, c->d_d4, c->d_ld};
+    void *ptrs[] = {c->d_E, c->d_S, c->d_S1, c->d_pt, c->d_pair, c->d_rtype, c->d_hp, c->d_est, c->d_ieO, c->d_ieI,
+                    c->d_mlb, c->d_cpp, c->d_pup, c->d_2d, c->d_Pacc, c->d_Pabs, c->d_d4, c->d_cx, c->d_pmx,
+                    c->d_R, c->d_items, c->d_ld};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (c->e0) hipEventDestroy(c->e0);
@@ -354,8 +360,10 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
             // get_e_stP (part_func.cc:877-884); w == 0 is never read with a nonzero factor
             if (w >= 1 && w != 2) est[ix] = pow(compute_int_pf(*c, p, p + w, p + 1, p + w - 1), c->pen.e_stP);
         }
-    const size_t ie_n = (size_t)PF_IEW * PF_IEW * plane;
-    std::vector<double> ie(ie_n, 0.0);
+    // ieO / ieI: get_e_intP by outer / inner pair, each pair's 29 x 29 window contiguous
+    constexpr int W2 = PF_IEW * PF_IEW;
+    const size_t ie_n = (size_t)W2 * plane;
+    std::vector<double> ie(ie_n, 0.0), ieI(ie_n, 0.0);
     {
         const int nthr = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         run_threads(n, nthr, [&](int w0, int w1) {
@@ -366,21 +374,64 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
                         for (int u2 = 0; u2 < PF_IEW; ++u2) {
                             const int ip = p + 1 + u1, jp = q - 1 - u2;
                             if (ip >= jp || (u1 == 0 && u2 == 0)) continue;  // get_e_intP's stack case is 0
-                            ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + w) * rs + p] =
+                            ie[((size_t)w * rs + p) * W2 + u1 * PF_IEW + u2] =
                                 pow(compute_int_pf(*c, p, q, ip, jp), c->pen.e_intP);
                         }
                 }
         });
+        // ieI[g][j][u1][u2] = ieO[g+2+u1+u2][j-1-u1][u1][u2] (closing (j-1-u1, j+g+1+u2))
+        run_threads(n, nthr, [&](int g0, int g1) {
+            for (int g = g0; g < g1; ++g)
+                for (int j = 1; j + g <= n; ++j)
+                    for (int u1 = 0; u1 < PF_IEW; ++u1)
+                        for (int u2 = 0; u2 < PF_IEW; ++u2) {
+                            const int p = j - 1 - u1, w = g + 2 + u1 + u2;
+                            if (p < 1 || p + w > n) continue;
+                            ieI[((size_t)g * rs + j) * W2 + u1 * PF_IEW + u2] = ie[((size_t)w * rs + p) * W2 + u1 * PF_IEW + u2];
+                        }
+        });
     }
 
     // level layout
-    c->lv.assign(std::max(n - 2, 1), PfLvl{0, 0, 0, 0});
-    long long off = 0;
+    c->lv.assign(std::max(n - 2, 1), PfLvl{0, 0, 0, 0, 0, 0});
+    long long off = 0, offx = 0, offm = 0, maxC = 1;
     for (int t = 0; t <= n - 3; ++t) {
         const long long m = n - t - 2, M = m * (m + 1) / 2;
-        c->lv[t] = PfLvl{off, (t + 1) * M, (int)M, 0};
+        c->lv[t] = PfLvl{off, (t + 1) * M, (int)M, 0, offx, offm};
         off += (long long)PF_NMAT4 * (t + 1) * M;
+        offx += 2 * (t + 1) * M;
+        offm += m * n * (t + 1);
+        maxC = std::max(maxC, (t + 1) * M);
         c->cells += (t + 1) * M;
+    }
+    // k_pf_iloop work items: the cells of each pairing closing pair in 64-lane chunks, encoded as
+    // ccj_items.h's (unsharded).  PL and PR rows are the MFE engine's; PM rows here start at h = 0,
+    // since get_PMiloop has no hairpin bound on (j, k) (part_func.cc:804-824)
+    std::vector<uint32_t> items;
+    c->ifirst.assign(std::max(n - 1, 2), 0);
+    {
+        struct PT {
+            const int8_t *p;
+            int rs;
+            int operator()(int i, int j) const { return p[(size_t)(j - i) * rs + i]; }
+        } ptf{pt.data(), rs};
+        for (int t = 0; t <= n - 3; ++t) {
+            c->ifirst[t] = (long long)items.size();
+            const ItemRows R = item_rows(n, t, 1, 0);
+            for (int x = 0; x < R.nPL + R.nPR; ++x) {
+                uint32_t it0 = 0;
+                const int cnt = item_row(ptf, n, t, R, x, 1, 0, it0);
+                for (int q = 0; q < cnt; ++q) items.push_back(it0 | (uint32_t)q);
+            }
+            for (int h = 0; h <= R.m - 1; ++h)  // PM: pair (j, k = j+h+2), lanes a in [alo, ahi]
+                for (int j = 1; j + h + 2 <= n; ++j) {
+                    const int k = j + h + 2, alo = std::max(2, t - (n - k)), ahi = std::min(t - 2, j - 1);
+                    if (alo > ahi || ptf(j, k) <= 0) continue;
+                    const uint32_t it0 = (2u << 30) | ((uint32_t)h << 20) | ((uint32_t)j << 10);
+                    for (int q = 0; q <= (ahi - alo) / 64; ++q) items.push_back(it0 | (uint32_t)q);
+                }
+        }
+        c->ifirst[std::max(n - 2, 1)] = (long long)items.size();
     }
 
     // device
@@ -406,7 +457,9 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     PFCHK(c, up((void **)&c->d_rtype, rt8, 8));
     PFCHK(c, up((void **)&c->d_hp, c->hp.data(), plane * sizeof(double)));
     PFCHK(c, up((void **)&c->d_est, est.data(), plane * sizeof(double)));
-    PFCHK(c, up((void **)&c->d_ie, ie.data(), ie_n * sizeof(double)));
+    PFCHK(c, up((void **)&c->d_ieO, ie.data(), ie_n * sizeof(double)));
+    PFCHK(c, up((void **)&c->d_ieI, ieI.data(), ie_n * sizeof(double)));
+    PFCHK(c, up((void **)&c->d_items, items.data(), items.size() * sizeof(uint32_t)));
     PFCHK(c, up((void **)&c->d_mlb, c->mlb.data(), c->mlb.size() * sizeof(double)));
     PFCHK(c, up((void **)&c->d_cpp, c->cpp.data(), c->cpp.size() * sizeof(double)));
     PFCHK(c, up((void **)&c->d_pup, c->pup.data(), c->pup.size() * sizeof(double)));
@@ -415,6 +468,12 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     PFCHK(c, hipMalloc((void **)&c->d_Pacc, plane * sizeof(long long)));
     PFCHK(c, hipMalloc((void **)&c->d_Pabs, plane * sizeof(unsigned long long)));
     PFCHK(c, hipMalloc((void **)&c->d_d4, (size_t)std::max(off, 1LL) * sizeof(int)));
+    // the copies stay 0 where the pair cannot pair (never written): set once per context
+    PFCHK(c, hipMalloc((void **)&c->d_cx, (size_t)std::max(offx, 1LL) * sizeof(int)));
+    PFCHK(c, hipMalloc((void **)&c->d_pmx, (size_t)std::max(offm, 1LL) * sizeof(int)));
+    PFCHK(c, hipMemset(c->d_cx, 0, (size_t)std::max(offx, 1LL) * sizeof(int)));
+    PFCHK(c, hipMemset(c->d_pmx, 0, (size_t)std::max(offm, 1LL) * sizeof(int)));
+    PFCHK(c, hipMalloc((void **)&c->d_R, (size_t)3 * maxC * sizeof(double)));
 
     PfDev &D = c->D;
     D.n = n;
@@ -429,7 +488,8 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     D.rtype = c->d_rtype;
     D.hp = c->d_hp;
     D.est = c->d_est;
-    D.ie = c->d_ie;
+    D.ieO = c->d_ieO;
+    D.ieI = c->d_ieI;
     D.mlb = c->d_mlb;
     D.cpp = c->d_cpp;
     D.pup = c->d_pup;
@@ -446,6 +506,10 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     D.Pacc = c->d_Pacc;
     D.Pabs = c->d_Pabs;
     D.d4 = c->d_d4;
+    D.cx = c->d_cx;
+    D.pmx = c->d_pmx;
+    D.items = c->d_items;
+    D.R = c->d_R;
     D.ld = c->d_ld;
     return CCJ_OK;
 }
@@ -460,11 +524,16 @@ int fill_impl(ccj_pf_ctx *c) {
     PFCHK(c, hipMemsetAsync(c->d_Pabs, 0, plane * sizeof(unsigned long long), c->st));
     PFCHK(c, hipEventRecord(c->e0, c->st));
     // level t needs the 2-D spans <= t-1; span s needs P(s), i.e. the levels <= s-3
-    if (n >= 3) PFCHK(c, (hipError_t)ccjk_pf_level(&c->D, c->lv.data(), 0, c->st));
+    auto level = [&](int t) -> hipError_t {
+        const long long f = c->ifirst[t];
+        hipError_t e = (hipError_t)ccjk_pf_iloop(&c->D, t, f, (int)(c->ifirst[t + 1] - f), c->st);
+        return e != hipSuccess ? e : (hipError_t)ccjk_pf_level(&c->D, c->lv.data(), t, c->st);
+    };
+    if (n >= 3) PFCHK(c, level(0));
     for (int s = 0; s <= n - 1; ++s) {
         PFCHK(c, (hipError_t)ccjk_pf_pterm(&c->D, s, c->st));
         PFCHK(c, (hipError_t)ccjk_pf_diag(&c->D, s, c->st));
-        if (s + 1 <= n - 3) PFCHK(c, (hipError_t)ccjk_pf_level(&c->D, c->lv.data(), s + 1, c->st));
+        if (s + 1 <= n - 3) PFCHK(c, level(s + 1));
     }
     PFCHK(c, hipEventRecord(c->e1, c->st));
     c->h2d.assign((size_t)CCJ_PF_NMAT2 * plane, 0.0);

@@ -23,14 +23,11 @@
 // reference skips it) adds a signed zero here: it changes no bit of a nonzero partial sum, and
 // every 4-D sum ends in an int truncation, where the sign of a zero is lost.  So the iloop terms
 // are added branch-free, which lets the loads of consecutive terms overlap.
+// The interior-loop sums (get_PLiloop / get_PRiloop / get_PMiloop, up to 29 x 29 terms per cell)
+// run before each level in k_pf_iloop, one wave per closing pair (i,j) / (k,l) / (j,k) and its
+// cells, reading copies of PL / PR / PM laid out so that the 64 lanes of one candidate term read
+// consecutive words; k_pf_level adds the finished sums in their place.
 #pragma clang fp contract(off)
-
-// CCJ_PF_ABLATE_ILOOP (timing experiments only, wrong results): skip the interior-loop windows
-#ifdef CCJ_PF_ABLATE_ILOOP
-#define PF_ILOOP_ON 0
-#else
-#define PF_ILOOP_ON 1
-#endif
 
 #include <hip/hip_runtime.h>
 
@@ -260,7 +257,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     while ((h + 1) * m - (((h + 1) * h) >> 1) <= off) ++h;
     const int i = off - (h * m - ((h * (h - 1)) >> 1)) + 1, j = i + a, k = j + h + 2, l = k + b;
     int *cell = D.d4 + L.lb + (long long)a * L.M + off;
-    const long long C = L.C;
+    const long long C = L.C, off0 = (long long)a * L.M + off;  // off0: the cell in R's planes
     auto put = [&](int x, double v) -> int {
         const int r = x86_trunc(v);
         cell[x * C] = r;
@@ -391,18 +388,8 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         if (G.pt(i, j) > 0) {
             const bool in = a >= 2;
             double r = 0;
-            r += (in ? X(PF_PL, 2, 2, 1, 1) : 0) * D.est[a * rs + i];
-            // d = i+1+u1 < min(j, i+30); dp = j-1-u2 > max(d+3, j-30): u1 <= min(a,30)-2, u2 <= min(a-u1-6, 28)
-            const int u1m = PF_ILOOP_ON ? imin(a, MAXLOOP) - 2 : -1;
-            for (int u1 = 0; u1 <= u1m; ++u1) {
-                const int u2m = imin(a - u1 - 6, PF_IEW - 1);
-#pragma unroll 4
-                for (int u2 = 0; u2 <= u2m; ++u2) {
-                    const double e = D.ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + a) * rs + i];
-                    const int dt = 2 + u1 + u2;
-                    r += e * X(PF_PL, dt, dt, 1 + u2, 1 + u1) * 1.0;
-                }
-            }
+            if (a >= 6) r = D.R[off0];  // k_pf_iloop: the stack term, then the window
+            else r += (in ? X(PF_PL, 2, 2, 1, 1) : 0) * D.est[a * rs + i];  // no window (u2 <= a-u1-6)
             c += r;
             double q = 0;
             q += (in ? X(PF_PLmloop10, 2, 2, 1, 1) : 0) * ap * bp;
@@ -411,6 +398,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
             if (j >= i + TURN + 1) c += (in ? X(PF_PfromL, 2, 2, 1, 1) : 0) * 1.0;
         }
         PL = put(PF_PL, c);
+        if (G.pt(i, j) > 0) D.cx[L.lbx + a * L.M + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = PL;
     }
     // PR (:432-447), get_PRiloop (:770-790), get_PRmloop (:792-802); (i, j, k+1, l-1) is
     // (t-2, a, h+1, i), outside when b < 2
@@ -420,17 +408,8 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         if (G.pt(k, l) > 0) {
             const bool in = b >= 2;
             double r = 0;
-            r += (in ? X(PF_PR, 2, 0, 1, 0) : 0) * D.est[b * rs + k];
-            const int u1m = PF_ILOOP_ON ? imin(b, MAXLOOP) - 2 : -1;
-            for (int u1 = 0; u1 <= u1m; ++u1) {
-                const int u2m = imin(b - u1 - 6, PF_IEW - 1);
-#pragma unroll 4
-                for (int u2 = 0; u2 <= u2m; ++u2) {
-                    const double e = D.ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + b) * rs + k];
-                    const int dt = 2 + u1 + u2;
-                    r += e * X(PF_PR, dt, 0, 1 + u1, 0) * 1.0;
-                }
-            }
+            if (b >= 6) r = D.R[C + off0];
+            else r += (in ? X(PF_PR, 2, 0, 1, 0) : 0) * D.est[b * rs + k];
             c += r;
             double q = 0;
             q += (in ? X(PF_PRmloop10, 2, 0, 1, 0) : 0) * ap * bp;
@@ -439,6 +418,8 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
             if (l >= k + TURN + 1) c += (in ? X(PF_PfromR, 2, 0, 1, 0) : 0) * 1.0;
         }
         PR = put(PF_PR, c);
+        const int q = i + h - 1;
+        if (G.pt(k, l) > 0) D.cx[L.lbx + C + a * L.M + ((q * (q + 1)) >> 1) + i - 1] = PR;
     }
     // PM (:449-467), get_PMiloop (:804-824), get_PMmloop (:826-836); (i, j-1, k+1, l) is
     // (t-2, a-1, h+2, i), outside when a < 1 or b < 1
@@ -452,18 +433,8 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
             // or S[n+1]; the factor multiplies PM(i, j-1, k+1, l), which is then outside the matrix
             // (0), so any finite value gives 0 — use 0 instead of reading past the table
             const double est_m = (j > 1 && k < n) ? D.est[(h + 4) * rs + (j - 1)] : 0.0;
-            r += (in ? X(PF_PM, 2, 1, 2, 0) : 0) * est_m;
-            // d = j-1-u1 > max(i, j-30), dp = k+1+u2 < min(l, k+30): u1 <= min(a-2, 28), u2 <= min(b-2, 28)
-            const int u1m = PF_ILOOP_ON ? imin(a - 2, PF_IEW - 1) : -1, u2m = imin(b - 2, PF_IEW - 1);
-            for (int u1 = 0; u1 <= u1m; ++u1) {
-                const int d = j - 1 - u1;
-#pragma unroll 4
-                for (int u2 = 0; u2 <= u2m; ++u2) {
-                    const double e = D.ie[((size_t)(u1 * PF_IEW + u2) * (n + 1) + (h + 4 + u1 + u2)) * rs + d];
-                    const int dt = 2 + u1 + u2;
-                    r += e * X(PF_PM, dt, 1 + u1, dt, 0) * 1.0;
-                }
-            }
+            if (a >= 2 && b >= 2) r = D.R[2 * C + off0];
+            else r += (in ? X(PF_PM, 2, 1, 2, 0) : 0) * est_m;
             c += r;
             double q = 0;
             q += (in ? X(PF_PMmloop10, 2, 1, 2, 0) : 0) * ap * bp;
@@ -473,6 +444,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
             if (i == j && k == l) c += 1.0;
         }
         PM = put(PF_PM, c);
+        if (G.pt(j, k) > 0) D.pmx[L.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = PM;
     }
     // PO (:469-486), get_POiloop (:838-858: reads PO(d,j,dp,k) with dp > k, always 0), get_POmloop;
     // (i+1, j, k, l-1) is (t-2, a-1, h, i+1), outside when a < 1 or b < 1
@@ -527,6 +499,112 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Interior-loop sums of level t (get_PLiloop :736-756, get_PRiloop :770-790, get_PMiloop :804-824),
+// one wave per work item of ccj_items.h (a closing pair and up to 64 of the cells it closes):
+//   PL  pair (i, j = i+a), lanes h      PL(d, dp, k, l)  = PLx(t-dt, a-dt, h+1+u2, d)
+//   PR  pair (k, l = k+b), lanes i      PR(i, j, d, dp)  = PRx(t-dt, a, h+1+u1, i)
+//   PM  pair (j, k),       lanes a      PM(i, d, dp, l)  = PMx(t-dt, h+dt, d, a-1-u1)
+// (dt = 2+u1+u2).  In each copy the lanes of one term read consecutive words; the weights of one
+// pair's window are contiguous (ieO / ieI) and wave-uniform, so they come through scalar loads.
+// r = stack term, then the window terms in the reference's (u1, u2) order; the copies hold 0 where
+// the inner pair cannot pair (the 4-D value there is 0), so every term is added branch-free.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long first, int nitems) {
+    const int wv = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (wv >= nitems) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t it = (uint32_t)__builtin_amdgcn_readfirstlane((int)D.items[first + wv]);
+    const int role = (int)(it >> 30), f1 = (int)((it >> 20) & 1023), f2 = (int)((it >> 10) & 1023), ch = (int)(it & 1023);
+    const PfG G{D};
+    const int n = D.n, rs = D.rs, m = n - t - 2;
+    const PfLvl L = D.ld[t];
+    typedef const __attribute__((address_space(1))) int gint;
+    const int *cx = D.cx, *pmx = D.pmx;
+    constexpr int W2 = PF_IEW * PF_IEW;
+    double r = 0;
+    long long dst;  // the cell in R
+    bool act;
+    if (role == 0) {  // PL: lanes h <= m-i
+        const int a = f1, i = f2, j = i + a, h = ch * 64 + lane;
+        act = h <= m - i;
+        const int hc = act ? h : m - i;
+        dst = (long long)a * L.M + hc * m - ((hc * (hc - 1)) >> 1) + i - 1;
+        {   // PL(i+1, j-1, k, l) = PLx(t-2, a-2, h+1, i+1)
+            const PfLvl L2 = D.ld[t - 2];
+            const int x = *(gint *)(cx + L2.lbx + (long long)(a - 2) * L2.M + i * (m + 2) - ((i * (i - 1)) >> 1) + hc + 1);
+            r += x * D.est[a * rs + i];
+        }
+        // d = i+1+u1 < min(j, i+30); dp = j-1-u2 > max(d+3, j-30): u1 <= min(a,30)-2, u2 <= min(a-u1-6, 28)
+        const double *ew = D.ieO + ((size_t)a * rs + i) * W2;
+        const int u1m = imin(a, MAXLOOP) - 2;
+        for (int u1 = 0; u1 <= u1m; ++u1) {
+            const int d = i + 1 + u1, u2m = imin(a - u1 - 6, PF_IEW - 1);
+#pragma unroll 4
+            for (int u2 = 0; u2 <= u2m; ++u2) {
+                const int dt = 2 + u1 + u2, ms = m + dt;
+                const PfLvl Ls = D.ld[t - dt];
+                const int x = *(gint *)(cx + Ls.lbx + (long long)(a - dt) * Ls.M + (d - 1) * ms - (((d - 1) * (d - 2)) >> 1) +
+                                        hc + 1 + u2);
+                r += ew[u1 * PF_IEW + u2] * x * 1.0;
+            }
+        }
+    } else if (role == 1) {  // PR: q = i+h-1 fixed, lanes i <= q+1
+        const int a = f1, q = f2, b = t - a, k = q + a + 3, i = ch * 64 + lane + 1;
+        act = i <= q + 1;
+        const int ic = act ? i : q + 1, h = q + 1 - ic;
+        dst = L.C + (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) + ic - 1;
+        {   // PR(i, j, k+1, l-1) = PRx(t-2, a, h+1, i): row q+1
+            const PfLvl L2 = D.ld[t - 2];
+            const int x = *(gint *)(cx + L2.lbx + L2.C + (long long)a * L2.M + (((q + 1) * (q + 2)) >> 1) + ic - 1);
+            r += x * D.est[b * rs + k];
+        }
+        const double *ew = D.ieO + ((size_t)b * rs + k) * W2;
+        const int u1m = imin(b, MAXLOOP) - 2;
+        for (int u1 = 0; u1 <= u1m; ++u1) {
+            const int u2m = imin(b - u1 - 6, PF_IEW - 1), qq = q + 1 + u1;
+            const int rowo = ((qq * (qq + 1)) >> 1) + ic - 1;
+#pragma unroll 4
+            for (int u2 = 0; u2 <= u2m; ++u2) {
+                const PfLvl Ls = D.ld[t - 2 - u1 - u2];
+                const int x = *(gint *)(cx + Ls.lbx + Ls.C + (long long)a * Ls.M + rowo);
+                r += ew[u1 * PF_IEW + u2] * x * 1.0;
+            }
+        }
+    } else {  // PM: pair (j, k = j+h+2), lanes a in [alo, ahi]
+        const int h = f1, j = f2, k = j + h + 2;
+        const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, j - 1);
+        const int a = alo + ch * 64 + lane;
+        act = a <= ahi;
+        const int ac = act ? a : ahi, i = j - ac, b = t - ac;
+        dst = 2 * L.C + (long long)ac * L.M + h * m - ((h * (h - 1)) >> 1) + i - 1;
+        {   // PM(i, j-1, k+1, l) = PMx(t-2, h+2, j-1, a-1); a >= 2, b >= 2 so j > 1 and k < n
+            const PfLvl L2 = D.ld[t - 2];
+            const int x = *(gint *)(pmx + L2.pmb + ((long long)(h + 2) * n + j - 2) * (t - 1) + ac - 1);
+            r += x * D.est[(h + 4) * rs + (j - 1)];
+        }
+        // d = j-1-u1 > max(i, j-30), dp = k+1+u2 < min(l, k+30): u1 <= min(a-2, 28), u2 <= min(b-2, 28)
+        const double *ew = D.ieI + ((size_t)(h + 2) * rs + j) * W2;
+        const int u1m = imin(ahi - 2, PF_IEW - 1), u2m = imin(t - alo - 2, PF_IEW - 1);
+        const int u2l = b - 2;  // this lane's u2 bound
+        for (int u1 = 0; u1 <= u1m; ++u1) {
+            const int d = j - 1 - u1;
+            const bool on1 = u1 <= ac - 2;
+            const int ap = imax(ac - 1 - u1, 0);
+            const int u2e = imin(u2m, t - 4 - u1);  // a lane with u1 <= a-2 has b-2 <= t-4-u1
+#pragma unroll 4
+            for (int u2 = 0; u2 <= u2e; ++u2) {
+                const int dt = 2 + u1 + u2, tp = t - dt;
+                const PfLvl Ls = D.ld[tp];
+                const int x = *(gint *)(pmx + Ls.pmb + ((long long)(h + dt) * n + d - 1) * (tp + 1) + imin(ap, tp));
+                const double v = ew[u1 * PF_IEW + u2] * x * 1.0;
+                if (on1 && u2 <= u2l) r += v;
+            }
+        }
+    }
+    if (act) D.R[dst] = r;
+}
+
 // canonical-order gather of one 4-D matrix for the parity hashes: out[q] for the q-th cell of
 // i = 1..n, j = i..n, k = j+2..n, l = k..n; one thread per (i, j, k) row of l.
 __global__ __launch_bounds__(256) void k_pf_canon(PfDev D, int x, const long long *__restrict__ rowoff, int nrows,
@@ -560,6 +638,13 @@ extern "C" int ccjk_pf_level(const PfDev *D, const PfLvl *Lh, int t, void *strea
     if (M <= 0) return 0;
     hipLaunchKernelGGL(k_pf_level, dim3((unsigned)((M + 255) / 256), (unsigned)(t + 1)), dim3(256), 0, (hipStream_t)stream,
                        *D, t);
+    return (int)hipGetLastError();
+}
+
+extern "C" int ccjk_pf_iloop(const PfDev *D, int t, long long first, int nitems, void *stream) {
+    if (nitems <= 0) return 0;
+    hipLaunchKernelGGL(k_pf_iloop, dim3((unsigned)((nitems + 3) / 4)), dim3(256), 0, (hipStream_t)stream, *D, t, first,
+                       nitems);
     return (int)hipGetLastError();
 }
 

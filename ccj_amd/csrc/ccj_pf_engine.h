@@ -5,8 +5,10 @@
 //   elem(x,t,a,h,i) = lb_t + x*C_t + a*M_t + h*m_t - h(h-1)/2 + (i-1),  m_t = n-t-2,
 //   M_t = m_t(m_t+1)/2, C_t = (t+1) M_t.
 // 2-D matrices: doubles, span-major [w][p] with row stride rs = n+2.
-// Interior-loop weights ie[u1][u2][w][p] = get_e_intP of the loop closed by (p, p+w) around
-// (p+1+u1, p+w-1-u2) (part_func.cc:886-891), u1, u2 < PF_IEW.
+// Interior-loop weights get_e_intP (part_func.cc:886-891), u1, u2 < PF_IEW, in two layouts whose
+// 29 x 29 window of one pair is contiguous (k_pf_iloop reads a window row with one load):
+//   ieO[w][p][u1][u2]: the loop closed by (p, p+w) around (p+1+u1, p+w-1-u2)   (PL, PR)
+//   ieI[g][j][u1][u2]: the loop closed by (j-1-u1, j+g+1+u2) around (j, j+g)    (PM)
 #pragma once
 #include <stdint.h>
 
@@ -32,6 +34,8 @@ struct PfLvl {
     long long C;   // cells of one matrix at level t
     int M;         // cells of one a-block
     int pad;
+    long long lbx; // element offset of level t in the PL/PR copies (PLx then PRx, C each)
+    long long pmb; // element offset of level t in the PM copy (m * n * (t+1))
 };
 
 struct PfDev {
@@ -43,13 +47,20 @@ struct PfDev {
     const int8_t *rtype;  // 8
     const double *hp;     // [w][p] HairpinE
     const double *est;    // [w][p] get_e_stP
-    const double *ie;     // [u1][u2][w][p] get_e_intP
+    const double *ieO, *ieI;  // get_e_intP by outer / inner pair (above)
     const double *mlb, *cpp, *pup;  // expMLbase[], expcp_pen[], expPUP_pen[] (n+2)
     double *V, *VM, *WM, *WMv, *WMp, *WBP, *WPP, *P;  // [w][p]
     long long *Pacc;      // [w][p] exact integer P sums
     unsigned long long *Pabs;  // [w][p] sum of |term| (exactness check: < 2^53 => the reference's double sum is exact)
     int *d4;
     const PfLvl *ld;
+    // interior-loop copies of PL / PR / PM in the MFE engine's layouts (written by
+    // k_pf_level where the pair can pair), so that k_pf_iloop's lanes read consecutive words:
+    //   PLx(t,a,h,i) = lbx + a*M + G(i-1) + h;  PRx = lbx + C + a*M + q(q+1)/2 + i-1, q = i+h-1;
+    //   PMx = pmb + (h*n + j-1)*(t+1) + a
+    int *cx, *pmx;
+    const uint32_t *items;  // k_pf_iloop work items of all levels (ccj_items.h)
+    double *R;              // k_pf_iloop's interior-loop sums of the level being filled, [role][a*M + off]
 };
 
 }  // namespace ccj
@@ -58,5 +69,6 @@ extern "C" {
 int ccjk_pf_pterm(const ccj::PfDev *D, int s, void *stream);
 int ccjk_pf_diag(const ccj::PfDev *D, int s, void *stream);
 int ccjk_pf_level(const ccj::PfDev *D, const ccj::PfLvl *Lh, int t, void *stream);
+int ccjk_pf_iloop(const ccj::PfDev *D, int t, long long first, int nitems, void *stream);
 int ccjk_pf_canon(const ccj::PfDev *D, int x, const long long *rowoff, int nrows, int *out, void *stream);
 }
