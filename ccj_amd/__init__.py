@@ -184,6 +184,12 @@ def lib() -> ctypes.CDLL:
     L.ccj_pf_last_message.restype = cp
     L.ccj_pf_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     L.ccj_pf_timing.restype = ip
+    L.ccj_pf_set_timing.argtypes = [vp, ip]
+    L.ccj_pf_set_timing.restype = ip
+    L.ccj_pf_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+    L.ccj_pf_kernel_ms.restype = ip
+    L.ccj_pf_work_model.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+    L.ccj_pf_work_model.restype = ip
     _lib = L
     return L
 
@@ -634,6 +640,24 @@ class W_final_pf:
         t = ctypes.c_float()
         self._check(lib().ccj_pf_timing(self._h, ctypes.byref(t)))
         return t.value
+
+    PF_KERNELS = ("k_pf_iloop", "k_pf_level", "k_pf_pterm", "k_pf_diag")
+
+    def set_timing(self, on: bool = True):
+        """Event pairs around every launch of the following fills (ccj_pf_set_timing)."""
+        self._check(lib().ccj_pf_set_timing(self._h, 1 if on else 0))
+
+    def kernel_ms(self) -> dict:
+        """Summed launch durations of the last timed fill per kernel family (ms)."""
+        v = (ctypes.c_double * 4)()
+        self._check(lib().ccj_pf_kernel_ms(self._h, v))
+        return dict(zip(self.PF_KERNELS, v))
+
+    def work_model(self) -> dict:
+        """Algorithmic HBM bytes of one fill per kernel family (ccj_pf_work_model)."""
+        v = (ctypes.c_double * 4)()
+        self._check(lib().ccj_pf_work_model(self._h, v))
+        return dict(zip(self.PF_KERNELS, v))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -180,8 +180,9 @@ struct ccj_pf_ctx {
     int *d_d4 = nullptr;
     int *d_cx = nullptr, *d_pmx = nullptr;  // k_pf_iloop's copies of PL / PR and PM (ccj_pf_engine.h)
     double *d_R = nullptr;                  // k_pf_iloop's sums of one level, 3 planes of max C_t
-    uint32_t *d_items = nullptr;
+    uint32_t *d_items = nullptr, *d_mO = nullptr, *d_mI = nullptr;
     std::vector<long long> ifirst;          // k_pf_iloop items of level t: [ifirst[t], ifirst[t+1])
+    std::vector<uint32_t> h_items, h_mO, h_mI;  // host copies (ccj_pf_work_model)
     PfLvl *d_ld = nullptr;
     hipStream_t st = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -192,6 +193,11 @@ struct ccj_pf_ctx {
     std::vector<double> W;
     double energy = 0;
     float fill_ms = 0;
+    // per-kernel-family timing (ccj_pf_set_timing): an event pair around every launch
+    bool timing = false;
+    std::vector<hipEvent_t> tev;
+    std::vector<int> tfam;      // family of launch q: 0 k_pf_iloop, 1 k_pf_level, 2 k_pf_pterm, 3 k_pf_diag
+    double kms[4] = {0, 0, 0, 0};
     std::string msg;
     // vrna_urn() of the reference build: rand() / RAND_MAX (utils.c:262-271, no HAVE_ERAND48), on
     // this context's own glibc random_r state (a fresh one behaves like a process that never
@@ -285,12 +291,116 @@ void run_threads(int total, int nthr, const std::function<void(int, int)> &f) {
 void free_dev(ccj_pf_ctx *c) {
     void *ptrs[] = {c->d_E, c->d_S, c->d_S1, c->d_pt, c->d_pair, c->d_rtype, c->d_hp, c->d_est, c->d_ieO, c->d_ieI,
                     c->d_mlb, c->d_cpp, c->d_pup, c->d_2d, c->d_Pacc, c->d_Pabs, c->d_d4, c->d_cx, c->d_pmx,
-                    c->d_R, c->d_items, c->d_ld};
+                    c->d_R, c->d_items, c->d_mO, c->d_mI, c->d_ld};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (c->e0) hipEventDestroy(c->e0);
     if (c->e1) hipEventDestroy(c->e1);
+    for (hipEvent_t e : c->tev) hipEventDestroy(e);
+    c->tev.clear();
     if (c->st) hipStreamDestroy(c->st);
+}
+
+// Algorithmic bytes of one fill per kernel family (ccj_pf_work_model): the operands each kernel's
+// recurrences read from and write to HBM-resident arrays, counted from the same enumerations the
+// kernels run (the small 2-D tables and weight windows, which stay in cache, are not charged).
+//   k_pf_iloop: 4 B per active lane per window term it loads (masked), 4 B stack operand, 8 B R store
+//   k_pf_level: 4 B per 4-D operand load of the 21 recurrences (split loops, seeds, P blocks as
+//               evaluated for this sequence's pairs), 8 B per R read, 21 x 4 B stores + 4 B per copy
+//   k_pf_pterm: 2 x 4 B per PK product;  k_pf_diag: 8 B per 2-D operand of the span's sums
+struct PfWork {
+    double iloop = 0, level = 0, pterm = 0, diag = 0;
+};
+
+PfWork pf_work_model(const ccj_pf_ctx &c) {
+    const int n = c.n, rs = c.rs;
+    PfWork w;
+    if (n < 3) return w;
+    auto low = [](int u) { return u < 0 ? 0u : (2u << u) - 1u; };
+    const int nthr = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<double> il(n, 0.0), lv(n, 0.0);
+    run_threads(n - 2, nthr, [&](int t0, int t1) {
+        for (int t = t0; t < t1; ++t) {
+            const int m = n - t - 2;
+            double b_il = 0;
+            for (long long q = c.ifirst[t]; q < c.ifirst[t + 1]; ++q) {
+                const uint32_t it = c.h_items[q];
+                const int role = (int)(it >> 30), f1 = (int)((it >> 20) & 1023), f2 = (int)((it >> 10) & 1023),
+                          ch = (int)(it & 1023);
+                if (role < 2) {
+                    const int a = f1, b = t - a;
+                    const int lanes = role == 0 ? std::min(64, m - f2 + 1 - ch * 64) : std::min(64, f2 + 1 - ch * 64);
+                    const int w0 = role == 0 ? a : b, p0 = role == 0 ? f2 : f2 + a + 3;
+                    const uint32_t *mw = c.h_mO.data() + ((size_t)w0 * rs + p0) * PF_IEW;
+                    long long terms = 0;
+                    for (int u1 = 0; u1 <= std::min(w0, MAXLOOP) - 2; ++u1)
+                        terms += __builtin_popcount(mw[u1] & low(std::min(w0 - u1 - 6, PF_IEW - 1)));
+                    b_il += (double)lanes * (12.0 + 4.0 * terms);
+                } else {
+                    const int h = f1, j = f2, k = j + h + 2;
+                    const int alo = std::max(2, t - (n - k)), ahi = std::min(t - 2, j - 1);
+                    const int a0 = alo + ch * 64, a1 = std::min(ahi, a0 + 63);
+                    const uint32_t *mw = c.h_mI.data() + ((size_t)(h + 2) * rs + j) * PF_IEW;
+                    double lt = 0;
+                    for (int u1 = 0; u1 <= std::min(a1 - 2, PF_IEW - 1); ++u1) {
+                        uint32_t mk = mw[u1] & low(std::min(std::min(t - a0 - 2, PF_IEW - 1), t - 4 - u1));
+                        while (mk) {
+                            const int u2 = __builtin_ctz(mk);
+                            mk &= mk - 1;
+                            lt += std::max(0, std::min(a1, t - 2 - u2) - std::max(a0, u1 + 2) + 1);
+                        }
+                    }
+                    b_il += 12.0 * (a1 - a0 + 1) + 4.0 * lt;
+                }
+            }
+            il[t] = b_il;
+            double b_lv = 0;
+            for (int a = 0; a <= t; ++a) {
+                const int b = t - a;
+                const double split = (a >= 1 ? 11.0 * a - 6 : 0) + (b >= 1 ? 11.0 * b - 6 : 0) + 4.0 * (b >= 1) + (a >= 1);
+                for (int h = 0; h < m; ++h)
+                    for (int i = 1; i + h <= m; ++i) {
+                        const int j = i + a, k = j + h + 2, l = k + b;
+                        double r4 = split, by = 21.0 * 4;
+                        if (c.ptype(i, j) > 0) {
+                            const bool in = a >= 2;
+                            by += (a >= 6 ? 8 : 0) + 4;  // R or the stack operand; the copy store
+                            r4 += (a < 6 && in ? 1 : 0) + (in ? 2 : 0) + (in && j >= i + TURN + 1 ? 1 : 0);
+                        }
+                        if (c.ptype(k, l) > 0) {
+                            const bool in = b >= 2;
+                            by += (b >= 6 ? 8 : 0) + 4;
+                            r4 += (b < 6 && in ? 1 : 0) + (in ? 2 : 0) + (in && l >= k + TURN + 1 ? 1 : 0);
+                        }
+                        const bool in11 = a >= 1 && b >= 1;
+                        if (c.ptype(j, k) > 0) {
+                            const bool rr = a >= 2 && b >= 2;
+                            by += (rr ? 8 : 0) + 4;
+                            r4 += (!rr && in11 ? 1 : 0) + (in11 ? 2 : 0) + (in11 && k >= j + TURN - 1 ? 1 : 0);
+                        }
+                        if (c.ptype(i, l) > 0) r4 += in11 ? 3 + (l >= i + TURN + 1 ? 1 : 0) : 0;
+                        b_lv += 4.0 * r4 + by;
+                    }
+            }
+            lv[t] = b_lv;
+        }
+    });
+    for (int t = 0; t < n; ++t) {
+        w.iloop += il[t];
+        w.level += lv[t];
+    }
+    for (int s = 3; s <= n - 1; ++s)  // C(s,3) (j, d, k) triples per i, two 4-B operands each
+        w.pterm += 8.0 * (n - s) * ((double)s * (s - 1) * (s - 2) / 6.0);
+    for (int s = 0; s <= n - 1; ++s)
+        for (int i = 1; i + s <= n; ++i) {
+            const int j = i + s;
+            double ops = 0;
+            for (int k = i + 1; k <= std::min(j - TURN - 2, i + MAXLOOP + 1); ++k)
+                ops += std::max(0, j - (std::max(k + TURN + 1 + MAXLOOP + 2, k + j - i) - MAXLOOP - 2));
+            ops += 3.0 * std::max(0, j - TURN - 1 - i) * 2 + 2.0 * s * 3 * 2 + 4.0 * std::max(0, j - TURN - i) * 3;
+            w.diag += 8.0 * ops;
+        }
+    return w;
 }
 
 int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_pf_ctx *c) {
@@ -391,6 +501,25 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
                         }
         });
     }
+    // window masks: a term adds nothing when its weight is 0.0 or the pair of the 4-D value it reads
+    // cannot pair (that value is 0): mO over (p+1+u1, p+w-1-u2), mI over (j-1-u1, j+g+1+u2)
+    std::vector<uint32_t> mO(plane * PF_IEW, 0u), mI(plane * PF_IEW, 0u);
+    for (int w = 0; w <= n - 1; ++w)
+        for (int p = 1; p + w <= n; ++p)
+            for (int u1 = 0; u1 < PF_IEW; ++u1) {
+                const size_t r = ((size_t)w * rs + p) * PF_IEW + u1;
+                for (int u2 = 0; u2 < PF_IEW; ++u2) {
+                    const size_t e = ((size_t)w * rs + p) * W2 + u1 * PF_IEW + u2;
+                    {   // outer (p, p+w)
+                        const int ip = p + 1 + u1, jp = p + w - 1 - u2;
+                        if (ip < jp && ie[e] != 0.0 && c->ptype(ip, jp) > 0) mO[r] |= 1u << u2;
+                    }
+                    {   // inner (p, p+w) = (j, j+g)
+                        const int d = p - 1 - u1, dp = p + w + 1 + u2;
+                        if (d >= 1 && dp <= n && ieI[e] != 0.0 && c->ptype(d, dp) > 0) mI[r] |= 1u << u2;
+                    }
+                }
+            }
 
     // level layout
     c->lv.assign(std::max(n - 2, 1), PfLvl{0, 0, 0, 0, 0, 0});
@@ -460,6 +589,11 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     PFCHK(c, up((void **)&c->d_ieO, ie.data(), ie_n * sizeof(double)));
     PFCHK(c, up((void **)&c->d_ieI, ieI.data(), ie_n * sizeof(double)));
     PFCHK(c, up((void **)&c->d_items, items.data(), items.size() * sizeof(uint32_t)));
+    PFCHK(c, up((void **)&c->d_mO, mO.data(), mO.size() * sizeof(uint32_t)));
+    PFCHK(c, up((void **)&c->d_mI, mI.data(), mI.size() * sizeof(uint32_t)));
+    c->h_items = std::move(items);
+    c->h_mO = std::move(mO);
+    c->h_mI = std::move(mI);
     PFCHK(c, up((void **)&c->d_mlb, c->mlb.data(), c->mlb.size() * sizeof(double)));
     PFCHK(c, up((void **)&c->d_cpp, c->cpp.data(), c->cpp.size() * sizeof(double)));
     PFCHK(c, up((void **)&c->d_pup, c->pup.data(), c->pup.size() * sizeof(double)));
@@ -490,6 +624,8 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     D.est = c->d_est;
     D.ieO = c->d_ieO;
     D.ieI = c->d_ieI;
+    D.mO = c->d_mO;
+    D.mI = c->d_mI;
     D.mlb = c->d_mlb;
     D.cpp = c->d_cpp;
     D.pup = c->d_pup;
@@ -524,15 +660,34 @@ int fill_impl(ccj_pf_ctx *c) {
     PFCHK(c, hipMemsetAsync(c->d_Pabs, 0, plane * sizeof(unsigned long long), c->st));
     PFCHK(c, hipEventRecord(c->e0, c->st));
     // level t needs the 2-D spans <= t-1; span s needs P(s), i.e. the levels <= s-3
+    // timed launches: an event pair from the context's pool around each (ccj_pf_set_timing)
+    c->tfam.clear();
+    auto launch = [&](int fam, auto &&go) -> hipError_t {
+        const size_t q = c->tfam.size();
+        if (c->timing) {
+            while (c->tev.size() < 2 * q + 2) {
+                hipEvent_t e;
+                const hipError_t r = hipEventCreate(&e);
+                if (r != hipSuccess) return r;
+                c->tev.push_back(e);
+            }
+            c->tfam.push_back(fam);
+            const hipError_t r = hipEventRecord(c->tev[2 * q], c->st);
+            if (r != hipSuccess) return r;
+        }
+        const hipError_t e = (hipError_t)go();
+        if (e != hipSuccess || !c->timing) return e;
+        return hipEventRecord(c->tev[2 * q + 1], c->st);
+    };
     auto level = [&](int t) -> hipError_t {
         const long long f = c->ifirst[t];
-        hipError_t e = (hipError_t)ccjk_pf_iloop(&c->D, t, f, (int)(c->ifirst[t + 1] - f), c->st);
-        return e != hipSuccess ? e : (hipError_t)ccjk_pf_level(&c->D, c->lv.data(), t, c->st);
+        hipError_t e = launch(0, [&] { return ccjk_pf_iloop(&c->D, t, f, (int)(c->ifirst[t + 1] - f), c->st); });
+        return e != hipSuccess ? e : launch(1, [&] { return ccjk_pf_level(&c->D, c->lv.data(), t, c->st); });
     };
     if (n >= 3) PFCHK(c, level(0));
     for (int s = 0; s <= n - 1; ++s) {
-        PFCHK(c, (hipError_t)ccjk_pf_pterm(&c->D, s, c->st));
-        PFCHK(c, (hipError_t)ccjk_pf_diag(&c->D, s, c->st));
+        PFCHK(c, launch(2, [&] { return ccjk_pf_pterm(&c->D, s, c->st); }));
+        PFCHK(c, launch(3, [&] { return ccjk_pf_diag(&c->D, s, c->st); }));
         if (s + 1 <= n - 3) PFCHK(c, level(s + 1));
     }
     PFCHK(c, hipEventRecord(c->e1, c->st));
@@ -551,6 +706,12 @@ int fill_impl(ccj_pf_ctx *c) {
                 return pf_err(c, CCJ_E_PF_RANGE, msg);
             }
     PFCHK(c, hipEventElapsedTime(&c->fill_ms, c->e0, c->e1));
+    for (double &k : c->kms) k = 0;
+    for (size_t q = 0; q < c->tfam.size(); ++q) {
+        float ms = 0;
+        PFCHK(c, hipEventElapsedTime(&ms, c->tev[2 * q], c->tev[2 * q + 1]));
+        c->kms[c->tfam[q]] += ms;
+    }
 
     // W (part_func.cc:163-172)
     c->W.assign(n + 1, 1.0);  // W.resize(n+1, scale[1])
@@ -1036,6 +1197,28 @@ const char *ccj_pf_last_message(ccj_pf_ctx *c) { return c ? c->msg.c_str() : "";
 int ccj_pf_timing(ccj_pf_ctx *c, float *fill_ms) {
     if (!c || !fill_ms) return CCJ_E_ARG;
     *fill_ms = c->fill_ms;
+    return CCJ_OK;
+}
+
+int ccj_pf_set_timing(ccj_pf_ctx *c, int on) {
+    if (!c) return CCJ_E_ARG;
+    c->timing = on != 0;
+    return CCJ_OK;
+}
+
+int ccj_pf_kernel_ms(ccj_pf_ctx *c, double *ms4) {
+    if (!c || !ms4) return CCJ_E_ARG;
+    for (int k = 0; k < 4; ++k) ms4[k] = c->kms[k];
+    return CCJ_OK;
+}
+
+int ccj_pf_work_model(ccj_pf_ctx *c, double *bytes4) {
+    if (!c || !bytes4) return CCJ_E_ARG;
+    const PfWork w = pf_work_model(*c);
+    bytes4[0] = w.iloop;
+    bytes4[1] = w.level;
+    bytes4[2] = w.pterm;
+    bytes4[3] = w.diag;
     return CCJ_OK;
 }
 

@@ -508,8 +508,29 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
 // (dt = 2+u1+u2).  In each copy the lanes of one term read consecutive words; the weights of one
 // pair's window are contiguous (ieO / ieI) and wave-uniform, so they come through scalar loads.
 // r = stack term, then the window terms in the reference's (u1, u2) order; the copies hold 0 where
-// the inner pair cannot pair (the 4-D value there is 0), so every term is added branch-free.
+// the inner pair cannot pair (the 4-D value there is 0).  A term whose weight is 0.0 or whose inner
+// pair cannot pair adds a zero: per-pair bit masks (mO / mI) skip those loads altogether.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t low_bits(int u) { return u < 0 ? 0u : (2u << u) - 1u; }  // bits 0..u (u <= 30)
+
+// r + term(u) for each set bit u of mk in ascending order (the reference's u2 order), where lane
+// predicate on(u) holds; four terms per round, so that their loads are in flight together
+template <class T, class P>
+__device__ __forceinline__ double window_row(double r, uint32_t mk, T term, P on) {
+    while (mk) {
+        const uint32_t m1 = mk & (mk - 1), m2 = m1 & (m1 - 1), m3 = m2 & (m2 - 1);
+        const int q0 = __builtin_ctz(mk);
+        const int q1 = m1 ? __builtin_ctz(m1) : q0, q2 = m2 ? __builtin_ctz(m2) : q0, q3 = m3 ? __builtin_ctz(m3) : q0;
+        const double x0 = term(q0), x1 = term(q1), x2 = term(q2), x3 = term(q3);
+        if (on(q0)) r += x0;
+        if (m1 && on(q1)) r += x1;
+        if (m2 && on(q2)) r += x2;
+        if (m3 && on(q3)) r += x3;
+        mk = m3 & (m3 - 1);
+    }
+    return r;
+}
+
 __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long first, int nitems) {
     const int wv = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
     if (wv >= nitems) return;
@@ -536,18 +557,20 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             r += x * D.est[a * rs + i];
         }
         // d = i+1+u1 < min(j, i+30); dp = j-1-u2 > max(d+3, j-30): u1 <= min(a,30)-2, u2 <= min(a-u1-6, 28)
-        const double *ew = D.ieO + ((size_t)a * rs + i) * W2;
+        const size_t pr = (size_t)a * rs + i;
+        const double *ew = D.ieO + pr * W2;
+        const uint32_t *mw = D.mO + pr * PF_IEW;
         const int u1m = imin(a, MAXLOOP) - 2;
         for (int u1 = 0; u1 <= u1m; ++u1) {
             const int d = i + 1 + u1, u2m = imin(a - u1 - 6, PF_IEW - 1);
-#pragma unroll 4
-            for (int u2 = 0; u2 <= u2m; ++u2) {
+            const double *e1 = ew + u1 * PF_IEW;
+            r = window_row(r, mw[u1] & low_bits(u2m), [&](int u2) {
                 const int dt = 2 + u1 + u2, ms = m + dt;
                 const PfLvl Ls = D.ld[t - dt];
                 const int x = *(gint *)(cx + Ls.lbx + (long long)(a - dt) * Ls.M + (d - 1) * ms - (((d - 1) * (d - 2)) >> 1) +
                                         hc + 1 + u2);
-                r += ew[u1 * PF_IEW + u2] * x * 1.0;
-            }
+                return e1[u2] * x * 1.0;
+            }, [](int) { return true; });
         }
     } else if (role == 1) {  // PR: q = i+h-1 fixed, lanes i <= q+1
         const int a = f1, q = f2, b = t - a, k = q + a + 3, i = ch * 64 + lane + 1;
@@ -559,17 +582,19 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             const int x = *(gint *)(cx + L2.lbx + L2.C + (long long)a * L2.M + (((q + 1) * (q + 2)) >> 1) + ic - 1);
             r += x * D.est[b * rs + k];
         }
-        const double *ew = D.ieO + ((size_t)b * rs + k) * W2;
+        const size_t pr = (size_t)b * rs + k;
+        const double *ew = D.ieO + pr * W2;
+        const uint32_t *mw = D.mO + pr * PF_IEW;
         const int u1m = imin(b, MAXLOOP) - 2;
         for (int u1 = 0; u1 <= u1m; ++u1) {
             const int u2m = imin(b - u1 - 6, PF_IEW - 1), qq = q + 1 + u1;
             const int rowo = ((qq * (qq + 1)) >> 1) + ic - 1;
-#pragma unroll 4
-            for (int u2 = 0; u2 <= u2m; ++u2) {
+            const double *e1 = ew + u1 * PF_IEW;
+            r = window_row(r, mw[u1] & low_bits(u2m), [&](int u2) {
                 const PfLvl Ls = D.ld[t - 2 - u1 - u2];
                 const int x = *(gint *)(cx + Ls.lbx + Ls.C + (long long)a * Ls.M + rowo);
-                r += ew[u1 * PF_IEW + u2] * x * 1.0;
-            }
+                return e1[u2] * x * 1.0;
+            }, [](int) { return true; });
         }
     } else {  // PM: pair (j, k = j+h+2), lanes a in [alo, ahi]
         const int h = f1, j = f2, k = j + h + 2;
@@ -584,7 +609,9 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             r += x * D.est[(h + 4) * rs + (j - 1)];
         }
         // d = j-1-u1 > max(i, j-30), dp = k+1+u2 < min(l, k+30): u1 <= min(a-2, 28), u2 <= min(b-2, 28)
-        const double *ew = D.ieI + ((size_t)(h + 2) * rs + j) * W2;
+        const size_t pr = (size_t)(h + 2) * rs + j;
+        const double *ew = D.ieI + pr * W2;
+        const uint32_t *mw = D.mI + pr * PF_IEW;
         const int u1m = imin(ahi - 2, PF_IEW - 1), u2m = imin(t - alo - 2, PF_IEW - 1);
         const int u2l = b - 2;  // this lane's u2 bound
         for (int u1 = 0; u1 <= u1m; ++u1) {
@@ -592,14 +619,13 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             const bool on1 = u1 <= ac - 2;
             const int ap = imax(ac - 1 - u1, 0);
             const int u2e = imin(u2m, t - 4 - u1);  // a lane with u1 <= a-2 has b-2 <= t-4-u1
-#pragma unroll 4
-            for (int u2 = 0; u2 <= u2e; ++u2) {
+            const double *e1 = ew + u1 * PF_IEW;
+            r = window_row(r, u2e >= 0 ? mw[u1] & low_bits(u2e) : 0u, [&](int u2) {
                 const int dt = 2 + u1 + u2, tp = t - dt;
                 const PfLvl Ls = D.ld[tp];
                 const int x = *(gint *)(pmx + Ls.pmb + ((long long)(h + dt) * n + d - 1) * (tp + 1) + imin(ap, tp));
-                const double v = ew[u1 * PF_IEW + u2] * x * 1.0;
-                if (on1 && u2 <= u2l) r += v;
-            }
+                return e1[u2] * x * 1.0;
+            }, [&](int u2) { return on1 && u2 <= u2l; });
         }
     }
     if (act) D.R[dst] = r;

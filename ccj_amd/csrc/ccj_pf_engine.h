@@ -48,6 +48,7 @@ struct PfDev {
     const double *hp;     // [w][p] HairpinE
     const double *est;    // [w][p] get_e_stP
     const double *ieO, *ieI;  // get_e_intP by outer / inner pair (above)
+    const uint32_t *mO, *mI;  // [pair][u1]: bit u2 set when that weight is nonzero and the loop's other pair can pair
     const double *mlb, *cpp, *pup;  // expMLbase[], expcp_pen[], expPUP_pen[] (n+2)
     double *V, *VM, *WM, *WMv, *WMp, *WBP, *WPP, *P;  // [w][p]
     long long *Pacc;      // [w][p] exact integer P sums

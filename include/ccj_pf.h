@@ -116,6 +116,15 @@ const char *ccj_pf_last_message(ccj_pf_ctx *ctx);
 
 /* Fill timing of the last ccj_pf_fill (ms, HIP events). */
 int ccj_pf_timing(ccj_pf_ctx *ctx, float *fill_ms);
+/* on != 0: the following fills record an event pair around every kernel launch (measurement only;
+ * it adds the event cost to fill_ms).  ccj_pf_kernel_ms then gives the summed launch durations of
+ * the last fill per family: [0] k_pf_iloop, [1] k_pf_level, [2] k_pf_pterm, [3] k_pf_diag (0 when
+ * timing was off). */
+int ccj_pf_set_timing(ccj_pf_ctx *ctx, int on);
+int ccj_pf_kernel_ms(ccj_pf_ctx *ctx, double *ms4);
+/* Algorithmic HBM bytes of one fill per kernel family (same order): the operands the
+ * recurrences read and write, counted over this sequence's work items.  Host-side, no GPU work. */
+int ccj_pf_work_model(ccj_pf_ctx *ctx, double *bytes4);
 
 #ifdef __cplusplus
 }
