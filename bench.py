@@ -39,6 +39,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "sec/sequence + DP-cells/s at n=200 (Turner04), 1/2/4/8 GPU vs CPU ref"
+PF_METRIC = "partition-function DP-cells/s (W_final_pf::ccj_pf, SURVEY 8 f4)"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
 REF_N200_S = 1341.5    # BASELINE.md / SURVEY.md §6: reference fold of the headline sequence, 1 Xeon core
 
@@ -183,6 +184,93 @@ def cpu_baseline(n_sample=110, seed=3, params="Turner04", cores=None):
                       f"(seed {seed}, {params})"}
 
 
+def pf_cpu_baseline(n_sample=80, seed=3, cores=None):
+    """The reference's partition function (oracle/_ref/pf_driver: part_func.cc built from the reference
+    sources with -ffp-contract=off, Turner 2004 defaults, dangles 2) on k concurrent processes, one
+    n_sample-nt fold each (the reference is single-threaded); value = aggregate 4-D cells/s over the
+    slowest process's wall time.  None when the driver is not built."""
+    k = cores or host_cores()
+    drv = os.path.join(ROOT, "oracle", "_ref", "pf_driver")
+    if not os.path.exists(drv):
+        return None
+    cells = num_cells(n_sample)
+    t0 = time.perf_counter()
+    procs = [subprocess.Popen([drv, rseq(seed + r, n_sample), "-d", "2"], stdout=subprocess.DEVNULL,
+                              stderr=subprocess.DEVNULL) for r in range(k)]
+    rcs = [p.wait(timeout=900) for p in procs]
+    wall = time.perf_counter() - t0
+    if any(rcs):
+        return None
+    return {"value": k * cells / wall, "unit": "DP-cells/s", "cores": k, "kind": "reference", "seconds": wall,
+            "n": n_sample,
+            "sample": f"{k} concurrent reference partition-function folds (W_final_pf::ccj_pf incl. its "
+                      f"constructor) of {n_sample}-nt random RNAs (seeds {seed}..{seed + k - 1}, Turner 2004, "
+                      f"dangles 2), one per host core; O(n^5), so its cells/s falls with n"}
+
+
+def pf_bench(a, rank, world, dist, barrier):
+    """--pf: one step = ccj_pf() (the whole fill + W + energy) of the rank's sequence on a context
+    created before the timed region.  Replicas only: the PF path has no sharded form, so --gpus N
+    runs N independent folds (seed + rank), weak scaling."""
+    from ccj_amd import W_final_pf
+    seq = rseq(a.seed + rank, a.n)
+    t_c = time.perf_counter()
+    pf = W_final_pf(seq, dangle=2, params=a.params)
+    create_ms = (time.perf_counter() - t_c) * 1e3
+    for _ in range(a.warmup):
+        pf.ccj_pf()
+    barrier()
+    fill_ms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        e = pf.ccj_pf()
+        fill_ms += pf.fill_ms()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    elapsed = max_over_ranks(elapsed, dist)
+    # after the timed region: one fill with an event pair around every launch (per-family durations)
+    pf.set_timing(True)
+    pf.ccj_pf()
+    kms = pf.kernel_ms()
+    pf.set_timing(False)
+    work = pf.work_model()
+    pf.close()
+    if rank != 0:
+        return
+    cells = num_cells(a.n)
+    nl = {"k_pf_iloop": max(a.n - 2, 1), "k_pf_level": max(a.n - 2, 1), "k_pf_pterm": max(a.n - 3, 1),
+          "k_pf_diag": a.n}
+
+    def roof(k):
+        ms = kms[k]
+        gbs = work[k] / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+        return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                "traffic": None, "kernel": k, "launches_per_fold": nl[k], "avg_launch_us": ms * 1e3 / nl[k],
+                "algorithmic_bytes_per_fold": work[k], "kernel_ms_per_fold": ms}
+    dom = max(kms, key=kms.get)
+    out = {
+        "metric": PF_METRIC, "value": cells * world * a.steps / elapsed, "unit": "DP-cells/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64+int32", "data": "synthetic",
+        "config": {"workload": f"CCJ partition function (W_final_pf::ccj_pf: fill of the 21 int32 4-D and 8 double "
+                               f"2-D matrices, W, energy; bit-identical to part_func.cc) of a {a.n}-nt random "
+                               f"ACGU RNA per GPU (seed {a.seed}+rank), rna_{a.params}, dangles 2; replicas",
+                   "n": a.n, "seed": a.seed, "params": a.params, "cells_per_fold": cells,
+                   "parallelism": f"replicas{world}"},
+        "sec_per_sequence": elapsed / a.steps, "nt_per_s": a.n * world * a.steps / elapsed,
+        "fill_ms": fill_ms / a.steps, "create_ms": create_ms, "energy": e,
+        "kernel_ms_instrumented_fold": kms,
+        "roofline": roof(dom),
+        "roofline_by_kernel": {k: roof(k) for k in kms},
+    }
+    if world == 1 and not a.no_cpu_baseline:
+        cb = pf_cpu_baseline(a.pf_cpu_sample_n, cores=a.cpu_cores)
+        if cb:
+            out["cpu_baseline"] = cb
+            out["speedup_vs_cpu_baseline_cells_per_s"] = out["value"] / cb["value"]
+    print(json.dumps(out), flush=True)
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None)
@@ -204,6 +292,10 @@ def parse_args(argv=None):
                     help="folds in flight per GPU (contexts): 2 overlaps one fold's traceback and the next "
                          "sequence's setup with the next fill (default 1, measured faster; 2 only when two "
                          "contexts fit in HBM, never band-sharded)")
+    ap.add_argument("--pf", action="store_true",
+                    help="the partition-function path (W_final_pf::ccj_pf, SURVEY §8 f4) instead of the MFE "
+                         "fold: one step = one PF fill + W of the rank's sequence (replicas, no collective)")
+    ap.add_argument("--pf-cpu-sample-n", type=int, default=80)
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the rank launch, barrier and max-over-ranks accounting only (tests)")
     return ap.parse_args(argv)
@@ -255,6 +347,12 @@ def main(argv=None):
                               "unit": "DP-cells/s", "n_gpus": world, "ranks_reported": ranks, "steps": a.steps,
                               "warmup": a.warmup, "dry_run": True, "shard": shard, "comm_id_agreed": comm_ok,
                               "seeds": [rank_seed(a.seed, r, world, 0, a.distinct) for r in range(world)]}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    if a.pf:
+        pf_bench(a, rank, world, dist, barrier)
         if dist is not None:
             dist.destroy_process_group()
         return
