@@ -184,7 +184,11 @@ struct ccj_pf_ctx {
     std::vector<long long> ifirst;          // k_pf_iloop items of level t: [ifirst[t], ifirst[t+1])
     std::vector<uint32_t> h_items, h_mO, h_mI;  // host copies (ccj_pf_work_model)
     PfLvl *d_ld = nullptr;
-    hipStream_t st = nullptr;
+    hipStream_t st = nullptr;     // levels (k_pf_level), the memsets, the result copies
+    hipStream_t st_il = nullptr;  // k_pf_iloop(t): after level t-2
+    hipStream_t st_d = nullptr;   // k_pf_pterm(s), k_pf_diag(s): after level s-3
+    std::vector<hipEvent_t> ev_lev, ev_il, ev_dg;  // level t done, iloop t done, span s done
+    hipEvent_t ev_start = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     PfDev D{};
     // results
@@ -298,6 +302,14 @@ void free_dev(ccj_pf_ctx *c) {
     if (c->e1) hipEventDestroy(c->e1);
     for (hipEvent_t e : c->tev) hipEventDestroy(e);
     c->tev.clear();
+    for (auto *v : {&c->ev_lev, &c->ev_il, &c->ev_dg}) {
+        for (hipEvent_t e : *v)
+            if (e) hipEventDestroy(e);
+        v->clear();
+    }
+    if (c->ev_start) hipEventDestroy(c->ev_start);
+    if (c->st_il) hipStreamDestroy(c->st_il);
+    if (c->st_d) hipStreamDestroy(c->st_d);
     if (c->st) hipStreamDestroy(c->st);
 }
 
@@ -566,6 +578,13 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     // device
     PFCHK(c, hipSetDevice(device));
     PFCHK(c, hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    PFCHK(c, hipStreamCreateWithFlags(&c->st_il, hipStreamNonBlocking));
+    PFCHK(c, hipStreamCreateWithFlags(&c->st_d, hipStreamNonBlocking));
+    PFCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
+    for (auto *v : {&c->ev_lev, &c->ev_il, &c->ev_dg}) {
+        v->assign(n + 1, nullptr);
+        for (hipEvent_t &e : *v) PFCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     PFCHK(c, hipEventCreate(&c->e0));
     PFCHK(c, hipEventCreate(&c->e1));
     auto up = [&](void **d, const void *h, size_t bytes) -> hipError_t {
@@ -607,7 +626,8 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     PFCHK(c, hipMalloc((void **)&c->d_pmx, (size_t)std::max(offm, 1LL) * sizeof(int)));
     PFCHK(c, hipMemset(c->d_cx, 0, (size_t)std::max(offx, 1LL) * sizeof(int)));
     PFCHK(c, hipMemset(c->d_pmx, 0, (size_t)std::max(offm, 1LL) * sizeof(int)));
-    PFCHK(c, hipMalloc((void **)&c->d_R, (size_t)3 * maxC * sizeof(double)));
+    PFCHK(c, hipMalloc((void **)&c->d_R, (size_t)2 * 3 * maxC * sizeof(double)));
+    c->D.Rst = 3 * maxC;
 
     PfDev &D = c->D;
     D.n = n;
@@ -662,7 +682,7 @@ int fill_impl(ccj_pf_ctx *c) {
     // level t needs the 2-D spans <= t-1; span s needs P(s), i.e. the levels <= s-3
     // timed launches: an event pair from the context's pool around each (ccj_pf_set_timing)
     c->tfam.clear();
-    auto launch = [&](int fam, auto &&go) -> hipError_t {
+    auto launch = [&](int fam, hipStream_t s, auto &&go) -> hipError_t {
         const size_t q = c->tfam.size();
         if (c->timing) {
             while (c->tev.size() < 2 * q + 2) {
@@ -672,24 +692,49 @@ int fill_impl(ccj_pf_ctx *c) {
                 c->tev.push_back(e);
             }
             c->tfam.push_back(fam);
-            const hipError_t r = hipEventRecord(c->tev[2 * q], c->st);
+            const hipError_t r = hipEventRecord(c->tev[2 * q], s);
             if (r != hipSuccess) return r;
         }
         const hipError_t e = (hipError_t)go();
         if (e != hipSuccess || !c->timing) return e;
-        return hipEventRecord(c->tev[2 * q + 1], c->st);
+        return hipEventRecord(c->tev[2 * q + 1], s);
     };
-    auto level = [&](int t) -> hipError_t {
+    // Three streams: level t needs k_pf_iloop(t) and the spans <= t-1; k_pf_iloop(t)
+    // reads the copies of levels <= t-2 and refills the R buffer level t-2 read; P(s) needs the
+    // levels <= s-3 and span s the spans < s.  So iloop(t) and the span s = t+1 (with its P terms)
+    // run beside level t-1, off the level chain.  Every event is recorded before a wait on it is
+    // enqueued (host order below).
+    const int nl = n - 2;  // levels 0 .. n-3
+    auto span = [&](int s) -> hipError_t {
+        hipError_t e = launch(2, c->st_d, [&] { return ccjk_pf_pterm(&c->D, s, c->st_d); });
+        if (e == hipSuccess) e = launch(3, c->st_d, [&] { return ccjk_pf_diag(&c->D, s, c->st_d); });
+        return e != hipSuccess ? e : hipEventRecord(c->ev_dg[s], c->st_d);
+    };
+    auto iloop = [&](int t) -> hipError_t {
         const long long f = c->ifirst[t];
-        hipError_t e = launch(0, [&] { return ccjk_pf_iloop(&c->D, t, f, (int)(c->ifirst[t + 1] - f), c->st); });
-        return e != hipSuccess ? e : launch(1, [&] { return ccjk_pf_level(&c->D, c->lv.data(), t, c->st); });
+        const hipError_t e = launch(0, c->st_il, [&] { return ccjk_pf_iloop(&c->D, t, f, (int)(c->ifirst[t + 1] - f), c->st_il); });
+        return e != hipSuccess ? e : hipEventRecord(c->ev_il[t], c->st_il);
     };
-    if (n >= 3) PFCHK(c, level(0));
-    for (int s = 0; s <= n - 1; ++s) {
-        PFCHK(c, launch(2, [&] { return ccjk_pf_pterm(&c->D, s, c->st); }));
-        PFCHK(c, launch(3, [&] { return ccjk_pf_diag(&c->D, s, c->st); }));
-        if (s + 1 <= n - 3) PFCHK(c, level(s + 1));
+    PFCHK(c, hipEventRecord(c->ev_start, c->st));
+    PFCHK(c, hipStreamWaitEvent(c->st_d, c->ev_start, 0));
+    PFCHK(c, hipStreamWaitEvent(c->st_il, c->ev_start, 0));
+    for (int s = 0; s <= std::min(2, n - 1); ++s) PFCHK(c, span(s));   // no P terms below span 3
+    for (int t = 0; t <= std::min(1, nl - 1); ++t) PFCHK(c, iloop(t));
+    for (int t = 0; t < nl; ++t) {
+        PFCHK(c, hipStreamWaitEvent(c->st, c->ev_il[t], 0));
+        if (t >= 1) PFCHK(c, hipStreamWaitEvent(c->st, c->ev_dg[t - 1], 0));
+        PFCHK(c, launch(1, c->st, [&] { return ccjk_pf_level(&c->D, c->lv.data(), t, c->st); }));
+        PFCHK(c, hipEventRecord(c->ev_lev[t], c->st));
+        if (t + 2 < nl) {
+            PFCHK(c, hipStreamWaitEvent(c->st_il, c->ev_lev[t], 0));
+            PFCHK(c, iloop(t + 2));
+        }
+        if (t + 3 <= n - 1) {
+            PFCHK(c, hipStreamWaitEvent(c->st_d, c->ev_lev[t], 0));
+            PFCHK(c, span(t + 3));
+        }
     }
+    PFCHK(c, hipStreamWaitEvent(c->st, c->ev_dg[n - 1], 0));
     PFCHK(c, hipEventRecord(c->e1, c->st));
     c->h2d.assign((size_t)CCJ_PF_NMAT2 * plane, 0.0);
     PFCHK(c, hipMemcpyAsync(c->h2d.data(), c->d_2d, c->h2d.size() * sizeof(double), hipMemcpyDeviceToHost, c->st));

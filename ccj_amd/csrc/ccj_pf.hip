@@ -258,6 +258,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     const int i = off - (h * m - ((h * (h - 1)) >> 1)) + 1, j = i + a, k = j + h + 2, l = k + b;
     int *cell = D.d4 + L.lb + (long long)a * L.M + off;
     const long long C = L.C, off0 = (long long)a * L.M + off;  // off0: the cell in R's planes
+    const double *Rt = D.R + (t & 1) * D.Rst;                   // k_pf_iloop(t)'s buffer
     auto put = [&](int x, double v) -> int {
         const int r = x86_trunc(v);
         cell[x * C] = r;
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         if (G.pt(i, j) > 0) {
             const bool in = a >= 2;
             double r = 0;
-            if (a >= 6) r = D.R[off0];  // k_pf_iloop: the stack term, then the window
+            if (a >= 6) r = Rt[off0];  // k_pf_iloop: the stack term, then the window
             else r += (in ? X(PF_PL, 2, 2, 1, 1) : 0) * D.est[a * rs + i];  // no window (u2 <= a-u1-6)
             c += r;
             double q = 0;
@@ -408,7 +409,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         if (G.pt(k, l) > 0) {
             const bool in = b >= 2;
             double r = 0;
-            if (b >= 6) r = D.R[C + off0];
+            if (b >= 6) r = Rt[C + off0];
             else r += (in ? X(PF_PR, 2, 0, 1, 0) : 0) * D.est[b * rs + k];
             c += r;
             double q = 0;
@@ -433,7 +434,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
             // or S[n+1]; the factor multiplies PM(i, j-1, k+1, l), which is then outside the matrix
             // (0), so any finite value gives 0 — use 0 instead of reading past the table
             const double est_m = (j > 1 && k < n) ? D.est[(h + 4) * rs + (j - 1)] : 0.0;
-            if (a >= 2 && b >= 2) r = D.R[2 * C + off0];
+            if (a >= 2 && b >= 2) r = Rt[2 * C + off0];
             else r += (in ? X(PF_PM, 2, 1, 2, 0) : 0) * est_m;
             c += r;
             double q = 0;
@@ -628,7 +629,7 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             }, [&](int u2) { return on1 && u2 <= u2l; });
         }
     }
-    if (act) D.R[dst] = r;
+    if (act) D.R[(t & 1) * D.Rst + dst] = r;
 }
 
 // canonical-order gather of one 4-D matrix for the parity hashes: out[q] for the q-th cell of

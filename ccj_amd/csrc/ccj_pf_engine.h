@@ -61,7 +61,8 @@ struct PfDev {
     //   PMx = pmb + (h*n + j-1)*(t+1) + a
     int *cx, *pmx;
     const uint32_t *items;  // k_pf_iloop work items of all levels (ccj_items.h)
-    double *R;              // k_pf_iloop's interior-loop sums of the level being filled, [role][a*M + off]
+    double *R;              // k_pf_iloop's interior-loop sums, two level buffers (t & 1) of [role][a*M + off]
+    long long Rst;          // doubles per buffer (3 * max C_t)
 };
 
 }  // namespace ccj
