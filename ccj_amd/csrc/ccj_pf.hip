@@ -68,29 +68,53 @@ struct PfG {  // getters with the reference's semantics
 
 // ---------------------------------------------------------------------------------------------
 // P(i, i+s) (compute_P, part_func.cc:383-393): sum over j < d < k of PK(i,j,d+1,k) * PK(j+1,d,k+1,l),
-// the product in int.  Lanes take 64 consecutive i; a workgroup takes one (j-i, d-i) and loops k.
+// the product in int.  The sum is exact in int64 (checked through Pabs), so its order is free:
+// a workgroup of 4 waves takes 64 consecutive i (lanes), one j-i (blockIdx.y) and a run of
+// PT_DD values of d-i (blockIdx.z), wave w every 4th of them; each lane loops k, 4 terms per round
+// in flight, and the 4 waves' partial sums meet in LDS, so each interval gets one atomic pair per
+// workgroup (PT_DD (j, d) pairs) instead of one per (j, d).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_pf_pterm(PfDev D, int s) {
-    const int jo = blockIdx.y, dd = blockIdx.z;  // j = i+jo, d = i+dd
-    if (dd <= jo || dd > s - 2) return;
-    const int i = blockIdx.x * 64 + threadIdx.x + 1;
-    if (i + s > D.n) return;
-    // PK(i, j, d+1, k): level jo + (ko-dd-1), block jo, row dd-jo-1, position i;
-    // PK(j+1, d, k+1, l): level (dd-jo-1) + (s-ko-1), block dd-jo-1, row ko-dd-1, position i+jo+1
-    // (ko = k-i): wave-uniform level descriptors, lanes at consecutive positions
-    const int n = D.n, a1 = jo, h1 = dd - jo - 1, a2 = dd - jo - 1;
+constexpr int PT_DD = 16;
+
+__global__ __launch_bounds__(256) void k_pf_pterm(PfDev D, int s) {
+    const int jo = blockIdx.y, dd0 = jo + 1 + (int)blockIdx.z * PT_DD;  // j = i+jo, d = i+dd
+    if (dd0 > s - 2) return;  // whole workgroup
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int n = D.n;
+    const int i = blockIdx.x * 64 + lane + 1;
+    const int ic = imin(i, n - s);  // idle lanes re-read a valid interval
     typedef const __attribute__((address_space(1))) int gint;
     long long acc = 0;
     unsigned long long aabs = 0;
-    for (int ko = dd + 1; ko < s; ++ko) {
-        const int h2 = ko - dd - 1, t1 = a1 + h2, t2 = a2 + (s - ko - 1);
-        const int m1 = n - t1 - 2, m2 = n - t2 - 2;
-        const PfLvl L1 = D.ld[t1], L2 = D.ld[t2];
-        const long long U1 = L1.lb + PF_PK * L1.C + (long long)a1 * L1.M + (long long)h1 * m1 - (((long long)h1 * (h1 - 1)) >> 1) - 1;
-        const long long U2 = L2.lb + PF_PK * L2.C + (long long)a2 * L2.M + (long long)h2 * m2 - (((long long)h2 * (h2 - 1)) >> 1) + jo;
-        const long long x = imul_wrap(*(gint *)(D.d4 + U1 + i), *(gint *)(D.d4 + U2 + i));
-        acc += x;
-        aabs += (unsigned long long)(x < 0 ? -x : x);
+    const int dd1 = imin(dd0 + PT_DD - 1, s - 2);
+    for (int dd = dd0 + w; dd <= dd1; dd += 4) {
+        // PK(i, j, d+1, k): level jo + (ko-dd-1), block jo, row dd-jo-1, position i;
+        // PK(j+1, d, k+1, l): level (dd-jo-1) + (s-ko-1), block dd-jo-1, row ko-dd-1, position i+jo+1
+        // (ko = k-i): wave-uniform level descriptors, lanes at consecutive positions
+        const int a1 = jo, h1 = dd - jo - 1, a2 = dd - jo - 1;
+#pragma unroll 4
+        for (int ko = dd + 1; ko < s; ++ko) {
+            const int h2 = ko - dd - 1, t1 = a1 + h2, t2 = a2 + (s - ko - 1);
+            const int m1 = n - t1 - 2, m2 = n - t2 - 2;
+            const PfLvl L1 = D.ld[t1], L2 = D.ld[t2];
+            const long long U1 = L1.lb + PF_PK * L1.C + (long long)a1 * L1.M + (long long)h1 * m1 - (((long long)h1 * (h1 - 1)) >> 1) - 1;
+            const long long U2 = L2.lb + PF_PK * L2.C + (long long)a2 * L2.M + (long long)h2 * m2 - (((long long)h2 * (h2 - 1)) >> 1) + jo;
+            const long long x = imul_wrap(*(gint *)(D.d4 + U1 + ic), *(gint *)(D.d4 + U2 + ic));
+            acc += x;
+            aabs += (unsigned long long)(x < 0 ? -x : x);
+        }
+    }
+    __shared__ long long sacc[3][64];
+    __shared__ unsigned long long sabs[3][64];
+    if (w > 0) {
+        sacc[w - 1][lane] = acc;
+        sabs[w - 1][lane] = aabs;
+    }
+    __syncthreads();
+    if (w > 0 || i + s > n) return;
+    for (int q = 0; q < 3; ++q) {
+        acc += sacc[q][lane];
+        aabs += sabs[q][lane];
     }
     if (acc) atomicAdd((unsigned long long *)&D.Pacc[s * D.rs + i], (unsigned long long)acc);
     if (aabs) atomicAdd(&D.Pabs[s * D.rs + i], aabs);
@@ -648,8 +672,8 @@ __global__ __launch_bounds__(256) void k_pf_canon(PfDev D, int x, const long lon
 extern "C" int ccjk_pf_pterm(const PfDev *D, int s, void *stream) {
     const int ni = D->n - s;
     if (s < 3 || ni <= 0) return 0;
-    hipLaunchKernelGGL(k_pf_pterm, dim3((unsigned)((ni + 63) / 64), (unsigned)(s - 2), (unsigned)(s - 1)), dim3(64), 0,
-                       (hipStream_t)stream, *D, s);
+    hipLaunchKernelGGL(k_pf_pterm, dim3((unsigned)((ni + 63) / 64), (unsigned)(s - 2), (unsigned)((s - 2 + PT_DD - 1) / PT_DD)),
+                       dim3(256), 0, (hipStream_t)stream, *D, s);
     return (int)hipGetLastError();
 }
 
