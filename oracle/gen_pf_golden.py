@@ -13,6 +13,8 @@ records, as data, in tests/golden/pf_golden.json:
 Parameter sets: "default" = the reference's compiled-in Turner 2004 tables (no -P), otherwise
 -P /root/reference/params/rna_<name>.par.  The reference never leaves this container; only these
 numbers travel.  Usage: python3 oracle/gen_pf_golden.py [--jobs 8] [--big]
+       python3 oracle/gen_pf_golden.py --large   (tests/golden/pf_golden_large.json: the bench.py --pf
+       sequence, n=200 seed 5 with rna_Turner04.par, and n=150; about an hour of reference time)
 """
 import argparse
 import json
@@ -26,6 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DRV = os.path.join(ROOT, "oracle", "_ref", "pf_driver")
 PARDIR = "/root/reference/params"
 OUT = os.path.join(ROOT, "tests", "golden", "pf_golden.json")
+OUT_LARGE = os.path.join(ROOT, "tests", "golden", "pf_golden_large.json")
 
 
 def rseq(seed, n):
@@ -62,6 +65,12 @@ def cases(big):
         out.append(("big80_default", rseq(8, 80), "default", 2, 3))
         out.append(("big100_DirksPierce09", rseq(9, 100), "DirksPierce09", 2, 5))
     return out
+
+
+def large_cases():
+    # bench.py --pf's default workload (rseq(5, 200), Turner04, dangles 2) and a second size/set
+    return [("pf200_Turner04_seed5", rseq(5, 200), "Turner04", 2, None),
+            ("pf150_DirksPierce09_seed4", rseq(4, 150), "DirksPierce09", 2, 11)]
 
 
 def run(case):
@@ -121,7 +130,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=8)
     ap.add_argument("--big", action="store_true")
+    ap.add_argument("--large", action="store_true")
     a = ap.parse_args()
+    if a.large:
+        with ThreadPoolExecutor(2) as ex:
+            recs = list(ex.map(run, large_cases()))
+        with open(OUT_LARGE, "w") as f:
+            json.dump({"generator": "oracle/gen_pf_golden.py --large",
+                       "driver": "oracle/_ref/pf_driver (part_func.cc, -ffp-contract=off)", "cases": recs}, f, indent=0)
+        print("wrote %d cases to %s" % (len(recs), OUT_LARGE))
+        return 0
     cs = cases(a.big)
     with ThreadPoolExecutor(a.jobs) as ex:
         recs = list(ex.map(run, cs))

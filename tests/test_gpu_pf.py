@@ -103,3 +103,40 @@ def test_pf_after_other_contexts():
                 assert pf.get4("PM", 1, 1, 32, 32) == 1 and pf.get4("PK", 1, 2, 4, 32) == 2580
         finally:
             pf.close()
+
+
+GOLD_LARGE = os.path.join(os.path.dirname(__file__), "golden", "pf_golden_large.json")
+LARGE = json.load(open(GOLD_LARGE))["cases"] if os.path.exists(GOLD_LARGE) else []
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not LARGE, reason="tests/golden/pf_golden_large.json not generated (oracle/gen_pf_golden.py --large)")
+@pytest.mark.parametrize("case", LARGE, ids=[c["name"] for c in LARGE])
+def test_pf_matches_reference_large(case):
+    """bench.py --pf's own workload (n=200, seed 5, Turner04) and n=150 DirksPierce09 against the
+    reference's part_func.cc: every bit of W, all 29 matrices, the samples."""
+    test_pf_matches_reference(case)
+
+
+@pytest.mark.gpu
+def test_pf_kernel_timing_and_work_model():
+    """ccj_pf_set_timing / ccj_pf_kernel_ms / ccj_pf_work_model: every family timed in a timed fill,
+    nothing in an untimed one, and the timed fill's results unchanged."""
+    import ccj_amd
+    c = next(c for c in CASES if c["name"] == "big60_default")
+    pf = ccj_amd.W_final_pf(c["seq"], params=c["params"])
+    try:
+        pf.set_timing(True)
+        e = pf.ccj_pf()
+        km = pf.kernel_ms()
+        assert repr(e) == repr(float(c["energy"]))
+        assert set(km) == set(pf.PF_KERNELS) and all(v > 0 for v in km.values())
+        assert sum(km.values()) < 10 * pf.fill_ms()
+        pf.set_timing(False)
+        pf.ccj_pf()
+        assert all(v == 0 for v in pf.kernel_ms().values())
+        w = pf.work_model()
+        # the level kernel reads at least its 21 stores' worth per cell; every family does work
+        assert w["k_pf_level"] >= 84 * ccj_amd.num_cells(60) and all(v > 0 for v in w.values())
+    finally:
+        pf.close()
