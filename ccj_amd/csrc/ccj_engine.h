@@ -44,28 +44,20 @@ struct LevelDesc {
 
 struct LvlDev {     // per-level descriptor read by the level kernel (one s_load_dwordx8)
     long long lb;  // element offset of level t in the 4-D storage
-    long long lr;  // dword offset of level t in the loop records (rec_level_dwords(C) dwords)
+    long long lr;  // record offset of level t in the AoS loop records (3 record types x C)
     int C;         // cells per matrix in level t = (t+1)*M
     int M;         // cells per a-block = m(m+1)/2, m = n-t-2
-    int rl;        // dword offset of the level's RL section from lr (rec_rl_off(C))
-    int pad;
+    int pad[2];
 };
 
-// Loop records: the operands the fused split-point loops of k_level4d read at one
-// neighbour cell, packed as int16 pairs, so each neighbour costs one dwordx3/dwordx4 load instead of
-// 5-7 int16 loads.  One record per side, each holding exactly the fields that side's terms read
-// (round 3: the a-loop's two sides used to share one 16-byte RA record, 8 fields of which each side
-// reads 5 or 6; per split step the a-loop now loads 24 bytes instead of 32, the b-loop 28 instead
-// of 32).  Four record types per level, each indexed like a matrix (a*M + G(h) + i-1):
-//   RI (a-loop, i side, 12 B): PLmloop00 PMmloop00 | POmloop00 PfromL    | PfromO -
-//   RJ (a-loop, j side, 12 B): PLmloop00 PMmloop00 | PfromL PLmloop10    | PfromMprime PK
-//   RK (b-loop, k side, 12 B): PRmloop00 PMmloop00 | PfromR min(PL,PR)   | PK -
-//   RL (b-loop, l side, 16 B): PRmloop00 PMmloop00 | POmloop00 PMmloop10 | POmloop10 PfromR | PfromO -
-// Level layout in dwords: RI [0, 3C), RJ [3C, 6C), RK [6C, 9C), RL [rl, rl + 4C) with rl = 9C
-// rounded up to 16 bytes.  Values are the stored (clamped) int16 matrix values; unused slots hold
-// 32767.
-__host__ __device__ __forceinline__ long long rec_rl_off(long long C) { return (9 * C + 3) & ~3LL; }
-__host__ __device__ __forceinline__ long long rec_level_dwords(long long C) { return rec_rl_off(C) + 4 * C; }
+// AoS loop records: the operands the fused split-point loops of k_level4d read at
+// one neighbour cell, 8 int16 per 16-byte record, so each neighbour costs one dwordx4 load instead
+// of 5-7 int16 loads.  Three record types per level, each indexed like a matrix (a*M + G(h) + i-1):
+//   RA (a-loop, both sides): PLmloop00 PMmloop00 | POmloop00 PfromL | PfromO PLmloop10 | PfromMprime PK
+//   RK (b-loop, k side):     PRmloop00 PMmloop00 | PfromR min(PL,PR) | PK -          | -  -
+//   RL (b-loop, l side):     PRmloop00 PMmloop00 | POmloop00 PMmloop10 | POmloop10 PfromR | PfromO -
+// Values are the stored (clamped) int16 matrix values; unused slots hold 32767.
+enum RecType { RA = 0, RK = 1, RL = 2, NREC = 3 };
 
 // Split-point sharing (k_level4d).  The cells of one gap column — same (j,k,l)
 // for the i-side split, (i,k,l) j-side, (i,j,l) k-side, (i,j,k) l-side — sit on consecutive levels
@@ -151,8 +143,8 @@ struct DevTables {
     int16_t *d4;                   // 4-D storage base
     const long long *lb;           // element offset of level t in d4
     const LvlDev *ld;             // per-level descriptors
-    uint32_t *rec;                 // loop records (dwords), level t at ld[t].lr
-    long long nrec;                // record dwords allocated (debug bounds checks)
+    uint4 *rec;                    // AoS loop records, level t at ld[t].lr
+    long long nrec;                // records allocated (debug bounds checks)
     // interior-loop copies of PL / PR / PM, laid out so that the lanes of one k_iloop wave share
     // the loop's closing pair:
     //   PLx(t,a,h,i) = lbx + a*M + G(i-1) + h               (h fastest: fixed (i,j), lanes k)

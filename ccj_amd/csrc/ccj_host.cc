@@ -131,7 +131,7 @@ struct ccj_ctx {
     LvlDev *d_ld = nullptr;
     int16_t *d4x = nullptr, *pmx = nullptr;  // interior-loop copies of PL/PR and PM (IT_PAD into the allocations)
     int16_t *d4x_alloc = nullptr, *pmx_alloc = nullptr;
-    uint32_t *d_rec = nullptr;               // loop records (ccj_engine.h)
+    uint4 *d_rec = nullptr;                  // AoS loop records
     uint4 *d_acc = nullptr;                  // partial-record ring (split-point sharing)
     int16_t *d_lord = nullptr;               // long-scan a-blocks per sharing level, longest first
     int *d_lord_off = nullptr;
@@ -1700,11 +1700,10 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     const size_t ie_elems = (size_t)IE_U * IE_U * (n + 1) * c->rs;
     if (c->total4 > 0 && hipMalloc(&c->d4, (size_t)c->total4 * sizeof(int16_t)) != hipSuccess)
         return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for 4-D matrices failed", c->total4 * 2e-9);
-    // loop records: RI, RJ, RK (12 B) and RL (16 B) per cell (ccj_engine.h)
-    c->nrec = 0;
-    for (int t = 0; t < (int)c->lv_host.size(); ++t) c->nrec += rec_level_dwords(c->lv_host[t].C);
-    if (c->nrec > 0 && hipMalloc(&c->d_rec, (size_t)c->nrec * sizeof(uint32_t)) != hipSuccess)
-        return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for loop records failed", c->nrec * 4e-9);
+    // AoS loop records: NREC 16-byte records per cell (ccj_engine.h)
+    c->nrec = c->total4 / NMAT4 * NREC;
+    if (c->nrec > 0 && hipMalloc(&c->d_rec, (size_t)c->nrec * sizeof(uint4)) != hipSuccess)
+        return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for loop records failed", c->nrec * 16e-9);
     // split-point sharing: the level range it covers (every level of it runs unsplit, so each leader
     // and its followers run one cell per lane) and the partial-record ring
     int g_lo = 0, g_hi = 0;
@@ -1845,9 +1844,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         std::vector<LvlDev> ld(c->lv_off.size());
         long long lr = 0;
         for (size_t t = 0; t < ld.size(); ++t) {
-            const long long C = c->lv_host[t].C;
-            ld[t] = LvlDev{c->lv_off[t], lr, c->lv_host[t].C, c->lv_host[t].M, (int)rec_rl_off(C), 0};
-            lr += rec_level_dwords(C);
+            ld[t] = LvlDev{c->lv_off[t], lr, c->lv_host[t].C, c->lv_host[t].M, {0, 0}};
+            lr += (long long)NREC * c->lv_host[t].C;
         }
         HIPCHK(cp, hipMemcpy(c->d_ld, ld.data(), ld.size() * sizeof(LvlDev), hipMemcpyHostToDevice));
     }

@@ -1004,20 +1004,15 @@ __device__ __forceinline__ uint4 pack_acc(const int *f, int nf) {
     return make_uint4(pk16(c[0], c[1]), pk16(c[2], c[3]), pk16(c[4], c[5]), pk16(c[6], c[7]));
 }
 
-// the four records of one cell (values as stored, i.e. already clamped; ccj_engine.h)
-__device__ __forceinline__ void write_records(const DevTables &T, const LvlDev &L, unsigned cell, int Lm00, int Mm00,
+// the three records of one cell (values as stored, i.e. already clamped)
+__device__ __forceinline__ void write_records(const DevTables &T, long long lr, int C, unsigned cell, int Lm00, int Mm00,
                                               int Om00, int fL, int fO, int Lm10, int fMp, int K, int Rm00, int fR,
                                               int PLR, int Mm10, int Om10) {
-    uint32_t *rp = T.rec + L.lr;
-    const unsigned C3 = 3u * (unsigned)L.C, c3 = 3u * cell;
-    *(uint3 *)(rp + c3) = make_uint3(pk16(Lm00, Mm00), pk16(Om00, fL), pk16(fO, INTERN_INF));
-    *(uint3 *)(rp + C3 + c3) = make_uint3(pk16(Lm00, Mm00), pk16(fL, Lm10), pk16(fMp, K));
-    *(uint3 *)(rp + 2u * C3 + c3) = make_uint3(pk16(Rm00, Mm00), pk16(fR, PLR), pk16(K, INTERN_INF));
-    *(uint4 *)(rp + (unsigned)L.rl + 4u * cell) = make_uint4(pk16(Rm00, Mm00), pk16(Om00, Mm10), pk16(Om10, fR), pk16(fO, INTERN_INF));
+    uint4 *rp = T.rec + lr;
+    rp[cell] = make_uint4(pk16(Lm00, Mm00), pk16(Om00, fL), pk16(fO, Lm10), pk16(fMp, K));
+    rp[(unsigned)C + cell] = make_uint4(pk16(Rm00, Mm00), pk16(fR, PLR), pk16(K, INTERN_INF), pk16(INTERN_INF, INTERN_INF));
+    rp[2u * (unsigned)C + cell] = make_uint4(pk16(Rm00, Mm00), pk16(Om00, Mm10), pk16(Om10, fR), pk16(fO, INTERN_INF));
 }
-// record loads: one neighbour's RI / RJ / RK (12 B, dwordx3) or RL (16 B, dwordx4) at cell index x
-__device__ __forceinline__ uint3 ld_rec3(const uint32_t *rp, unsigned sec, unsigned x) { return *(const uint3 *)(rp + sec + 3u * x); }
-__device__ __forceinline__ uint4 ld_rec4(const uint32_t *rp, unsigned sec, unsigned x) { return *(const uint4 *)(rp + sec + 4u * x); }
 
 
 // Software-pipelined split scan: visits s = s0, s0+step, ... <= last, issuing the loads of step
@@ -1145,7 +1140,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     if ((dt) < 1 || (dt) > t || (ap_) < 0 || (ap_) > t - (dt) || h + (dh) >= m + (dt) || i + (di) < 1 || \
         i + (di) > m + (dt) - h - (dh)) atomicOr(T.err, 4)
 #define CHKR(idx) \
-    if ((long long)(idx) < 0 || (long long)(idx) + 3 >= T.nrec) atomicOr(T.err, 8)
+    if ((long long)(idx) < 0 || (long long)(idx) >= T.nrec) atomicOr(T.err, 8)
 #define CHKA(idx) \
     if (!T.acc || (long long)(idx) >= T.accC) atomicOr(T.err, 256)
 #else
@@ -1191,7 +1186,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     int pLm00 = seed, pLm01 = INF, pLm10 = INF, pMm00 = seed, pMm10 = INF;
     int pOm00 = seed, pOm10 = INF;
     int fL1 = INF, fL2 = INF, fM = INF, fO1 = INF, pK1 = INF;
-    struct AV { int2 w2i, w2j; uint3 wi, wj; int s; };  // raw loads of one split step
+    struct AV { int2 w2i, w2j; uint4 wi, wj; int s; };  // raw loads of one split step
     auto load_a = [&](int s) {
         AV v;
         v.s = s;
@@ -1209,21 +1204,20 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         const int Ui = (a - s) * L.M + s;                          // X(d,j,k,l), d = i+s: lane L0 + h*s
         const int Uj = (a - s) * L.M + s * m + ((s * (s + 1)) >> 1);  // X(i,d,k,l), d = j-s: lane L0
         const unsigned lh = L0 + uh * (unsigned)s;
-        // RI at X(d,j,k,l): x = Lm00|Mm00, y = Om00|fL, z = fO|-
-        // RJ at X(i,d,k,l): x = Lm00|Mm00, y = fL|Lm10, z = fMp|K   (ccj_engine.h)
-        const uint32_t *rp = T.rec + L.lr;
-        CHKR(L.lr + 3 * ((unsigned)Ui + lh));
-        CHKR(L.lr + 3 * L.C + 3 * ((unsigned)Uj + L0));
-        v.wi = ld_rec3(rp, 0u, (unsigned)Ui + lh);
-        v.wj = ld_rec3(rp, 3u * (unsigned)L.C, (unsigned)Uj + L0);
+        // one RA record per side (ccj_engine.h): x = Lm00|Mm00, y = Om00|fL, z = fO|Lm10, w = fMp|K
+        const uint4 *rp = T.rec + L.lr;
+        CHKR(L.lr + (unsigned)Ui + lh);
+        CHKR(L.lr + (unsigned)Uj + L0);
+        v.wi = rp[(unsigned)Ui + lh];
+        v.wj = rp[(unsigned)Uj + L0];
         return v;
     };
     auto step_a = [&](const AV &v, int mask) {
         const int wbp_i = v.w2i.x, wp_i = v.w2i.y, wbp_j = v.w2j.x, wp_j = v.w2j.y;
         const int wb_i = WBD(wbp_i, v.s), wb_j = WBD(wbp_j, v.s);
         const int Lm00i = lo16(v.wi.x), Mm00i = hi16(v.wi.x), Om00i = lo16(v.wi.y), fLi = hi16(v.wi.y), fOi = lo16(v.wi.z);
-        const int Lm00j = lo16(v.wj.x), Mm00j = hi16(v.wj.x), fLj = lo16(v.wj.y), Lm10j = hi16(v.wj.y);
-        const int fMpj = lo16(v.wj.z), Kj = hi16(v.wj.z);
+        const int Lm00j = lo16(v.wj.x), Mm00j = hi16(v.wj.x), fLj = hi16(v.wj.y), Lm10j = hi16(v.wj.z);
+        const int fMpj = lo16(v.wj.w), Kj = hi16(v.wj.w);
         pLm00 = imin(pLm00, imin(wb_i + Lm00i, Lm00j + wb_j));  // :449-458
         pLm01 = imin(pLm01, Lm00j + wbp_j);                     // :468-471
         pLm10 = imin(pLm10, wbp_i + Lm00i);                     // :481-483
@@ -1248,7 +1242,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         for (int r = 0; r < SHARE_R; ++r)
 #pragma unroll
             for (int f = 0; f < 7; ++f) AI_[r][f] = AJ_[r][f] = INF;
-        struct LA { uint3 wi, wj; int2 q[SHARE_R], p[SHARE_R]; int s; };  // raw loads of one split step
+        struct LA { uint4 wi, wj; int2 q[SHARE_R], p[SHARE_R]; int s; };  // raw loads of one split step
         auto ld = [&](int s) {
             LA v;
             v.s = s;
@@ -1256,11 +1250,11 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             const int Ui = (a - s) * L.M + s;
             const int Uj = (a - s) * L.M + s * m + ((s * (s + 1)) >> 1);
             const unsigned lh = L0 + uh * (unsigned)s;
-            const uint32_t *rp = T.rec + L.lr;
-            CHKR(L.lr + 3 * ((unsigned)Ui + lh));
-            CHKR(L.lr + 3 * L.C + 3 * ((unsigned)Uj + L0));
-            v.wi = ld_rec3(rp, 0u, (unsigned)Ui + lh);
-            v.wj = ld_rec3(rp, 3u * (unsigned)L.C, (unsigned)Uj + L0);
+            const uint4 *rp = T.rec + L.lr;
+            CHKR(L.lr + (unsigned)Ui + lh);
+            CHKR(L.lr + (unsigned)Uj + L0);
+            v.wi = rp[(unsigned)Ui + lh];
+            v.wj = rp[(unsigned)Uj + L0];
             // span-major rows: W(i-r, i+s-1) and W(j-s+1, j+r) have span s-1+r, coalesced along the lanes
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
@@ -1273,8 +1267,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         auto st = [&](const LA &v, int mask) {
             const int Lm00i = lo16(v.wi.x), Mm00i = hi16(v.wi.x), Om00i = lo16(v.wi.y), fLi = hi16(v.wi.y);
             const int fOi = lo16(v.wi.z);
-            const int Lm00j = lo16(v.wj.x), Mm00j = hi16(v.wj.x), fLj = lo16(v.wj.y), Lm10j = hi16(v.wj.y);
-            const int fMpj = lo16(v.wj.z), Kj = hi16(v.wj.z);
+            const int Lm00j = lo16(v.wj.x), Mm00j = hi16(v.wj.x), fLj = hi16(v.wj.y), Lm10j = hi16(v.wj.z);
+            const int fMpj = lo16(v.wj.w), Kj = hi16(v.wj.w);
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int wbpi = v.q[r].x, wpi = v.q[r].y, wbi = WBD(wbpi, v.s + r);
@@ -1392,7 +1386,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     // ---- fused b-loop: split point d inside [k, l] ----
     int pRm00 = seed, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
     int fR1 = INF, fR2 = INF, fMp = INF, fO2 = INF, pK2 = INF;
-    struct BV { int2 w2k, w2l; uint3 wk; uint4 wl; int s; };  // raw loads of one split step
+    struct BV { int2 w2k, w2l; uint4 wk, wl; int s; };  // raw loads of one split step
     auto load_b = [&](int s) {
         BV v;
         v.s = s;
@@ -1412,11 +1406,11 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         const unsigned lh = L0 + uh * (unsigned)s;
         // RK at X(i,j,d,l): x = Rm00|Mm00, y = fR|min(PL,PR), z = K|-
         // RL at X(i,j,k,d): x = Rm00|Mm00, y = Om00|Mm10, z = Om10|fR, w = fO|-
-        const uint32_t *rp = T.rec + L.lr;
-        CHKR(L.lr + 6 * L.C + 3 * ((unsigned)Uk + L0));
-        CHKR(L.lr + L.rl + 4 * ((unsigned)Ul + lh));
-        v.wk = ld_rec3(rp, 6u * (unsigned)L.C, (unsigned)Uk + L0);
-        v.wl = ld_rec4(rp, (unsigned)L.rl, (unsigned)Ul + lh);
+        const uint4 *rp = T.rec + L.lr;
+        CHKR(L.lr + L.C + (unsigned)Uk + L0);
+        CHKR(L.lr + 2 * L.C + (unsigned)Ul + lh);
+        v.wk = rp[(unsigned)(L.C + Uk) + L0];
+        v.wl = rp[(unsigned)(2 * L.C + Ul) + lh];
         return v;
     };
     auto step_b = [&](const BV &v, int mask) {
@@ -1452,7 +1446,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #pragma unroll
             for (int f = 0; f < 9; ++f) AL_[r][f] = INF;
         }
-        struct LB { uint3 wk; uint4 wl; int2 q[SHARE_R], p[SHARE_R]; int s; };  // raw loads of one split step
+        struct LB { uint4 wk, wl; int2 q[SHARE_R], p[SHARE_R]; int s; };  // raw loads of one split step
         auto ld = [&](int s) {
             LB v;
             v.s = s;
@@ -1460,11 +1454,11 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             const int Uk = a * L.M + s * m + ((s * (s + 1)) >> 1);
             const int Ul = a * L.M;
             const unsigned lh = L0 + uh * (unsigned)s;
-            const uint32_t *rp = T.rec + L.lr;
-            CHKR(L.lr + 6 * L.C + 3 * ((unsigned)Uk + L0));
-            CHKR(L.lr + L.rl + 4 * ((unsigned)Ul + lh));
-            v.wk = ld_rec3(rp, 6u * (unsigned)L.C, (unsigned)Uk + L0);
-            v.wl = ld_rec4(rp, (unsigned)L.rl, (unsigned)Ul + lh);
+            const uint4 *rp = T.rec + L.lr;
+            CHKR(L.lr + L.C + (unsigned)Uk + L0);
+            CHKR(L.lr + 2 * L.C + (unsigned)Ul + lh);
+            v.wk = rp[(unsigned)(L.C + Uk) + L0];
+            v.wl = rp[(unsigned)(2 * L.C + Ul) + lh];
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
@@ -1774,7 +1768,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     // loop records and interior-loop copies (the copies only where a later k_iloop can read them:
     // its pair can pair); in sharded fills the other ranks' cells get both from k_unpack
     if (!copies) return;
-    write_records(T, Lt, (unsigned)(a * Mt) + L0, clamp_store(vPLm00), clamp_store(vPMm00), clamp_store(vPOm00),
+    write_records(T, Lt.lr, C, (unsigned)(a * Mt) + L0, clamp_store(vPLm00), clamp_store(vPMm00), clamp_store(vPOm00),
                   clamp_store(vPfromL), clamp_store(vPfromO), clamp_store(vPLm10), clamp_store(vPfromMp),
                   clamp_store(vPK), clamp_store(vPRm00), clamp_store(vPfromR), imin(sPL, sPR), clamp_store(vPMm10),
                   clamp_store(vPOm10));
@@ -1792,10 +1786,6 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 __global__ __launch_bounds__(512) void k_level4d(DevTables T, int t, int wavesPerA, int split, int G, int rank, int nblk, int copies) {
     level4d_body<false>(T, t, wavesPerA, split, G, rank, nblk, copies);
 }
-// (CCJ_LEAD_WAVES: timing builds that pin the leaders' occupancy, tools/ablate.sh)
-#ifdef CCJ_LEAD_WAVES
-__attribute__((amdgpu_waves_per_eu(CCJ_LEAD_WAVES, CCJ_LEAD_WAVES)))
-#endif
 __global__ __launch_bounds__(512) void k_level4d_lead(DevTables T, int t, int wavesPerA, int split, int G, int rank, int nblk,
                                                       int copies) {
     level4d_body<true>(T, t, wavesPerA, split, G, rank, nblk, copies);
@@ -1915,7 +1905,7 @@ __global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r
 #pragma unroll
         for (int x = 0; x < NMAT4; ++x) v[x] = dst[x * C];
     }
-    write_records(T, Lt, (unsigned)(a * Mt + c), v[PLmloop00], v[PMmloop00], v[POmloop00], v[PfromL], v[PfromO],
+    write_records(T, Lt.lr, Lt.C, (unsigned)(a * Mt + c), v[PLmloop00], v[PMmloop00], v[POmloop00], v[PfromL], v[PfromO],
                   v[PLmloop10], v[PfromMprime], v[PK], v[PRmloop00], v[PfromR], imin(v[PL], v[PR]), v[PMmloop10],
                   v[POmloop10]);
     if (ptype(T, i, j) > 0) T.d4x[X.lbx + (long long)a * Mt + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = (int16_t)v[PL];
