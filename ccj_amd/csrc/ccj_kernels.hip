@@ -670,6 +670,24 @@ extern "C" int ccjk_items(const DevTables *T, int G, int rank, int simulate, lon
 // IL_B entries are loaded together (one s_load burst), then IL_B partner values, then reduced.
 // Null tail entries (dt 63) hit T.dummy, so the last batch needs no masking (PL/PR: cnt is the
 // whole list; PM stops early and substitutes null entries).
+// Loads at wave-uniform addresses of data no kernel of the fill writes (candidate lists, segment
+// tables): through the constant address space, so they are scalar (SMEM) loads.  As plain global
+// loads the compiler cannot prove them unclobbered (the kernel stores to T.d4), emits vector loads
+// plus readfirstlane, and a wave waiting for its next list entries then waits for every partner
+// load before them too (vmcnt counts in order): one memory latency per batch instead of one per
+// two batches.
+__device__ __forceinline__ uint32_t ld_const(const uint32_t *p) {
+    return *(const __attribute__((address_space(4))) uint32_t *)(unsigned long long)p;  // inttoptr: no flat cast
+}
+__device__ __forceinline__ uint2 ld_const(const uint2 *p) {
+    const unsigned long long v = *(const __attribute__((address_space(4))) unsigned long long *)(unsigned long long)p;
+    return make_uint2((unsigned)v, (unsigned)(v >> 32));
+}
+__device__ __forceinline__ const uint2 *uni_ptr(const uint2 *p) {
+    const unsigned long long v = (unsigned long long)p;
+    return (const uint2 *)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v)) |
+                           ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32)) << 32));
+}
 __device__ __forceinline__ int il_u1(uint32_t x) { return (int)((x >> 16) & 31u); }
 __device__ __forceinline__ int il_dt(uint32_t x) { return (int)(x >> 21); }
 __device__ __forceinline__ int il_e(uint32_t x) { return (int)(int16_t)(x & 0xffffu); }
@@ -681,12 +699,14 @@ template <bool CROSS, bool PMWIN>
 __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restrict__ ent, int cnt,
                                        unsigned long long Atab, int Btab, unsigned lofs2, int as, int bs) {
     int b1 = INF;
+    cnt = __builtin_amdgcn_readfirstlane(cnt);
     if (cnt <= 0) return b1;
+    ent = uni_ptr(ent);
     auto fetch = [&](int e0, uint2 *E) {
         const uint2 *ep = ent + e0;
 #pragma unroll
         for (int u = 0; u < IL_B; ++u) {
-            E[u] = ep[u];
+            E[u] = ld_const(ep + u);
             // PM stops at dt <= t-2, before the list's null tail: past cnt, substitute a null entry
             if (PMWIN && e0 + u >= cnt) E[u] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0u);
         }
@@ -713,7 +733,12 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
             }
 #endif
             // global address space: a plain pointer rebuilt from an integer would become a flat load
+#ifdef CCJ_ABLATE_ILHOT
+            // timing only: every partner read hits the same cache-resident line (wrong results)
+            v[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)T.dummy + lofs2 + (((uintptr_t)p) & 0));
+#else
             v[u] = *(const __attribute__((address_space(1))) int16_t *)(p + lofs2);
+#endif
         }
     };
     auto reduce = [&](const uint2 *E, const int *v) {
@@ -809,7 +834,11 @@ __device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__rest
                 }
             }
 #endif
+#ifdef CCJ_ABLATE_ILHOT
+            v[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)T.dummy + lofs2 + ((A + off) & 0));
+#else
             v[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)(A + off) + lofs2);
+#endif
         }
     };
     auto reduce = [&](const uint32_t *E, const int *v) {
@@ -868,10 +897,11 @@ __device__ __forceinline__ ILGroups il_groups(int nact, int lane) {
 }
 
 // one wave per work item (host-built list for level t: closing pairs that can pair, heaviest first)
-__global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long first, int nitems, int G_SH, int rank) {
+constexpr int IL_WPB = 4;  // waves (consecutive items) per k_iloop workgroup (1, 2, 8, 16 measured +3.6 ... +9 ms)
+__global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long long first, int nitems, int G_SH, int rank) {
     const int n = T.n, rs = T.rs, m = n - t - 2;
     const int lane = threadIdx.x & 63;
-    const int w = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int w = (int)blockIdx.x * IL_WPB + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (w >= nitems) return;
     const uint32_t it = T.items[first + w];
     const int role = (int)(it >> 30), f1 = (int)((it >> 20) & 1023u), f2 = (int)((it >> 10) & 1023u);
@@ -899,9 +929,9 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
                    2 * (T.ldx[tl].lbx + (long long)(a - lane) * T.ld[tl].M + (long long)i * m + (long long)i * lane + lane - 1 - BIAS);
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
         if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
-        const int e0 = (int)T.ilseg[pidx * IL_SEG + 3];
+        const int e0 = (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
         const uint2 *le = T.il + pidx * IL_CAP + e0;
-        const int lc = (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0;
+        const int lc = (int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0;
         const int b1 = G == 1 ? il_scan<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0)
                               : il_scan_g<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl);
 #ifdef CCJ_DEBUG_BOUNDS
@@ -930,9 +960,9 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         if (lvl_ok) Atab = (unsigned long long)T.d4x + 2 * (T.ldx[tl].lbx + T.ld[tl].C + (long long)a * T.ld[tl].M);
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
         if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
-        const int e0 = (int)T.ilseg[pidx * IL_SEG + 3];
+        const int e0 = (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
         const uint2 *le = T.il + pidx * IL_CAP + e0;
-        const int lc = (int)T.ilseg[pidx * IL_SEG + IL_SEG - 1] - e0;
+        const int lc = (int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0;
         const int b1 = G == 1 ? il_scan<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0)
                               : il_scan_g<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl);
 #ifdef CCJ_DEBUG_BOUNDS
@@ -969,8 +999,8 @@ __global__ __launch_bounds__(256) void k_iloop(DevTables T, int t, long long fir
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
         if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
         // entries with dt > t-2 fit no cell of this level
-        const int cnt = (int)T.ilmseg[pidx * IL_SEG + imin(t - 1, IL_SEG - 1)];
-        const int e0 = (int)T.ilmseg[pidx * IL_SEG + 3];
+        const int cnt = (int)ld_const(T.ilmseg + pidx * IL_SEG + imin(t - 1, IL_SEG - 1));
+        const int e0 = (int)ld_const(T.ilmseg + pidx * IL_SEG + 3);
         const uint2 *le = T.ilm + pidx * IL_CAP + e0;
         const int b1 = G == 1 ? il_scan<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as)
                               : il_scan_g<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl);
@@ -1772,6 +1802,9 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                   clamp_store(vPfromL), clamp_store(vPfromO), clamp_store(vPLm10), clamp_store(vPfromMp),
                   clamp_store(vPK), clamp_store(vPRm00), clamp_store(vPfromR), imin(sPL, sPR), clamp_store(vPMm10),
                   clamp_store(vPOm10));
+#ifdef CCJ_ABLATE_NOCOPY
+    return;  // timing only: no interior-loop copies (k_iloop then reads stale values)
+#endif
     const LvlX X = T.ldx[t];
     if (pl_ok) T.d4x[X.lbx + (long long)a * Mt + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = (int16_t)sPL;
     if (pr_ok) {
@@ -1847,7 +1880,7 @@ extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int n
     return 0;
 #endif
     if (nitems <= 0) return 0;
-    hipLaunchKernelGGL(k_iloop, dim3((unsigned)((nitems + 3) / 4)), dim3(256), 0, (hipStream_t)stream, *T, t, first_item,
+    hipLaunchKernelGGL(k_iloop, dim3((unsigned)((nitems + IL_WPB - 1) / IL_WPB)), dim3(64 * IL_WPB), 0, (hipStream_t)stream, *T, t, first_item,
                        nitems, G, rank);
     return (int)hipGetLastError();
 }

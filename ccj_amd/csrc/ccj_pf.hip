@@ -64,6 +64,40 @@ struct PfG {  // getters with the reference's semantics
     __device__ __forceinline__ int pt(int i, int j) const { return D.pt[(j - i) * D.rs + i]; }
 };
 
+// Wave-uniform loads of tables no kernel of the fill writes (level descriptors, expcp_pen /
+// expPUP_pen): through the constant address space, so they are scalar loads with their own wait
+// counter.  (As plain global loads the compiler cannot prove them unclobbered and emits vector
+// loads, which a split loop then waits for in order with everything issued before them.)
+__device__ __forceinline__ double ldc_f64(const double *p) {
+    return *(const __attribute__((address_space(4))) double *)(unsigned long long)p;
+}
+struct PfLvlS { long long lb, C; int M; };
+__device__ __forceinline__ PfLvlS ldc_lvl(const PfLvl *p) {
+    const auto *q = (const __attribute__((address_space(4))) PfLvl *)(unsigned long long)p;
+    return PfLvlS{q->lb, q->C, q->M};
+}
+
+// Software-pipelined split loop over s = s0 .. s1: the loads of step s+1 are issued before step s
+// is reduced, into two alternating buffers (no register copies across the back-edge, which would
+// make the compiler wait for every load of the trip first).  The reduce adds each sum's terms in
+// the reference's order, so the bits do not change.
+template <class V, class LD, class RD>
+__device__ __forceinline__ void pf_pipe(int s, int s1, LD ld, RD rd) {
+    if (s > s1) return;
+    V A = ld(s);
+#pragma unroll 1
+    for (;;) {
+        if (s + 1 > s1) { rd(A); return; }
+        const V B = ld(s + 1);
+        rd(A);
+        ++s;
+        if (s + 1 > s1) { rd(B); return; }
+        A = ld(s + 1);
+        rd(B);
+        ++s;
+    }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -266,6 +300,9 @@ __global__ __launch_bounds__(64) void k_pf_diag(PfDev D, int s) {
 // The split loops run over s = d - i (or d - k):
 //   X1(s) = X(i+s, j, k, l)   X2(s) = X(i, i+s, k, l)   X3(s) = X(i, j, k+s, l)   X4(s) = X(i, j, k, k+s)
 // ---------------------------------------------------------------------------------------------
+#ifdef CCJ_PF_LEVEL_WAVES
+__attribute__((amdgpu_waves_per_eu(CCJ_PF_LEVEL_WAVES)))
+#endif
 __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     const PfG G{D};
     const PfExp &E = *D.E;
@@ -332,66 +369,168 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     cRm10 += (b >= 1 ? X(PF_PRmloop10, 1, 0, 1, 0) : 0) * cp1;  // PRmloop10(i,j,k+1,l) * expcp_pen[1] (:618-626)
     cMm01 += (b >= 1 ? X(PF_PMmloop01, 1, 0, 1, 0) : 0) + cp1;  // PMmloop01(i,j,k+1,l) "+ expcp_pen[1]" (:642-650)
     cMm10 += (a >= 1 ? X(PF_PMmloop10, 1, 1, 1, 0) : 0) * cp1;  // PMmloop10(i,j-1,k,l) * expcp_pen[1] (:652-663)
-    // (i,j) gap, d = i+s
-#pragma unroll 2
-    for (int s = 0; s <= a; ++s) {
-        if (s > 0) {  // X1 = X(i+s, j, k, l), WB(i, i+s-1) / WBP(i, i+s-1)
-            const double bpi = BPi(s), wbi = cpp[s] + bpi;
-            const int lm00 = X1(PF_PLmloop00, s), mm00 = X1(PF_PMmloop00, s), om00 = X1(PF_POmloop00, s);
-            cLm00 += wbi * lm00;  // :558-560
-            cLm10 += bpi * lm00;  // :582-584
-            cMm10 += bpi * mm00;  // :656-658
-            cOm00 += wbi * om00;  // :669-670
-            cOm10 += bpi * om00;  // :690-692
-        }
-        if (s < a) {  // X2 = X(i, i+s, k, l), WB(i+s+1, j) / WBP(i+s+1, j)
-            const double bpj = BPj(s), wbj = cpp[a - s] + bpj;
-            const int lm00 = X2(PF_PLmloop00, s);
-            cLm00 += lm00 * wbj;                      // :561-562
-            cLm01 += lm00 * bpj;                      // :574-576
-            if (s > 0) cLm10 += X2(PF_PLmloop10, s) * wbj;  // :585-587
-            cMm00 += X2(PF_PMmloop00, s) * wbj;       // :632-633
-            if (s > 0) {  // PfromL / PfromM / PfromO / PK: d = i+1 .. j-1, WP(i, d-1), WP(d+1, j)
-                const double wpi = WPi(s), wpj = WPj(s);
-                cFL += X1(PF_PfromL, s) * wpi;  // :491-493
-                cFL += X2(PF_PfromL, s) * wpj;
-                cFM += X2(PF_PfromM, s) * wpj;  // :523-524
-                cFO += X1(PF_PfromO, s) * wpi;  // :540-541
-                cK += X2(PF_PK, s) * wpj;       // :398-399
-            }
-        }
+    // 4-D operand of a split step: matrix x at (t-dt, a-da, h+dh, i+di), descriptor by scalar load
+    auto Xs = [&](const PfLvlS &Lp, int x, int dt, int da, int dh, int di) -> int {
+        const int mp = m + dt;
+        const long long U = Lp.lb + (long long)x * Lp.C + (long long)(a - da) * Lp.M + (long long)dh * mp -
+                            (((long long)dh * (dh - 1)) >> 1) + di;
+        return *(gint *)(D.d4 + U + (off + h * (dt - dh)));
+    };
+    // (i,j) gap, d = i+s: s = 0 (the X2 terms only), s = 1 .. a-1 pipelined, s = a (the X1 terms only)
+    if (a >= 1) {  // s = 0: X2 = X(i, i, k, l), WB(i+1, j) / WBP(i+1, j)
+        const double bpj = BPj(0), wbj = ldc_f64(cpp + a) + bpj;
+        const int lm00 = X2(PF_PLmloop00, 0);
+        cLm00 += lm00 * wbj;  // :561-562
+        cLm01 += lm00 * bpj;  // :574-576
+        cMm00 += X2(PF_PMmloop00, 0) * wbj;  // :632-633
+    }
+    struct SA { double bpi, wppi, bpj, wppj; int lm1, mm1, om1, fl1, fo1, lm2, l102, mm2, fl2, fm2, k2, s; };
+    auto ldA = [&](int s) {
+        SA v;
+        v.s = s;
+        const PfLvlS L1 = ldc_lvl(D.ld + t - s), L2 = ldc_lvl(D.ld + b + s);
+        v.bpi = WBP[(s - 1) * rs + i];
+        v.bpj = WBP[(a - s - 1) * rs + i + s + 1];
+        v.wppi = WPP[(s - 1) * rs + i];
+        v.wppj = WPP[(a - s - 1) * rs + i + s + 1];
+        v.lm1 = Xs(L1, PF_PLmloop00, s, s, 0, s);  // X1 = X(i+s, j, k, l)
+        v.mm1 = Xs(L1, PF_PMmloop00, s, s, 0, s);
+        v.om1 = Xs(L1, PF_POmloop00, s, s, 0, s);
+        v.fl1 = Xs(L1, PF_PfromL, s, s, 0, s);
+        v.fo1 = Xs(L1, PF_PfromO, s, s, 0, s);
+        v.lm2 = Xs(L2, PF_PLmloop00, a - s, a - s, a - s, 0);  // X2 = X(i, i+s, k, l)
+        v.l102 = Xs(L2, PF_PLmloop10, a - s, a - s, a - s, 0);
+        v.mm2 = Xs(L2, PF_PMmloop00, a - s, a - s, a - s, 0);
+        v.fl2 = Xs(L2, PF_PfromL, a - s, a - s, a - s, 0);
+        v.fm2 = Xs(L2, PF_PfromM, a - s, a - s, a - s, 0);
+        v.k2 = Xs(L2, PF_PK, a - s, a - s, a - s, 0);
+        return v;
+    };
+    auto rdA = [&](const SA &v) {
+        const int s = v.s;
+        const double bpi = v.bpi, wbi = ldc_f64(cpp + s) + bpi;  // WB(i, i+s-1) / WBP(i, i+s-1)
+        cLm00 += wbi * v.lm1;  // :558-560
+        cLm10 += bpi * v.lm1;  // :582-584
+        cMm10 += bpi * v.mm1;  // :656-658
+        cOm00 += wbi * v.om1;  // :669-670
+        cOm10 += bpi * v.om1;  // :690-692
+        const double bpj = v.bpj, wbj = ldc_f64(cpp + (a - s)) + bpj;  // WB(i+s+1, j) / WBP(i+s+1, j)
+        cLm00 += v.lm2 * wbj;   // :561-562
+        cLm01 += v.lm2 * bpj;   // :574-576
+        cLm10 += v.l102 * wbj;  // :585-587
+        cMm00 += v.mm2 * wbj;   // :632-633
+        // PfromL / PfromM / PfromO / PK: d = i+1 .. j-1, WP(i, d-1), WP(d+1, j)
+        const double wpi = ldc_f64(pup + s) + v.wppi, wpj = ldc_f64(pup + (a - s)) + v.wppj;
+        cFL += v.fl1 * wpi;  // :491-493
+        cFL += v.fl2 * wpj;
+        cFM += v.fm2 * wpj;  // :523-524
+        cFO += v.fo1 * wpi;  // :540-541
+        cK += v.k2 * wpj;    // :398-399
+    };
+    pf_pipe<SA>(1, a - 1, ldA, rdA);
+    if (a >= 1) {  // s = a: X1 = X(j, j, k, l), WB(i, j-1) / WBP(i, j-1)
+        const double bpi = BPi(a), wbi = ldc_f64(cpp + a) + bpi;
+        const int lm00 = X1(PF_PLmloop00, a), mm00 = X1(PF_PMmloop00, a), om00 = X1(PF_POmloop00, a);
+        cLm00 += wbi * lm00;  // :558-560
+        cLm10 += bpi * lm00;  // :582-584
+        cMm10 += bpi * mm00;  // :656-658
+        cOm00 += wbi * om00;  // :669-670
+        cOm10 += bpi * om00;  // :690-692
     }
     if (b >= 1) cOm00 = X(PF_POmloop00, 1, 0, 0, 0) * (cpp[1] + WBP[l]);  // :671-673: assigns POmloop00(i,j,k,l-1) * WB(l,l)
-    // (k,l) gap, d = k+s
-#pragma unroll 2
-    for (int s = 0; s <= b; ++s) {
-        if (s > 0) {  // X3 = X(i, j, k+s, l), WB(k, k+s-1) / WBP(k, k+s-1)
-            const double bpk = BPk(s), wbk = cpp[s] + bpk;
-            const int rm00 = X3(PF_PRmloop00, s);
-            cRm00 += wbk * rm00;                   // :596-598
-            cRm10 += bpk * rm00;                   // :622-624
-            cMm00 += X3(PF_PMmloop00, s) * wbk;    // :634-636
-        }
-        if (s < b) {  // X4 = X(i, j, k, k+s), WB(k+s+1, l) / WBP(k+s+1, l)
-            const double bpl = BPl(s), wbl = cpp[b - s] + bpl;
-            const int rm00 = X4(PF_PRmloop00, s);
-            cRm00 += rm00 * wbl;                   // :599-600
-            cRm01 += rm00 * bpl;                   // :612-614
-            cMm01 += X4(PF_PMmloop00, s) * bpl;    // :646-648
-            cOm01 += X4(PF_POmloop00, s) * bpl;    // :682-684
-            if (s > 0) {  // d = k+1 .. l-1
-                const int om10 = X4(PF_POmloop10, s);
-                const double wpk = WPk(s), wpl = WPl(s);
-                cMm10 += om10 * wbl;               // :659-661
-                cOm10 += om10 + wbl;               // :693-695 ("+ get_WB")
-                cFR += X3(PF_PfromR, s) * wpk;     // :508-510
-                cFR += X4(PF_PfromR, s) * wpl;
-                cFM += X3(PF_PfromM, s) * wpk;     // :526-527
-                cFO += X4(PF_PfromO, s) * wpl;     // :544-545
-                cK += X3(PF_PK, s) * wpk;          // :401-402
-            }
-        }
+    // (k,l) gap, d = k+s: s = 0 (the X4 terms only), s = 1 .. b-1 pipelined, s = b (the X3 terms only)
+    if (b >= 1) {  // s = 0: X4 = X(i, j, k, k), WB(k+1, l) / WBP(k+1, l)
+        const double bpl = BPl(0), wbl = ldc_f64(cpp + b) + bpl;
+        const int rm00 = X4(PF_PRmloop00, 0);
+        cRm00 += rm00 * wbl;                   // :599-600
+        cRm01 += rm00 * bpl;                   // :612-614
+        cMm01 += X4(PF_PMmloop00, 0) * bpl;    // :646-648
+        cOm01 += X4(PF_POmloop00, 0) * bpl;    // :682-684
     }
+    struct SB { double bpk, wppk, bpl, wppl; int rm3, mm3, fr3, fm3, k3, rm4, mm4, om4, o104, fr4, fo4, s; };
+    auto ldB = [&](int s) {
+        SB v;
+        v.s = s;
+        const PfLvlS L3 = ldc_lvl(D.ld + t - s), L4 = ldc_lvl(D.ld + a + s);
+        v.bpk = WBP[(s - 1) * rs + k];
+        v.bpl = WBP[(b - s - 1) * rs + k + s + 1];
+        v.wppk = WPP[(s - 1) * rs + k];
+        v.wppl = WPP[(b - s - 1) * rs + k + s + 1];
+        v.rm3 = Xs(L3, PF_PRmloop00, s, 0, s, 0);  // X3 = X(i, j, k+s, l)
+        v.mm3 = Xs(L3, PF_PMmloop00, s, 0, s, 0);
+        v.fr3 = Xs(L3, PF_PfromR, s, 0, s, 0);
+        v.fm3 = Xs(L3, PF_PfromM, s, 0, s, 0);
+        v.k3 = Xs(L3, PF_PK, s, 0, s, 0);
+        v.rm4 = Xs(L4, PF_PRmloop00, b - s, 0, 0, 0);  // X4 = X(i, j, k, k+s)
+        v.mm4 = Xs(L4, PF_PMmloop00, b - s, 0, 0, 0);
+        v.om4 = Xs(L4, PF_POmloop00, b - s, 0, 0, 0);
+        v.o104 = Xs(L4, PF_POmloop10, b - s, 0, 0, 0);
+        v.fr4 = Xs(L4, PF_PfromR, b - s, 0, 0, 0);
+        v.fo4 = Xs(L4, PF_PfromO, b - s, 0, 0, 0);
+        return v;
+    };
+    auto rdB = [&](const SB &v) {
+        const int s = v.s;
+        const double bpk = v.bpk, wbk = ldc_f64(cpp + s) + bpk;  // WB(k, k+s-1) / WBP(k, k+s-1)
+        cRm00 += wbk * v.rm3;  // :596-598
+        cRm10 += bpk * v.rm3;  // :622-624
+        cMm00 += v.mm3 * wbk;  // :634-636
+        const double bpl = v.bpl, wbl = ldc_f64(cpp + (b - s)) + bpl;  // WB(k+s+1, l) / WBP(k+s+1, l)
+        cRm00 += v.rm4 * wbl;  // :599-600
+        cRm01 += v.rm4 * bpl;  // :612-614
+        cMm01 += v.mm4 * bpl;  // :646-648
+        cOm01 += v.om4 * bpl;  // :682-684
+        // d = k+1 .. l-1
+        const double wpk = ldc_f64(pup + s) + v.wppk, wpl = ldc_f64(pup + (b - s)) + v.wppl;
+        cMm10 += v.o104 * wbl;  // :659-661
+        cOm10 += v.o104 + wbl;  // :693-695 ("+ get_WB")
+        cFR += v.fr3 * wpk;     // :508-510
+        cFR += v.fr4 * wpl;
+        cFM += v.fm3 * wpk;     // :526-527
+        cFO += v.fo4 * wpl;     // :544-545
+        cK += v.k3 * wpk;       // :401-402
+    };
+    pf_pipe<SB>(1, b - 1, ldB, rdB);
+    if (b >= 1) {  // s = b: X3 = X(i, j, l, l), WB(k, l-1) / WBP(k, l-1)
+        const double bpk = BPk(b), wbk = ldc_f64(cpp + b) + bpk;
+        const int rm00 = X3(PF_PRmloop00, b);
+        cRm00 += wbk * rm00;                   // :596-598
+        cRm10 += bpk * rm00;                   // :622-624
+        cMm00 += X3(PF_PMmloop00, b) * wbk;    // :634-636
+    }
+    // The rest of the cell reads pair types, the level t-2 neighbours of the stack terms and
+    // k_pf_iloop's sums, none of which depends on the sums above: issue every load before the first
+    // store (gfx950's vmcnt counts loads and stores in order, so a load behind a store waits for it),
+    // then evaluate PL, PR, PM, PO exactly as before.
+    const int ptij = G.pt(i, j), ptkl = G.pt(k, l), ptjk = G.pt(j, k), ptil = G.pt(i, l);
+    const PfLvlS L2 = ldc_lvl(D.ld + (t >= 2 ? t - 2 : 0));
+    // PL: inner cell (i+1, j-1, k, l) = (t-2, a-2, h+1, i+1), outside the matrix (0) when a < 2
+    const bool inL = a >= 2;
+    const int xL = (inL && a < 6) ? Xs(L2, PF_PL, 2, 2, 1, 1) : 0;
+    const int xLm10 = inL ? Xs(L2, PF_PLmloop10, 2, 2, 1, 1) : 0, xLm01 = inL ? Xs(L2, PF_PLmloop01, 2, 2, 1, 1) : 0;
+    const int xFL = inL ? Xs(L2, PF_PfromL, 2, 2, 1, 1) : 0;
+    const double rL = a >= 6 ? Rt[off0] : 0.0, eL = a < 6 ? D.est[a * rs + i] : 0.0;
+    // PR: (i, j, k+1, l-1) = (t-2, a, h+1, i), outside when b < 2
+    const bool inR = b >= 2;
+    const int xR = (inR && b < 6) ? Xs(L2, PF_PR, 2, 0, 1, 0) : 0;
+    const int xRm10 = inR ? Xs(L2, PF_PRmloop10, 2, 0, 1, 0) : 0, xRm01 = inR ? Xs(L2, PF_PRmloop01, 2, 0, 1, 0) : 0;
+    const int xFR = inR ? Xs(L2, PF_PfromR, 2, 0, 1, 0) : 0;
+    const double rR = b >= 6 ? Rt[C + off0] : 0.0, eR = b < 6 ? D.est[b * rs + k] : 0.0;
+    // PM: (i, j-1, k+1, l) = (t-2, a-1, h+2, i), outside when a < 1 or b < 1
+    const bool inM = a >= 1 && b >= 1, winM = a >= 2 && b >= 2;
+    const int xM = (inM && !winM) ? Xs(L2, PF_PM, 2, 1, 2, 0) : 0;
+    const int xMm10 = inM ? Xs(L2, PF_PMmloop10, 2, 1, 2, 0) : 0, xMm01 = inM ? Xs(L2, PF_PMmloop01, 2, 1, 2, 0) : 0;
+    const int xFM = inM ? Xs(L2, PF_PfromM, 2, 1, 2, 0) : 0;
+    // get_e_stP(j-1, k+1): for j == 1 or k == n the reference indexes pair[][] with S[0] (= n) or
+    // S[n+1]; the factor multiplies PM(i, j-1, k+1, l), which is then outside the matrix (0), so
+    // any finite value gives 0 — use 0 instead of reading past the table
+    const double rM = winM ? Rt[2 * C + off0] : 0.0, eM = (!winM && j > 1 && k < n) ? D.est[(h + 4) * rs + (j - 1)] : 0.0;
+    // PO: (i+1, j, k, l-1) = (t-2, a-1, h, i+1), outside when a < 1 or b < 1
+    const int xO = inM ? Xs(L2, PF_PO, 2, 1, 0, 1) : 0;
+    const int xOm10 = inM ? Xs(L2, PF_POmloop10, 2, 1, 0, 1) : 0, xOm01 = inM ? Xs(L2, PF_POmloop01, 2, 1, 0, 1) : 0;
+    const int xFO = inM ? Xs(L2, PF_PfromO, 2, 1, 0, 1) : 0;
+    const double eO = D.est[(t + h + 2) * rs + i];
+
     put(PF_PLmloop00, cLm00);
     put(PF_PLmloop01, cLm01);
     put(PF_PLmloop10, cLm10);
@@ -405,87 +544,75 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     put(PF_POmloop01, cOm01);
     put(PF_POmloop10, cOm10);
 
-    // PL (:414-430) with get_PLiloop (:736-756) and get_PLmloop (:758-768); the inner cell
-    // (i+1, j-1, k, l) is (t-2, a-2, h+1, i+1), outside the matrix (0) when a < 2
+    // PL (:414-430) with get_PLiloop (:736-756) and get_PLmloop (:758-768)
     int PL = 0;
     {
         double c = 0;
-        if (G.pt(i, j) > 0) {
-            const bool in = a >= 2;
+        if (ptij > 0) {
             double r = 0;
-            if (a >= 6) r = Rt[off0];  // k_pf_iloop: the stack term, then the window
-            else r += (in ? X(PF_PL, 2, 2, 1, 1) : 0) * D.est[a * rs + i];  // no window (u2 <= a-u1-6)
+            if (a >= 6) r = rL;  // k_pf_iloop: the stack term, then the window
+            else r += xL * eL;   // no window (u2 <= a-u1-6)
             c += r;
             double q = 0;
-            q += (in ? X(PF_PLmloop10, 2, 2, 1, 1) : 0) * ap * bp;
-            q += (double)imul_wrap(in ? X(PF_PLmloop01, 2, 2, 1, 1) : 0, D.ap_int) * bp;
+            q += xLm10 * ap * bp;
+            q += (double)imul_wrap(xLm01, D.ap_int) * bp;
             c += q * bp;
-            if (j >= i + TURN + 1) c += (in ? X(PF_PfromL, 2, 2, 1, 1) : 0) * 1.0;
+            if (j >= i + TURN + 1) c += xFL * 1.0;
         }
         PL = put(PF_PL, c);
-        if (G.pt(i, j) > 0) D.cx[L.lbx + a * L.M + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = PL;
+        if (ptij > 0) D.cx[L.lbx + a * L.M + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = PL;
     }
-    // PR (:432-447), get_PRiloop (:770-790), get_PRmloop (:792-802); (i, j, k+1, l-1) is
-    // (t-2, a, h+1, i), outside when b < 2
+    // PR (:432-447), get_PRiloop (:770-790), get_PRmloop (:792-802)
     int PR = 0;
     {
         double c = 0;
-        if (G.pt(k, l) > 0) {
-            const bool in = b >= 2;
+        if (ptkl > 0) {
             double r = 0;
-            if (b >= 6) r = Rt[C + off0];
-            else r += (in ? X(PF_PR, 2, 0, 1, 0) : 0) * D.est[b * rs + k];
+            if (b >= 6) r = rR;
+            else r += xR * eR;
             c += r;
             double q = 0;
-            q += (in ? X(PF_PRmloop10, 2, 0, 1, 0) : 0) * ap * bp;
-            q += (in ? X(PF_PRmloop01, 2, 0, 1, 0) : 0) * ap * bp;
+            q += xRm10 * ap * bp;
+            q += xRm01 * ap * bp;
             c += q * bp;
-            if (l >= k + TURN + 1) c += (in ? X(PF_PfromR, 2, 0, 1, 0) : 0) * 1.0;
+            if (l >= k + TURN + 1) c += xFR * 1.0;
         }
         PR = put(PF_PR, c);
         const int q = i + h - 1;
-        if (G.pt(k, l) > 0) D.cx[L.lbx + C + a * L.M + ((q * (q + 1)) >> 1) + i - 1] = PR;
+        if (ptkl > 0) D.cx[L.lbx + C + a * L.M + ((q * (q + 1)) >> 1) + i - 1] = PR;
     }
-    // PM (:449-467), get_PMiloop (:804-824), get_PMmloop (:826-836); (i, j-1, k+1, l) is
-    // (t-2, a-1, h+2, i), outside when a < 1 or b < 1
+    // PM (:449-467), get_PMiloop (:804-824), get_PMmloop (:826-836)
     int PM = 0;
     {
         double c = 0;
-        if (G.pt(j, k) > 0) {
-            const bool in = a >= 1 && b >= 1;
+        if (ptjk > 0) {
             double r = 0;
-            // get_e_stP(j-1, k+1): for j == 1 or k == n the reference indexes pair[][] with S[0] (= n)
-            // or S[n+1]; the factor multiplies PM(i, j-1, k+1, l), which is then outside the matrix
-            // (0), so any finite value gives 0 — use 0 instead of reading past the table
-            const double est_m = (j > 1 && k < n) ? D.est[(h + 4) * rs + (j - 1)] : 0.0;
-            if (a >= 2 && b >= 2) r = Rt[2 * C + off0];
-            else r += (in ? X(PF_PM, 2, 1, 2, 0) : 0) * est_m;
+            if (winM) r = rM;
+            else r += xM * eM;
             c += r;
             double q = 0;
-            q += (in ? X(PF_PMmloop10, 2, 1, 2, 0) : 0) * ap * bp;
-            q += (in ? X(PF_PMmloop01, 2, 1, 2, 0) : 0) * ap * bp;
+            q += xMm10 * ap * bp;
+            q += xMm01 * ap * bp;
             c += q * bp;
-            if (k >= j + TURN - 1) c += (in ? X(PF_PfromM, 2, 1, 2, 0) : 0) * 1.0;
+            if (k >= j + TURN - 1) c += xFM * 1.0;
             if (i == j && k == l) c += 1.0;
         }
         PM = put(PF_PM, c);
-        if (G.pt(j, k) > 0) D.pmx[L.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = PM;
+        if (ptjk > 0) D.pmx[L.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = PM;
     }
-    // PO (:469-486), get_POiloop (:838-858: reads PO(d,j,dp,k) with dp > k, always 0), get_POmloop;
-    // (i+1, j, k, l-1) is (t-2, a-1, h, i+1), outside when a < 1 or b < 1
+    // PO (:469-486), get_POiloop (:838-858: reads PO(d,j,dp,k) with dp > k, always 0), get_POmloop
     int PO = 0;
     {
         double c = 0;
-        if (G.pt(i, l) > 0) {
-            const bool in = a >= 1 && b >= 1;
+        if (ptil > 0) {
             double r = 0;
-            r += (in ? X(PF_PO, 2, 1, 0, 1) : 0) * D.est[(t + h + 2) * rs + i];
+            r += xO * eO;
             c += r;
             double q = 0;
-            q += (in ? X(PF_POmloop10, 2, 1, 0, 1) : 0) * ap * bp;
-            q += (in ? X(PF_POmloop01, 2, 1, 0, 1) : 0) * ap * bp;
+            q += xOm10 * ap * bp;
+            q += xOm01 * ap * bp;
             c += q * bp;
-            if (l >= i + TURN + 1) c += (in ? X(PF_PfromO, 2, 1, 0, 1) : 0) * 1.0;
+            if (l >= i + TURN + 1) c += xFO * 1.0;
         }
         PO = put(PF_PO, c);
     }
