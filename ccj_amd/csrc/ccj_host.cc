@@ -1541,14 +1541,14 @@ static int seq_setup(ccj_ctx *c) {
             for (int b; (b = next.fetch_add(1)) < nb;) {
                 const int t = b / G, r = b % G;
                 if (!(c->simulate || r == c->rank) || t < 4 || t >= c->nlev) continue;
-                const long long hc = count_level_items(pt.data(), rs, n, t, G, r);
+                const long long hc = count_level_items(pt.data(), rs, n, t, G, r, IL_CW);
                 if (!host_count && hc != cnt[b]) bad = true;  // check mode: host and GPU counts agree
                 cnt[b] = hc;
                 if (check) {  // CCJ_CHECK_ITEMS=1: the generic enumeration must agree
                     const ItemRows R = item_rows(n, t, G, r);
                     long long sum = 0;
                     uint32_t it0;
-                    for (int x = 0; x < R.nPL + R.nPR + R.nPM; ++x) sum += item_row(hpt, n, t, R, x, G, r, it0);
+                    for (int x = 0; x < R.nPL + R.nPR + R.nPM; ++x) sum += item_row(hpt, n, t, R, x, G, r, it0, IL_CW);
                     if (sum != cnt[b]) bad = true;
                 }
             }

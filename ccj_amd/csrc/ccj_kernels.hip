@@ -616,7 +616,7 @@ __global__ __launch_bounds__(256) void k_items(DevTables T, int G, int rank, int
     for (int c0 = 0; c0 < nrows; c0 += 256) {
         const int x = c0 + tid;
         uint32_t it0 = 0;
-        const int cnt = x < nrows ? item_row(pt, T.n, t, R, x, G, r, it0) : 0;
+        const int cnt = x < nrows ? item_row(pt, T.n, t, R, x, G, r, it0, IL_CW) : 0;
         // exclusive scan of cnt over the workgroup: wave scan, then the wave totals
         int inc = cnt;
 #pragma unroll
@@ -694,40 +694,49 @@ __device__ __forceinline__ int il_e(uint32_t x) { return (int)(int16_t)(x & 0xff
 
 // min over the wave's candidate list of energy + partner value (PL/PR/PM interior loops).
 // Software-pipelined one batch deep: the entries and partner loads of batch k+1 are issued before
-// batch k is reduced, so a wave keeps 2*IL_B partner loads in flight.
-template <bool CROSS, bool PMWIN>
-__device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restrict__ ent, int cnt,
-                                       unsigned long long Atab, int Btab, unsigned lofs2, int as, int bs) {
-    int b1 = INF;
+// batch k is reduced, so a wave keeps 2*IL_B partner loads in flight.  PAIR: the wave holds two
+// 64-cell chunks of its row (lane offsets lofs2 and lofs2b) and loads both partners of every
+// entry, so a list entry's decode and address cost is paid once per 128 cells; half as many
+// entries per batch keep the loads in flight (and the registers) at 2*IL_B.
+template <bool CROSS, bool PMWIN, bool PAIR>
+__device__ __forceinline__ int2 il_scan(const DevTables &T, const uint2 *__restrict__ ent, int cnt,
+                                        unsigned long long Atab, int Btab, unsigned lofs2, int as, int bs,
+                                        unsigned lofs2b, int asb, int bsb) {
+    constexpr int NB = PAIR ? IL_B / 2 : IL_B;
+    int b1 = INF, b2 = INF;
     cnt = __builtin_amdgcn_readfirstlane(cnt);
-    if (cnt <= 0) return b1;
+    if (cnt <= 0) return make_int2(b1, b2);
     ent = uni_ptr(ent);
     auto fetch = [&](int e0, uint2 *E) {
         const uint2 *ep = ent + e0;
 #pragma unroll
-        for (int u = 0; u < IL_B; ++u) {
+        for (int u = 0; u < NB; ++u) {
             E[u] = ld_const(ep + u);
             // PM stops at dt <= t-2, before the list's null tail: past cnt, substitute a null entry
             if (PMWIN && e0 + u >= cnt) E[u] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0u);
         }
     };
-    auto issue = [&](const uint2 *E, int *v) {
+    auto issue = [&](const uint2 *E, int *v, int *w) {
 #pragma unroll
-        for (int u = 0; u < IL_B; ++u) {
+        for (int u = 0; u < NB; ++u) {
             const int dt = il_dt(E[u].x), u1 = il_u1(E[u].x);
             unsigned off = (unsigned)__builtin_amdgcn_readlane(Btab, u1);
             if (CROSS) off += E[u].y;
             const char *p = (const char *)(rdl64(Atab, dt) + off);
 #ifdef CCJ_DEBUG_BOUNDS
             {   // the partner must lie inside its copy (or be the null target)
-                const int16_t *q = (const int16_t *)(p + lofs2);
-                const bool in = (q >= T.d4x && q < T.d4x + T.nx) || (q >= T.pmx && q < T.pmx + T.npm) ||
-                                (q >= T.dummy && q < T.dummy + T.n + 64);
-                if (!in || (dt != 63 && (dt < 2 || dt > 2 * MAXLOOP - 2))) {
+                bool bad = false;
+                for (int c = 0; c < (PAIR ? 2 : 1); ++c) {
+                    const int16_t *q = (const int16_t *)(p + (c ? lofs2b : lofs2));
+                    const bool in = (q >= T.d4x && q < T.d4x + T.nx) || (q >= T.pmx && q < T.pmx + T.npm) ||
+                                    (q >= T.dummy && q < T.dummy + T.n + 64);
+                    bad = bad || !in;
+                }
+                if (bad || (dt != 63 && (dt < 2 || dt > 2 * MAXLOOP - 2))) {
                     if (atomicOr(T.err, 64) == 0)
-                        printf("k_iloop OOB: dt %d u1 %d off %u lofs2 %u p-d4x %lld p-pmx %lld p-dummy %lld\n", dt, u1,
-                               off, lofs2, (long long)(q - T.d4x), (long long)(q - T.pmx), (long long)(q - T.dummy));
-                    v[u] = 0;
+                        printf("k_iloop OOB: dt %d u1 %d off %u lofs2 %u lofs2b %u pair %d\n", dt, u1, off, lofs2, lofs2b,
+                               (int)PAIR);
+                    v[u] = w[u] = 0;
                     continue;
                 }
             }
@@ -736,23 +745,27 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
 #ifdef CCJ_ABLATE_ILHOT
             // timing only: every partner read hits the same cache-resident line (wrong results)
             v[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)T.dummy + lofs2 + (((uintptr_t)p) & 0));
+            if (PAIR) w[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)T.dummy + lofs2 + 2);
 #else
             v[u] = *(const __attribute__((address_space(1))) int16_t *)(p + lofs2);
+            if (PAIR) w[u] = *(const __attribute__((address_space(1))) int16_t *)(p + lofs2b);
 #endif
         }
     };
-    auto reduce = [&](const uint2 *E, const int *v) {
+    auto reduce = [&](const uint2 *E, const int *v, const int *w) {
 #pragma unroll
-        for (int u = 0; u < IL_B; ++u) {
-            const int c = il_e(E[u].x) + v[u];
+        for (int u = 0; u < NB; ++u) {
+            const int e = il_e(E[u].x), c = e + v[u];
             if (PMWIN) {
                 const int u1 = il_u1(E[u].x), u2 = il_dt(E[u].x) - 2 - u1;
                 // get_PMiloop: d > i, dp < l.  Branch-free (a select of constants): a branch here
                 // splits the loop body, and the compiler then sign-extends the next batch's loads
                 // in the latch, draining every load before the back-edge
                 b1 = imin(b1, c + (((u1 > as - 2) | (u2 > bs - 2)) ? INF : 0));
+                if (PAIR) b2 = imin(b2, e + w[u] + (((u1 > asb - 2) | (u2 > bsb - 2)) ? INF : 0));
             } else {
                 b1 = imin(b1, c);
+                if (PAIR) b2 = imin(b2, e + w[u]);
             }
         }
     };
@@ -760,31 +773,31 @@ __device__ __forceinline__ int il_scan(const DevTables &T, const uint2 *__restri
     // batch they replace was reduced, so the loop carries no register copies.  (With one buffer
     // and a copy per trip, the copy of a just-issued load made the compiler wait for every load
     // before the back-edge: one full memory latency per batch instead of overlapped batches.)
-    uint2 Ea[IL_B], Eb[IL_B];
-    int va[IL_B], vb[IL_B];
+    uint2 Ea[NB], Eb[NB];
+    int va[NB], vb[NB], wa[NB], wb[NB];
     fetch(0, Ea);
-    issue(Ea, va);
-    int e0 = IL_B;
+    issue(Ea, va, wa);
+    int e0 = NB;
 #pragma unroll 1
     while (true) {
         if (e0 >= cnt) {
-            reduce(Ea, va);
+            reduce(Ea, va, wa);
             break;
         }
         fetch(e0, Eb);
-        issue(Eb, vb);
-        reduce(Ea, va);
-        e0 += IL_B;
+        issue(Eb, vb, wb);
+        reduce(Ea, va, wa);
+        e0 += NB;
         if (e0 >= cnt) {
-            reduce(Eb, vb);
+            reduce(Eb, vb, wb);
             break;
         }
         fetch(e0, Ea);
-        issue(Ea, va);
-        reduce(Eb, vb);
-        e0 += IL_B;
+        issue(Ea, va, wa);
+        reduce(Eb, vb, wb);
+        e0 += NB;
     }
-    return b1;
+    return make_int2(b1, b2);
 }
 
 // The same minimum for a wave whose row has at most 32 cells: the wave is G groups of W lanes
@@ -896,7 +909,8 @@ __device__ __forceinline__ ILGroups il_groups(int nact, int lane) {
     return {64 / W, W, lane / W, lane & (W - 1)};
 }
 
-// one wave per work item (host-built list for level t: closing pairs that can pair, heaviest first)
+// one wave per work item: a closing pair that can pair and up to IL_CW (two 64-lane chunks) of
+// its cells (ccj_items.h, built by k_items in enumeration order)
 constexpr int IL_WPB = 4;  // waves (consecutive items) per k_iloop workgroup (1, 2, 8, 16 measured +3.6 ... +9 ms)
 __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long long first, int nitems, int G_SH, int rank) {
     const int n = T.n, rs = T.rs, m = n - t - 2;
@@ -912,12 +926,14 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
     const long long BIAS = (long long)(n + 64) * (n + 64);  // keeps B >= 0
     if (role == 0) {
         // PL: wave = (a, i, h-chunk), lanes h; closing pair (i, j)
-        const int a = f1, i = f2;
-        const ILGroups lg = il_groups(imin(64, m - i - zc * 64 + 1), lane);
+        const int a = f1, i = f2, len = m - i + 1, h0 = zc * IL_CW;
+        const ILGroups lg = il_groups(imin(64, len - h0), lane);
         const int G = lg.G, gq = lg.gq;
-        const int h = zc * 64 + lg.rl;
-        const bool act = h <= m - i;
+        const bool pair = len - h0 > 64;  // a second 64-cell chunk (wave-uniform)
+        const int h = h0 + lg.rl, hb = h + 64;
+        const bool act = h <= m - i, actb = pair && hb <= m - i;
         const unsigned lofs2 = 2u * (unsigned)(act ? h : m - i);  // idle lanes re-read a valid cell
+        const unsigned lofs2b = 2u * (unsigned)(actb ? hb : m - i);
         const size_t pidx = (size_t)a * rs + i;
         // PLx(t-dt, a-dt, h+dt-1-u1, i+1+u1) = lbx + (a-dt)M + x(m+dt) - x(x-1)/2 + dt-1-u1 + h, x = i+u1
         //   = [lbx + (a-dt)M + i*m + i*dt + dt-1] + [u1*m - x(x-1)/2 - u1] + u1*dt
@@ -932,26 +948,32 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         const int e0 = (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
         const uint2 *le = T.il + pidx * IL_CAP + e0;
         const int lc = (int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0;
-        const int b1 = G == 1 ? il_scan<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0)
-                              : il_scan_g<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl);
+        const int2 bm = G > 1  ? make_int2(il_scan_g<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl), INF)
+                        : pair ? il_scan<true, false, true>(T, le, lc, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
+                               : il_scan<true, false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
-        if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
+        if ((act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) || (actb && hb >= m)) {
             atomicOr(T.err, 128);
             return;
         }
 #endif
-        if (act && gq == 0) T.d4[Lt.lb + (long long)PL * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
+        int16_t *dl = T.d4 + Lt.lb + (long long)PL * Lt.C + a * Lt.M + i - 1;
+        if (act && gq == 0) dl[h * m - ((h * (h - 1)) >> 1)] = (int16_t)clamp_store(bm.x);
+        if (actb) dl[hb * m - ((hb * (hb - 1)) >> 1)] = (int16_t)clamp_store(bm.y);
     } else if (role == 1) {
         // PR: wave = (a, q, i-chunk), lanes i; closing pair (k, l), q = i+h-1 = k-a-3
         const int a = f1, q = f2;
         const int b = t - a;
         const int k = q + a + 3;
-        const ILGroups lg = il_groups(imin(64, q + 1 - zc * 64), lane);
+        const int i0 = zc * IL_CW;
+        const ILGroups lg = il_groups(imin(64, q + 1 - i0), lane);
         const int G = lg.G, gq = lg.gq;
-        const int i = zc * 64 + lg.rl + 1;
-        const bool act = i <= q + 1;
+        const bool pair = q + 1 - i0 > 64;
+        const int i = i0 + lg.rl + 1, ib = i + 64;
+        const bool act = i <= q + 1, actb = pair && ib <= q + 1;
         const unsigned lofs2 = 2u * (unsigned)((act ? i : q + 1) - 1);
-        const int h = q + 1 - i;
+        const unsigned lofs2b = 2u * (unsigned)((actb ? ib : q + 1) - 1);
+        const int h = q + 1 - i, hb = q + 1 - ib;
         const size_t pidx = (size_t)b * rs + k;
         // PRx(t-dt, a, h+1+u1, i) = lbx + C + a*M + qq(qq+1)/2 + i-1, qq = q+1+u1
         const int qq = q + 1 + lane;
@@ -963,15 +985,18 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         const int e0 = (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
         const uint2 *le = T.il + pidx * IL_CAP + e0;
         const int lc = (int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0;
-        const int b1 = G == 1 ? il_scan<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0)
-                              : il_scan_g<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl);
+        const int2 bm = G > 1  ? make_int2(il_scan_g<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl), INF)
+                        : pair ? il_scan<false, false, true>(T, le, lc, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
+                               : il_scan<false, false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
-        if (act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) {
+        if ((act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) || (actb && (hb < 0 || ib > m - hb))) {
             atomicOr(T.err, 128);
             return;
         }
 #endif
-        if (act && gq == 0) T.d4[Lt.lb + (long long)PR * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(b1);
+        int16_t *dr = T.d4 + Lt.lb + (long long)PR * Lt.C + a * Lt.M;
+        if (act && gq == 0) dr[h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(bm.x);
+        if (actb) dr[hb * m - ((hb * (hb - 1)) >> 1) + ib - 1] = (int16_t)clamp_store(bm.y);
     } else {
         // PM: wave = (h, j, a-chunk), lanes a; pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
         const int h = f1, j = f2;
@@ -979,13 +1004,15 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         // the rank's own a-blocks in the window (all of [alo, ahi] when unsharded): lanes = own index
         int o0, o1;
         pm_own_range(n, t, j, k, G_SH, rank, o0, o1);  // ccj_items.h
-        const ILGroups lg = il_groups(imin(64, o1 - o0 - zc * 64 + 1), lane);
+        const int oz = zc * IL_CW;
+        const ILGroups lg = il_groups(imin(64, o1 - o0 - oz + 1), lane);
         const int G = lg.G, gq = lg.gq;
-        const int o = o0 + zc * 64 + lg.rl;
-        const bool act = o <= o1;
-        const int a = shard_a(imin(o, o1), G_SH, rank);
+        const bool pair = o1 - o0 - oz + 1 > 64;
+        const int o = o0 + oz + lg.rl, ob = o + 64;
+        const bool act = o <= o1, actb = pair && ob <= o1;
+        const int a = shard_a(imin(o, o1), G_SH, rank), ab = shard_a(imin(ob, o1), G_SH, rank);
         const int as = a;
-        const unsigned lofs2 = 2u * (unsigned)as;
+        const unsigned lofs2 = 2u * (unsigned)as, lofs2b = 2u * (unsigned)ab;
         const size_t pidx = (size_t)g * rs + j;
         // PMx(t-dt, a-1-u1, h+dt, j-1-u1) = pmb + (h+dt)*n*(t+1-dt) + (j-2-u1)(t+1-dt) - 1-u1 + a
         //   = [pmb + (h+dt)*n*(t+1-dt) + (j-2)(t+1-dt) - 1] + [-u1(t+2)] + u1*dt
@@ -1002,15 +1029,19 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         const int cnt = (int)ld_const(T.ilmseg + pidx * IL_SEG + imin(t - 1, IL_SEG - 1));
         const int e0 = (int)ld_const(T.ilmseg + pidx * IL_SEG + 3);
         const uint2 *le = T.ilm + pidx * IL_CAP + e0;
-        const int b1 = G == 1 ? il_scan<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as)
-                              : il_scan_g<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl);
+        const int2 bm = G > 1  ? make_int2(il_scan_g<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl), INF)
+                        : pair ? il_scan<true, true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, lofs2b, ab, t - ab)
+                               : il_scan<true, true, false>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, 0u, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
-        if (act && (a < 0 || a > t || h < 0 || h >= m || (j - a) < 1 || (j - a) > m - h)) {
+        if ((act && (a < 0 || a > t || h < 0 || h >= m || (j - a) < 1 || (j - a) > m - h)) ||
+            (actb && (ab < 0 || ab > t || (j - ab) < 1 || (j - ab) > m - h))) {
             atomicOr(T.err, 128);
             return;
         }
 #endif
-        if (act && gq == 0) T.d4[Lt.lb + (long long)PM * Lt.C + a * Lt.M + h * m - ((h * (h - 1)) >> 1) + (j - a) - 1] = (int16_t)clamp_store(b1);
+        int16_t *dm = T.d4 + Lt.lb + (long long)PM * Lt.C + h * m - ((h * (h - 1)) >> 1) + j - 1;
+        if (act && gq == 0) dm[a * Lt.M - a] = (int16_t)clamp_store(bm.x);
+        if (actb) dm[ab * Lt.M - ab] = (int16_t)clamp_store(bm.y);
     }
 }
 
@@ -1289,8 +1320,14 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
+#ifdef CCJ_ABLATE_WHOT
+                // timing only: every W operand load on one cache-resident line (wrong results)
+                v.q[r] = WBW[(lane & 15) + 0 * (o + i - r)];
+                v.p[r] = WBW[(lane & 15) + 16 + 0 * (o + j - s)];
+#else
                 v.q[r] = WBW[o + i - r];
                 v.p[r] = WBW[o + j - s + 1];
+#endif
             }
             return v;
         };
@@ -1492,8 +1529,13 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
+#ifdef CCJ_ABLATE_WHOT
+                v.q[r] = WBW[(lane & 15) + 0 * (o + k - r)];
+                v.p[r] = WBW[(lane & 15) + 16 + 0 * (o + l - s)];
+#else
                 v.q[r] = WBW[o + k - r];
                 v.p[r] = WBW[o + l - s + 1];
+#endif
             }
             return v;
         };
