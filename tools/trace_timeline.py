@@ -34,7 +34,13 @@ def main(path, which=-1):
         if k != "k_level4d":
             continue
         lead = fold[x + 1] if x + 1 < len(fold) and fold[x + 1][1] == "k_level4d_lead" else None
-        il = fold[x - 1] if fold[x - 1][1] == "k_iloop" else None
+        il = None  # k_iloop(t): just before level t, or before k_diag2d(t-1) when the diag is joined to st_il
+        for y in range(x - 1, max(x - 4, -1), -1):
+            if fold[y][1] == "k_iloop":
+                il = fold[y]
+                break
+            if fold[y][1].startswith("k_level4d"):
+                break
         dg = None
         for y in range(x - 1, max(x - 4, -1), -1):
             if fold[y][1] == "k_diag2d":
