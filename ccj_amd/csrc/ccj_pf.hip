@@ -797,6 +797,9 @@ __global__ __launch_bounds__(256) void k_pf_canon(PfDev D, int x, const long lon
 }
 
 extern "C" int ccjk_pf_pterm(const PfDev *D, int s, void *stream) {
+#ifdef CCJ_ABLATE_PF_PTERM
+    return 0;  // timing only: this PF kernel skipped (wrong results)
+#endif
     const int ni = D->n - s;
     if (s < 3 || ni <= 0) return 0;
     hipLaunchKernelGGL(k_pf_pterm, dim3((unsigned)((ni + 63) / 64), (unsigned)(s - 2), (unsigned)((s - 2 + PT_DD - 1) / PT_DD)),
@@ -805,6 +808,9 @@ extern "C" int ccjk_pf_pterm(const PfDev *D, int s, void *stream) {
 }
 
 extern "C" int ccjk_pf_diag(const PfDev *D, int s, void *stream) {
+#ifdef CCJ_ABLATE_PF_DIAG
+    return 0;  // timing only: this PF kernel skipped (wrong results)
+#endif
     const int ni = D->n - s;
     if (ni <= 0) return 0;
     hipLaunchKernelGGL(k_pf_diag, dim3((unsigned)ni), dim3(64), 0, (hipStream_t)stream, *D, s);
@@ -820,6 +826,9 @@ extern "C" int ccjk_pf_level(const PfDev *D, const PfLvl *Lh, int t, void *strea
 }
 
 extern "C" int ccjk_pf_iloop(const PfDev *D, int t, long long first, int nitems, void *stream) {
+#ifdef CCJ_ABLATE_PF_ILOOP
+    return 0;  // timing only: this PF kernel skipped (wrong results)
+#endif
     if (nitems <= 0) return 0;
     hipLaunchKernelGGL(k_pf_iloop, dim3((unsigned)((nitems + 3) / 4)), dim3(256), 0, (hipStream_t)stream, *D, t, first,
                        nitems);
