@@ -208,14 +208,14 @@ def pf_cpu_baseline(n_sample=80, seed=3, cores=None):
                       f"dangles 2), one per host core; O(n^5), so its cells/s falls with n"}
 
 
-def pf_bench(a, rank, world, dist, barrier):
+def pf_bench(a, rank, world, dist, barrier, dev=0):
     """--pf: one step = ccj_pf() (the whole fill + W + energy) of the rank's sequence on a context
     created before the timed region.  Replicas only: the PF path has no sharded form, so --gpus N
     runs N independent folds (seed + rank), weak scaling."""
     from ccj_amd import W_final_pf
     seq = rseq(a.seed + rank, a.n)
     t_c = time.perf_counter()
-    pf = W_final_pf(seq, dangle=2, params=a.params)
+    pf = W_final_pf(seq, dangle=2, params=a.params, device=dev)
     create_ms = (time.perf_counter() - t_c) * 1e3
     for _ in range(a.warmup):
         pf.ccj_pf()
@@ -301,6 +301,19 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def rank_device(local):
+    """The GPU of this rank: LOCAL_RANK when every GPU of the node is visible to each rank (the
+    driver's torch.distributed.run launch), else LOCAL_RANK modulo the visible devices (one GPU per
+    rank through HIP_VISIBLE_DEVICES, or a rehearsal of N ranks on a 1-GPU box).  Counting devices
+    does not initialise the GPU on this image."""
+    try:
+        import torch
+        n = torch.cuda.device_count()
+    except Exception:
+        n = 0
+    return local % n if n > 0 else local
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     a = parse_args(argv)
@@ -314,6 +327,7 @@ def main(argv=None):
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = rank_device(local) if not a.dry_run else local
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -352,7 +366,7 @@ def main(argv=None):
         return
 
     if a.pf:
-        pf_bench(a, rank, world, dist, barrier)
+        pf_bench(a, rank, world, dist, barrier, dev)
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -369,9 +383,9 @@ def main(argv=None):
     t_c = time.perf_counter()
     if shard:
         cid = share_comm_id(rank, dist, comm_unique_id)
-        ctxs = [W_final(seq_at(0), 2, params=a.params, device=local, shard_world=world, shard_rank=rank, comm_id=cid)]
+        ctxs = [W_final(seq_at(0), 2, params=a.params, device=dev, shard_world=world, shard_rank=rank, comm_id=cid)]
     else:
-        ctxs = [W_final(seq_at(0), 2, params=a.params, device=local) for _ in range(inflight)]
+        ctxs = [W_final(seq_at(0), 2, params=a.params, device=dev) for _ in range(inflight)]
     create_ms = (time.perf_counter() - t_c) * 1e3 / len(ctxs)
 
     def run_steps(nsteps, acc):
