@@ -306,6 +306,8 @@ def rank_device(local):
     driver's torch.distributed.run launch), else LOCAL_RANK modulo the visible devices (one GPU per
     rank through HIP_VISIBLE_DEVICES, or a rehearsal of N ranks on a 1-GPU box).  Counting devices
     does not initialise the GPU on this image."""
+    if local == 0:
+        return 0  # (no torch import on the single-rank path)
     try:
         import torch
         n = torch.cuda.device_count()
