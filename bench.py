@@ -301,6 +301,20 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def find_traffic(n, seed, params):
+    """The committed rocprofv3 FETCH_SIZE/WRITE_SIZE summary (tools/make_profiles.py) of this exact
+    workload: profiles/traffic*.json whose "config" is (n, seed, params); the untagged
+    profiles/traffic.json of rounds 1-3 is the headline n=200 seed 5 Turner04 fold."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic*.json"))):
+        with open(path) as f:
+            tj = json.load(f)
+        cfg = tj.get("config", {"n": 200, "seed": 5, "params": "Turner04"})
+        if (cfg.get("n"), cfg.get("seed"), cfg.get("params")) == (n, seed, params) and not tj.get("pf"):
+            return tj, os.path.basename(path)
+    return None, None
+
+
 def rank_device(local):
     """The GPU of this rank: LOCAL_RANK when every GPU of the node is visible to each rank (the
     driver's torch.distributed.run launch), else LOCAL_RANK modulo the visible devices (one GPU per
@@ -313,7 +327,12 @@ def rank_device(local):
         n = torch.cuda.device_count()
     except Exception:
         n = 0
-    return local % n if n > 0 else local
+    if n <= 0:
+        # no torch count: the visible-device list, else device 0 (never an index past what the
+        # rank can see, e.g. LOCAL_RANK 3 with one GPU per rank)
+        vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES") or ""
+        n = len([v for v in vis.split(",") if v.strip()])
+    return local % n if n > 0 else 0
 
 
 def main(argv=None):
@@ -341,6 +360,10 @@ def main(argv=None):
 
     shard = a.shard and world > 1
     cells = num_cells(a.n)
+    rank_devs = [dev]
+    if dist is not None:  # the rank -> GPU mapping goes on the line, so a mis-mapped rank is visible
+        rank_devs = [None] * world
+        dist.all_gather_object(rank_devs, dev)
 
     def seq_at(step):
         return rseq(a.seed if shard else rank_seed(a.seed, rank, world, step, a.distinct), a.n)
@@ -450,14 +473,12 @@ def main(argv=None):
     # (tools/gpu_profile.sh -> tools/make_profiles.py -> profiles/traffic.json); null when no
     # profile of this configuration is committed (it is not measured inside this run)
     traffic = traffic_src = None
-    tp = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tp) and a.n == 200 and a.seed == 5 and a.params == "Turner04" and world == 1:
-        with open(tp) as f:
-            tj = json.load(f)
+    tj, tname = find_traffic(a.n, a.seed, a.params) if world == 1 or not shard else (None, None)
+    if tj:
         tk = tj["kernels"].get("k_level4d_level")
         if tk:
             traffic = tk["hbm_bytes_per_launch"]
-            traffic_src = "profiles/traffic.json (" + tj.get("source", "rocprofv3 PMC passes") + ")"
+            traffic_src = f"profiles/{tname} (" + tj.get("source", "rocprofv3 PMC passes") + ")"
 
     if rank != 0:
         if dist is not None:
@@ -477,6 +498,7 @@ def main(argv=None):
         "value": value,
         "unit": "DP-cells/s",
         "n_gpus": world,
+        "rank_devices": rank_devs,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": sec_per_step * 1e3,

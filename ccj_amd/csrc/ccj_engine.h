@@ -80,9 +80,9 @@ enum RecType { RA = 0, RK = 1, RL = 2, NREC = 3 };
 #endif
 constexpr int SHARE_R = CCJ_SHARE_R;
 constexpr int SHARE_NACC = 4;
-// ring slots (one per target level): SHARE_R + 1, since in the prepass scheme the leader launch of
-// level t+1 (writing levels t+1 .. t+SHARE_R) runs while level t's plain launch reads slot t
-constexpr int SHARE_SLOTS = SHARE_R + 1;
+// ring slots (one per target level): the leader launch of level t reads slot t (its follower
+// sides) and writes slots t+1 .. t+SHARE_R-1, after level t's plain launch on the same stream
+constexpr int SHARE_SLOTS = SHARE_R;
 enum AccRec { AI = 0, AJ = 1, AK = 2, AL = 3 };
 
 // Band sharding: a-block a of every level belongs to rank (a / SHARD_GRP) % world,
@@ -165,7 +165,6 @@ struct DevTables {
     // slots x SHARE_NACC x accC
     int split_target;              // k_level4d: narrow levels split loops so ~this many waves run (0: never)
     int g_lo, g_hi;
-    int prepass;                   // 1: leader launch of level t runs beside level t-1, scans s >= 2
     // k_level4d_lead walks only the long-scan a-blocks of a sharing level, longest scan first:
     // rank r's list lord[lord_off[t*G+r] .. lord_off[t*G+r+1]) (device), lord_off_h = the same
     // offsets on the host

@@ -66,6 +66,7 @@ struct ccj_group {
     int arrived = 0;
     long gen = 0;
     bool broken = false;
+    int busy = 0;  // members between taking the peers' send pointers and finishing their copies
     // false when a member gave up (error or 120 s without the others)
     bool barrier() {
         std::unique_lock<std::mutex> lk(mu);
@@ -162,9 +163,6 @@ struct ccj_ctx {
     std::vector<unsigned long long> h_pk;
     int8_t *d_vt = nullptr;
     hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr, st_il = nullptr, st_d = nullptr;
-    hipStream_t st_pre = nullptr;        // prepass leader launches (level t beside level t-1)
-    std::vector<hipEvent_t> pre_done;    // prepass launch of level t finished
-    bool prepass = false;                // CCJ_PREPASS=1: leader launch of level t beside level t-1 (measured +0.5 ms at n=200)
     bool join_diag = true;               // k_diag2d(t-1) after k_iloop(t) on st_il (one cross-stream wait per level)
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<hipEvent_t> pp_done; // band-sharded: this rank's P-term push of span sigma done (before the exchange)
@@ -1427,15 +1425,32 @@ static int local_allgather(ccj_ctx *c, size_t slice) {
     ccj_group *g = c->lgroup;
     HIPCHK(c, hipStreamSynchronize(c->st));  // own slice packed
     if (!g->barrier()) return set_err(c, CCJ_E_STATE, "local exchange: a group member failed");
+    // take the peers' send buffers under the lock and hold the group busy until the copies are
+    // done: ccj_destroy of a peer waits for busy == 0 before it frees anything
+    std::vector<const int16_t *> src(g->world, nullptr);
     {
         std::lock_guard<std::mutex> lk(g->mu);
-        for (int r = 0; r < g->world; ++r)
-            if (!g->members[r]) return set_err(c, CCJ_E_STATE, "local exchange: rank %d has no context", r);
+        for (int r = 0; r < g->world; ++r) {
+            if (!g->members[r]) {
+                g->broken = true;  // every other member's next barrier fails instead of waiting
+                g->cv.notify_all();
+                return set_err(c, CCJ_E_STATE, "local exchange: rank %d has no context", r);
+            }
+            src[r] = g->members[r]->d_send;
+        }
+        ++g->busy;
     }
-    for (int r = 0; r < g->world; ++r)
-        HIPCHK(c, hipMemcpyAsync(c->d_recv + (size_t)r * slice, g->members[r]->d_send, slice * sizeof(int16_t),
-                                 hipMemcpyDeviceToDevice, c->st));
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    hipError_t e = hipSuccess;
+    for (int r = 0; r < g->world && e == hipSuccess; ++r)
+        e = hipMemcpyAsync(c->d_recv + (size_t)r * slice, src[r], slice * sizeof(int16_t), hipMemcpyDeviceToDevice, c->st);
+    const hipError_t e2 = hipStreamSynchronize(c->st);
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        --g->busy;
+        g->cv.notify_all();
+    }
+    HIPCHK(c, e);
+    HIPCHK(c, e2);
     if (!g->barrier()) return set_err(c, CCJ_E_STATE, "local exchange: a group member failed");
     return CCJ_OK;
 }
@@ -1607,12 +1622,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         if (opts && opts->split_target) c->split_target = opts->split_target < 0 ? 0 : opts->split_target;
         const char *lt = getenv("CCJ_LEVEL_TIMING");
         if (lt) c->level_timing = std::max(0, std::min(2, atoi(lt)));
-        const char *pp = getenv("CCJ_PREPASS");
-        c->prepass = pp && atoi(pp) != 0;
         // k_diag2d(t-1) behind k_iloop(t) on one side stream, so each level waits on one event
-        // (fill -0.25 ms at n=200 in 3/3 alternating runs); not with the prepass scheme, which waits
-        // on dg_done[t-1] before it would be recorded
-        c->join_diag = !c->prepass;
+        // (fill -0.25 ms at n=200 in 3/3 alternating runs)
+        c->join_diag = true;
         const char *g = getenv("CCJ_SHARE_SPLITS");
         c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
     }
@@ -1671,14 +1683,11 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_p, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_il, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_d, hipStreamNonBlocking));
-    HIPCHK(cp, hipStreamCreateWithFlags(&c->st_pre, hipStreamNonBlocking));
     // The cross-stream events only order work on this device, so they are recorded without the
     // default system-scope fence (hipEventDisableSystemFence: fill -0.65 ms at n=200).
     // ev_start / ev_end, which the host waits on, keep it.
     constexpr unsigned fence_fl = (unsigned)hipEventDisableSystemFence;
     const unsigned sync_fl = hipEventDisableTiming | fence_fl;
-    c->pre_done.resize(n + 1);
-    for (auto &e : c->pre_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
     c->il_done.resize(n + 1);
     for (auto &e : c->il_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
     c->dg_done.resize(n + 1);
@@ -1906,7 +1915,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.lord_off = c->d_lord_off;
     T.lord_off_h = c->lord_off.empty() ? nullptr : c->lord_off.data();
     T.accC = accC;
-    T.prepass = c->prepass && g_hi > g_lo;
     {
         const int G = c->world;
         HIPCHK(cp, hipMalloc(&c->d_icount, (size_t)n * G * sizeof(long long)));
@@ -2009,21 +2017,6 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     HIPCHK(c, hipStreamWaitEvent(c->st_d, c->ev_pre, 0));
     HIPCHK(c, hipStreamWaitEvent(c->st_il, c->ev_pre, 0));
     HIPCHK(c, hipStreamWaitEvent(c->st_p, c->ev_pre, 0));
-    HIPCHK(c, hipStreamWaitEvent(c->st_pre, c->ev_pre, 0));
-    // prepass leader launch of level t: needs 4-D levels <= t-2 and 2-D spans <= t-1;
-    // enqueued after level t-2, beside level t-1; level t's plain launch waits for it
-    auto enqueue_pre = [&](int t) -> int {
-        if (!c->T.prepass || t < c->T.g_lo || t >= c->T.g_hi || t >= c->nlev) return CCJ_OK;
-        if (t >= 2) HIPCHK(c, hipStreamWaitEvent(c->st_pre, c->lev_done[t - 2], 0));
-        if (t >= 1) HIPCHK(c, hipStreamWaitEvent(c->st_pre, c->dg_done[t - 1], 0));
-        for (int r = 0; r < c->world; ++r) {
-            if (!c->simulate && r != c->rank) continue;
-            HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, t, c->world, r, c->st_pre));
-        }
-        HIPCHK(c, hipEventRecord(c->pre_done[t], c->st_pre));
-        return CCJ_OK;
-    };
-    if (const int rc = enqueue_pre(0)) return rc;
     for (int s = 0; s < n; ++s) {
         hipEvent_t *ev = &c->tev[7 * (size_t)s];
         // timing markers (ev[0..6]) only when per-kernel timing is on
@@ -2046,7 +2039,6 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
             }
             if (const int rc = enqueue_diag(s, c->join_diag ? c->st_il : c->st_d)) return rc;
         }
-        if (const int rc = enqueue_pre(s + 1)) return rc;  // its inputs: lev_done[s-1], dg_done[s]
         if (s < c->nlev) {
             if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 3], 0));
             HIPCHK(c, trec(2, c->st_il));
@@ -2064,7 +2056,6 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
             HIPCHK(c, hipEventRecord(c->il_done[s], c->st_il));
             HIPCHK(c, hipStreamWaitEvent(st, c->il_done[s], 0));
             if (s >= 1 && !c->join_diag) HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s - 1], 0));
-            if (c->T.prepass && s >= c->T.g_lo && s < c->T.g_hi) HIPCHK(c, hipStreamWaitEvent(st, c->pre_done[s], 0));
             HIPCHK(c, trec(4, st));
             // the level: its plain launch, then (sharing levels) the leaders on the same stream, no
             // cross-stream hop between the two launches or between levels
@@ -2072,11 +2063,9 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                 if (!c->simulate && r != c->rank) continue;
                 HIPCHK(c, (hipError_t)ccjk_level4d(&c->T, s, G, r, 1, st));
             }
-            if (!c->T.prepass) {
-                for (int r = 0; r < G; ++r) {
-                    if (!c->simulate && r != c->rank) continue;
-                    HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, G, r, st));
-                }
+            for (int r = 0; r < G; ++r) {
+                if (!c->simulate && r != c->rank) continue;
+                HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, G, r, st));
             }
             if (G > 1 && !c->simulate) {
                 // band-sharded exchange: this rank's cells of the level, all 22
@@ -2745,8 +2734,12 @@ extern "C" const char *ccj_last_error(const ccj_ctx *c) { return c ? c->err.c_st
 extern "C" void ccj_destroy(ccj_ctx *c) {
     if (!c) return;
     if (c->lgroup) {  // leave the in-process group: no member may copy from this context's buffers
-        std::lock_guard<std::mutex> lk(c->lgroup->mu);
-        if (c->lgroup->members[c->rank] == c) c->lgroup->members[c->rank] = nullptr;
+        ccj_group *g = c->lgroup;
+        std::unique_lock<std::mutex> lk(g->mu);
+        if (g->members[c->rank] == c) g->members[c->rank] = nullptr;
+        g->broken = true;  // the exchange cannot complete without this rank
+        g->cv.notify_all();
+        g->cv.wait(lk, [&] { return g->busy == 0; });  // peers still copying from d_send
         c->lgroup = nullptr;
     }
     hipSetDevice(c->device);
@@ -2755,7 +2748,6 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->st_p) hipStreamSynchronize(c->st_p);
     if (c->st_il) hipStreamSynchronize(c->st_il);
     if (c->st_d) hipStreamSynchronize(c->st_d);
-    if (c->st_pre) hipStreamSynchronize(c->st_pre);
     hipFree(c->d4);
     hipFree(c->d_ie);
     hipFree(c->d_est);
@@ -2813,8 +2805,6 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->st_il) hipStreamDestroy(c->st_il);
     if (c->st_d) hipStreamDestroy(c->st_d);
-    if (c->st_pre) hipStreamDestroy(c->st_pre);
-    for (auto e : c->pre_done) hipEventDestroy(e);
     for (auto e : c->il_done) hipEventDestroy(e);
     for (auto e : c->dg_done) hipEventDestroy(e);
     for (auto e : c->tev) hipEventDestroy(e);

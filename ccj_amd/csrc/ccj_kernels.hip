@@ -1051,8 +1051,7 @@ __device__ __forceinline__ unsigned pk16(int lo, int hi) { return (unsigned)(uin
 __device__ __forceinline__ int lo16(unsigned w) { return (int)(int16_t)(w & 0xffffu); }
 __device__ __forceinline__ int hi16(unsigned w) { return (int)w >> 16; }
 
-// ints per lane a leader's split wave hands to part 0: the slices r = 0..R-1 of one side (the
-// followers' r >= 1 only, unless the prepass scheme hands r = 0 over too)
+// ints per lane a leader's split wave hands to part 0: the followers' slices r = 1..R-1 of one side
 constexpr int LEAD_RED = 15 * SHARE_R;
 
 // split-point sharing (ccj_engine.h): the SHARE_R W values of one split step, one per follower
@@ -1226,24 +1225,13 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     // On sharing levels every wave with a long scan (a leader, or a full scan on either side) runs
     // in its own launch (k_level4d_lead: more registers, scans split over several waves); the plain
     // kernel keeps the cells that only follow (short scans, full occupancy).
-    // Prepass scheme (T.prepass): the leader launch of level t runs one level EARLY,
-    // beside level t-1, and scans only the split points s >= 2 (source levels <= t-2), handing
-    // every result — the cell's own (r = 0) and its followers' — over through the partial-record
-    // ring; the plain launch of level t then finishes EVERY cell of the level: split step 1 (level
-    // t-1) for the long-scan sides, steps 1..a%R+1 for the followers (their leader skipped its own
-    // step 1, the followers' step a%R+1), plus the ring records.  Level t's critical path is then
-    // only short scans.
-    const bool prem = T.prepass && grp;
-    if (grp && (prem ? (LEAD && arole == 2 && brole == 2) : (LEAD != (arole != 2 || brole != 2)))) return;
-    // last split step this cell scans itself (in this launch)
-    const int a_stop = prem ? (LEAD ? (arole == 2 ? 0 : a) : (arole == 2 ? imin(ra + 1, a) : imin(1, a)))
-                            : (arole == 2 ? ra : a);
-    const int b_stop = prem ? (LEAD ? (brole == 2 ? 0 : b) : (brole == 2 ? imin(rb + 1, b) : imin(1, b)))
-                            : (brole == 2 ? rb : b);
-    const int s_first = (LEAD && prem) ? 2 : 1;  // first split step this cell scans itself
+    if (grp && LEAD != (arole != 2 || brole != 2)) return;
+    // last split step this cell scans itself
+    const int a_stop = arole == 2 ? ra : a;
+    const int b_stop = brole == 2 ? rb : b;
 
     // ---- fused a-loop: split point d inside [i, j] ----
-    const int seed = (LEAD && prem) ? INF : INTERN_INF + bp;  // A-Q3 seeds (the finishing launch adds them)
+    const int seed = INTERN_INF + bp;  // A-Q3 seeds
     int pLm00 = seed, pLm01 = INF, pLm10 = INF, pMm00 = seed, pMm10 = INF;
     int pOm00 = seed, pOm10 = INF;
     int fL1 = INF, fL2 = INF, fM = INF, fO1 = INF, pK1 = INF;
@@ -1357,10 +1345,10 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 J[6] = imin(J[6], Kj + wpj + mask);      // PK        :184-187
             }
         };
-        if (s_first + part <= a) pipe_scan_lead<LA>(s_first + part, split, a, a, ld, st);
-        // slices handed over through the ring: the followers' (r >= 1), and in the prepass scheme
-        // the cell's own (r = 0) too; otherwise r = 0 stays in this wave's accumulators
-        const int r0 = prem ? 0 : 1;
+        if (1 + part <= a) pipe_scan_lead<LA>(1 + part, split, a, a, ld, st);
+        // slices handed over through the ring: the followers' (r >= 1); r = 0 stays in this wave's
+        // accumulators
+        constexpr int r0 = 1;
         if (split > 1) {  // the split waves' slices meet in part 0
             int *slot = red + (wib / split) * (split - 1) * LEAD_RED * 64 + lane;
             if (part > 0) {
@@ -1386,7 +1374,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                         }
             __syncthreads();
         }
-        if (!prem) {
+        {
         pLm00 = imin(pLm00, imin(AI_[0][0], AJ_[0][0]));
         pLm10 = imin(AI_[0][1], AJ_[0][3]);
         pMm10 = AI_[0][2];
@@ -1426,13 +1414,11 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #endif
     if (arole == 1 && LEAD) {
         lead_a();
-    } else if (s_first + part <= a_stop) {
-        pipe_scan<AV>(s_first + part, split, a_stop, a, load_a, step_a);
+    } else if (1 + part <= a_stop) {
+        pipe_scan<AV>(1 + part, split, a_stop, a, load_a, step_a);
     }
-    // the ring record of the a-loop: a follower's leader partial (split points a%R+1 .. a, or
-    // a%R+2 .. a in the prepass scheme), and in the prepass scheme the own s >= 2 partial of a
-    // long-scan side
-    if (prem ? !LEAD : arole == 2) {
+    // the ring record of the a-loop: a follower's leader partial (split points a%R+1 .. a)
+    if (arole == 2) {
         const uint4 *ring = T.acc + (long long)((t % SHARE_SLOTS) * SHARE_NACC) * T.accC;
         const unsigned idx = (unsigned)(a * Mt) + L0;
         CHKA(idx);
@@ -1566,8 +1552,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 Q[8] = imin(Q[8], fOl + wpl_ + mask);       // PfromO    :429-431
             }
         };
-        if (s_first + part <= b) pipe_scan_lead<LB>(s_first + part, split, b, b, ld, st);
-        const int r0 = prem ? 0 : 1;
+        if (1 + part <= b) pipe_scan_lead<LB>(1 + part, split, b, b, ld, st);
+        constexpr int r0 = 1;
         if (split > 1) {
             int *slot = red + (wib / split) * (split - 1) * LEAD_RED * 64 + lane;
             if (part > 0) {
@@ -1595,7 +1581,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                     }
             __syncthreads();
         }
-        if (!prem) {
+        {
         pRm00 = imin(pRm00, imin(AK_[0][0], AL_[0][0]));
         pRm10 = AK_[0][1];
         pMm00 = imin(pMm00, AK_[0][2]);
@@ -1639,10 +1625,10 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #endif
     if (brole == 1 && LEAD) {
         lead_b();
-    } else if (s_first + part <= b_stop) {
-        pipe_scan<BV>(s_first + part, split, b_stop, b, load_b, step_b);
+    } else if (1 + part <= b_stop) {
+        pipe_scan<BV>(1 + part, split, b_stop, b, load_b, step_b);
     }
-    if (prem ? !LEAD : brole == 2) {  // the b-loop's ring record (as for the a-loop)
+    if (brole == 2) {  // the b-loop's ring record (as for the a-loop)
         const uint4 *ring = T.acc + (long long)((t % SHARE_SLOTS) * SHARE_NACC) * T.accC;
         const unsigned idx = (unsigned)(a * Mt) + L0;
         CHKA(idx);
@@ -1683,27 +1669,6 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         pRm00 = acc[12]; pRm01 = acc[13]; pRm10 = acc[14]; pMm01 = acc[15]; pOm01 = acc[16]; fR1 = acc[17];
         fR2 = acc[18]; fMp = acc[19]; fO2 = acc[20]; pK2 = acc[21];
         if (!lane_ok) return;
-    }
-    if (LEAD && prem) {
-        // prepass launch: the own s >= 2 partials of the full-scan sides go to the ring (the
-        // leaders' sides did inside lead_a / lead_b); the plain launch of level t finishes the cell
-        if (!lane_ok || part != 0) return;
-        uint4 *ring = T.acc + (long long)((t % SHARE_SLOTS) * SHARE_NACC) * T.accC;
-        const unsigned idx = (unsigned)(a * Mt) + L0;
-        CHKA(idx);
-        if (arole == 0) {
-            const int fi[7] = {pLm00, pLm10, pMm10, pOm00, pOm10, fL1, fO1};
-            const int fj[7] = {pLm00, pLm01, pMm00, pLm10, fL2, fM, pK1};
-            ring[(long long)AI * T.accC + idx] = pack_acc(fi, 7);
-            ring[(long long)AJ * T.accC + idx] = pack_acc(fj, 7);
-        }
-        if (brole == 0) {
-            const int fk[7] = {pRm00, pRm10, pMm00, fR1, fMp, pK2, fO2};
-            const int fl[8] = {pRm00, pRm01, pMm01, pOm00, pOm01, pMm10, pOm10, fR2};
-            ring[(long long)AK * T.accC + idx] = pack_acc(fk, 7);
-            ring[(long long)AL * T.accC + idx] = pack_acc(fl, 8);
-        }
-        return;
     }
     // ---- single-step seeds (:519, :533, :566, :580), level t-1
     int vPRm01 = pRm01, vPRm10 = pRm10, vPMm01 = pMm01, vPMm10 = pMm10;

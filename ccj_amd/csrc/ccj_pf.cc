@@ -25,9 +25,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <functional>
+#include <new>
 #include <string>
 #include <thread>
 #include <utility>
@@ -434,6 +436,26 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     c->pen = prob->pen ? *prob->pen : defp;
     c->rs = n + 2;
     const int rs = c->rs;
+    {
+        // Size check before any table is built: the two get_e_intP window tables (host, then
+        // device) and the int32 4-D store (21 x C(n+1,4) cells).  Past what the host or the GPU can
+        // hold, fail with CCJ_E_OOM up front instead of after seconds of table building.
+        const double plane_b = (double)(n + 1) * rs, cells = (double)(n + 1) * n * (n - 1) * (n - 2) / 24.0;
+        const double ie_b = 2.0 * PF_IEW * PF_IEW * plane_b * sizeof(double);
+        const double dev_b = ie_b + 21.0 * cells * sizeof(int) * 1.5;  // + copies, slack
+        const double host_b = ie_b;
+        size_t dfree = 0, dtotal = 0;
+        char msg[200];
+        if (hipSetDevice(device) == hipSuccess && hipMemGetInfo(&dfree, &dtotal) == hipSuccess && dev_b > (double)dfree) {
+            snprintf(msg, sizeof msg, "n=%d needs ~%.1f GB of device memory, %.1f GB free", n, dev_b / 1e9, dfree / 1e9);
+            return pf_err(c, CCJ_E_OOM, msg);
+        }
+        const long pages = sysconf(_SC_AVPHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+        if (pages > 0 && psz > 0 && host_b > (double)pages * (double)psz) {
+            snprintf(msg, sizeof msg, "n=%d needs ~%.1f GB of host memory for the interior-loop tables", n, host_b / 1e9);
+            return pf_err(c, CCJ_E_OOM, msg);
+        }
+    }
     // make_pair_matrix / encode_sequence (pair_mat.h:81-183)
     const int base_rtype[8] = {0, 2, 1, 4, 3, 6, 5, 7};
     memcpy(c->rtype, base_rtype, sizeof base_rtype);
@@ -743,9 +765,15 @@ int fill_impl(ccj_pf_ctx *c) {
     PFCHK(c, hipStreamSynchronize(c->st));
     // the exact int64 P sums equal the reference's serial double sums only while every partial sum
     // is an exactly representable integer: guaranteed by sum |term| < 2^53 (part_func.cc:383-393)
+    // CCJ_PF_RANGE_LOG2 lowers the 2^53 bound (tests only: reaches this exit with short sequences)
+    unsigned long long range_lim = 1ull << 53;
+    if (const char *e = getenv("CCJ_PF_RANGE_LOG2")) {
+        const int l2 = atoi(e);
+        if (l2 >= 1 && l2 <= 53) range_lim = 1ull << l2;
+    }
     for (int w = 0; w < n; ++w)
         for (int p = 1; p + w <= n; ++p)
-            if (pabs[(size_t)w * c->rs + p] >= (1ull << 53)) {
+            if (pabs[(size_t)w * c->rs + p] >= range_lim) {
                 char msg[160];
                 snprintf(msg, sizeof msg, "P(%d,%d): sum of |terms| >= 2^53, the reference's double sum may round", p, p + w);
                 return pf_err(c, CCJ_E_PF_RANGE, msg);
@@ -1046,7 +1074,12 @@ int ccj_pf_create(const ccj_problem *prob, const ccj_pf_raw *raw, int device, cc
     ccj_pf_ctx *c = new (std::nothrow) ccj_pf_ctx();
     if (!c) return CCJ_E_OOM;
     initstate_r(1, c->rnd_state, sizeof c->rnd_state, &c->rnd);
-    const int rc = create_impl(prob, raw, device, c);
+    int rc;
+    try {
+        rc = create_impl(prob, raw, device, c);
+    } catch (const std::bad_alloc &) {  // host tables: no exception crosses the C ABI
+        rc = pf_err(c, CCJ_E_OOM, "host allocation failed");
+    }
     if (rc != CCJ_OK) {
         fprintf(stderr, "ccj_pf_create: %s\n", c->msg.c_str());
         free_dev(c);

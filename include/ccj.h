@@ -8,7 +8,9 @@
  * and afterwards W (W_final.cc:68-79), backtrack (W_final.cc:84-104, pseudo_loop.cc:861-2820)
  * and bracket emission (W_final.cc:764-819).  This ABI replaces that whole body: one
  * ccj_fill() runs every recurrence on the GPU; ccj_result() runs W + backtrack + emission on
- * the host against a host mirror of the matrices, with the reference's getter semantics.
+ * the GPU by default (k_compute_W / k_backtrack over the device matrices), or, with
+ * ccj_options.host_traceback = 1, on the host against a host mirror; the getters keep the
+ * reference's semantics either way.
  *
  * Plain C types only (no torch / HIP types).  All positions are 1-based like the reference.
  * Not re-entrant per context; independent contexts may run on separate host threads.
@@ -103,8 +105,9 @@ int  ccj_create(const ccj_problem *prob, const ccj_options *opts, ccj_ctx **out)
  * while a fold is in flight. */
 int  ccj_reset(ccj_ctx *ctx, const char *seq);
 
-/* Run the whole DP fill on the GPU (replaces W_final.cc:60-67), then make the host mirror
- * valid (ccj_sync_host is implied). */
+/* Run the whole DP fill on the GPU (replaces W_final.cc:60-67).  With host_traceback = 1 it
+ * also makes the host mirror valid (ccj_sync_host is implied); by default the matrices stay on
+ * the device and the getters copy them on first use. */
 int  ccj_fill(ccj_ctx *ctx);
 
 /* Device-only fill, no host mirror (for timing the kernels alone).  CCJ_E_STATE while a fold
@@ -113,7 +116,9 @@ int  ccj_fill_device(ccj_ctx *ctx);
 /* Copy the device matrices to the host mirror. */
 int  ccj_sync_host(ccj_ctx *ctx);
 
-/* W (W_final.cc:68-79), backtrack and bracket emission on the host mirror.
+/* W (W_final.cc:68-79), backtrack and bracket emission: on the GPU by default (k_compute_W,
+ * k_backtrack; results copied back), on the host mirror with host_traceback = 1.  Both are
+ * bit-identical to the reference.
  * structure: buffer of n+1 chars (NUL-terminated on return); *energy_kcal = W[n]/100.0;
  * stdout_msgs: optional buffer receiving the reference's stdout side messages
  * ("Should not be here!\n" lines, W_final.cc:715), NUL-terminated, may be NULL. */

@@ -8,6 +8,7 @@ The bar is bit-identity: the fill evaluates every sum in the reference's order w
 contraction.
 """
 import json
+import math
 import os
 
 import pytest
@@ -77,8 +78,34 @@ def test_pf_past_295_checks_exactness():
     import ccj_amd
     pf = ccj_amd.W_final_pf("A" * 300, params="DirksPierce09")
     try:
-        assert pf.ccj_pf() == pytest.approx(0.0, abs=1e-9) or True
-        assert all(v == 1.0 for v in pf.W()[:5])
+        e = pf.ccj_pf()
+        # Z = W[n] = 1 and pf_scale = 1: -log(1) * kT / 1000 = -0.0, as the reference prints for
+        # poly-A ("ENERGY -0", oracle/_ref/pf_driver on A*30)
+        assert e == 0.0 and math.copysign(1.0, e) == -1.0
+        assert all(v == 1.0 for v in pf.W())
+    finally:
+        pf.close()
+
+
+@pytest.mark.gpu
+def test_pf_range_exit(monkeypatch):
+    """The exactness guard itself: with the bound lowered from 2^53 to 2^10 (CCJ_PF_RANGE_LOG2, a
+    test hook), a sequence whose P sums carry large terms fails with CCJ_E_PF_RANGE (10) naming the
+    interval, instead of returning a result."""
+    import ccj_amd
+    c = next(c for c in CASES if c["name"] == "big60_default")
+    monkeypatch.setenv("CCJ_PF_RANGE_LOG2", "10")
+    pf = ccj_amd.W_final_pf(c["seq"], params=c["params"])
+    try:
+        with pytest.raises(ccj_amd.CCJError) as ei:
+            pf.ccj_pf()
+        assert ei.value.code == 10, ei.value  # CCJ_E_PF_RANGE
+    finally:
+        pf.close()
+    monkeypatch.delenv("CCJ_PF_RANGE_LOG2")
+    pf = ccj_amd.W_final_pf(c["seq"], params=c["params"])
+    try:
+        assert repr(pf.ccj_pf()) == repr(float(c["energy"]))
     finally:
         pf.close()
 

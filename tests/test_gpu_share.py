@@ -82,23 +82,3 @@ def test_sharing_n400_same_result():
             wf.close()
     assert out[0] == out[1]
     assert len(out[0][1]) == n and out[0][0] == out[0][2][n] / 100.0
-
-
-@pytest.mark.parametrize("case", CASES[::2], ids=lambda c: f"n{len(c['seq'])}-{c['params']}")
-@pytest.mark.parametrize("kw", [{"split_target": -1}, {}, {"shard_world": 3, "shard_simulate": True}],
-                         ids=["all-levels", "default", "sharded3"])
-def test_prepass_scheme_matches_reference(case, kw, monkeypatch):
-    """CCJ_PREPASS=1: the leader launch of level t runs beside level t-1 over the
-    split points s >= 2 and hands the cell's own partial over through the ring too; the plain launch
-    finishes every cell.  Off by default (measured slower), kept bit-identical."""
-    monkeypatch.setenv("CCJ_PREPASS", "1")
-    got = _hashes(case["seq"], case["params"], case["dangles"], case["noGU"], **kw)
-    bad = [k for k in case["hashes"] if got[k] != case["hashes"][k]]
-    assert not bad, bad
-
-
-def test_prepass_scheme_at_n200(monkeypatch):
-    case = [c for c in golden("hashes_large.json") if c["tag"] == "t04_200"][0]
-    monkeypatch.setenv("CCJ_PREPASS", "1")
-    got = _hashes(case["seq"], case["params"])
-    assert {k: got[k] for k in case["hashes"]} == case["hashes"]

@@ -1,6 +1,6 @@
 """Copy the round's profile evidence from gpurun_out/prof (tools/gpu_profile.sh) into profiles/.
 
-usage: python tools/make_profiles.py ROUND      (e.g. r1)
+usage: python tools/make_profiles.py ROUND [--n N --seed S --params P] [--traffic-only] [--prof DIR]
 Writes profiles/<ROUND>_kernel_stats.csv (rocprofv3 --stats), profiles/<ROUND>_bench.json (the
 bench line), and profiles/traffic.json: FETCH_SIZE/WRITE_SIZE per launch of each profiled kernel,
 converted to bytes with the gfx950 calibration of tools/microbench/fetch_calib.hip (FETCH_SIZE
@@ -77,18 +77,32 @@ def level_spans(trace_csv):
 
 
 def main():
-    rnd = sys.argv[1]
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("round")
+    ap.add_argument("--prof", default=PROF, help="gpurun_out/prof-style directory (kt/, fetch/, write/)")
+    ap.add_argument("--n", type=int, default=200)
+    ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--params", default="Turner04")
+    ap.add_argument("--traffic-only", action="store_true", help="only the PMC summary (no stats/bench/spans)")
+    a = ap.parse_args()
+    rnd, prof = a.round, a.prof
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
-    shutil.copy(os.path.join(PROF, "kt", "kt_kernel_stats.csv"), os.path.join(out, f"{rnd}_kernel_stats.csv"))
-    with open(os.path.join(PROF, "bench_full.json")) as f:
-        line = f.read().strip().splitlines()[-1]
-    with open(os.path.join(out, f"{rnd}_bench.json"), "w") as f:
-        f.write(line + "\n")
-    fe = pmc(os.path.join(PROF, "fetch", "f_counter_collection.csv"), "FETCH_SIZE")
-    wr = pmc(os.path.join(PROF, "write", "w_counter_collection.csv"), "WRITE_SIZE")
-    traffic = {"round": rnd, "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- "
-               "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline",
+    headline = (a.n, a.seed, a.params) == (200, 5, "Turner04")
+    if not a.traffic_only:
+        shutil.copy(os.path.join(prof, "kt", "kt_kernel_stats.csv"), os.path.join(out, f"{rnd}_kernel_stats.csv"))
+        with open(os.path.join(prof, "bench_full.json")) as f:
+            line = f.read().strip().splitlines()[-1]
+        with open(os.path.join(out, f"{rnd}_bench.json"), "w") as f:
+            f.write(line + "\n")
+    fe = pmc(os.path.join(prof, "fetch", "f_counter_collection.csv"), "FETCH_SIZE")
+    wr = pmc(os.path.join(prof, "write", "w_counter_collection.csv"), "WRITE_SIZE")
+    cmd = "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+    if not headline:
+        cmd += f" --n {a.n} --seed {a.seed} --params {a.params}"
+    traffic = {"round": rnd, "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- " + cmd,
+               "config": {"n": a.n, "seed": a.seed, "params": a.params},
                "fetch_factor": FETCH_FACTOR, "write_factor": WRITE_FACTOR, "kernels": {}}
     for k in sorted(set(fe) | set(wr)):
         fb, fl = fe.get(k, (0.0, 1))
@@ -96,13 +110,15 @@ def main():
         traffic["kernels"][k] = {"launches": fl, "read_bytes_per_launch": FETCH_FACTOR * fb / max(fl, 1),
                                  "write_bytes_per_launch": WRITE_FACTOR * wb / max(wl, 1),
                                  "hbm_bytes_per_launch": FETCH_FACTOR * fb / max(fl, 1) + WRITE_FACTOR * wb / max(wl, 1)}
-    with open(os.path.join(out, "traffic.json"), "w") as f:
+    name = "traffic.json" if headline else f"traffic_n{a.n}_s{a.seed}_{a.params}.json"
+    with open(os.path.join(out, name), "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(traffic, indent=1))
-    sp = level_spans(os.path.join(PROF, "kt", "kt_kernel_trace.csv"))
-    with open(os.path.join(out, f"{rnd}_level_span.json"), "w") as f:
-        json.dump(sp, f, indent=1)
-    print(json.dumps(sp, indent=1))
+    if not a.traffic_only:
+        sp = level_spans(os.path.join(prof, "kt", "kt_kernel_trace.csv"))
+        with open(os.path.join(out, f"{rnd}_level_span.json"), "w") as f:
+            json.dump(sp, f, indent=1)
+        print(json.dumps(sp, indent=1))
 
 
 if __name__ == "__main__":
