@@ -159,6 +159,10 @@ struct DevTables {
     uint2 *il, *ilm;               // il: pair (p,p+w) closes the loop (PL, PR); ilm: pair encloses (PM)
     int16_t *dummy;                // n+64 values 32767: target of the null entries
     const uint32_t *items;         // k_iloop work items (role << 30 | f1 << 20 | f2 << 10 | chunk)
+    const uint32_t *tiles;         // k_iltile tiles (role << 30 | block << 20 | first key << 10 | cell chunk)
+    const unsigned long long *pb;  // pairability bits: [w][pbw words], bit p of row w = pt(p, p+w) > 0
+    int pbw;                       // 64-bit words per row (positions 0 .. n+1, plus one zero word)
+    int16_t *ieO, *ieI;            // k_iltile energy blocks: [w][p][848] by closing pair / by inner pair
     uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
     int *err;                      // device error word
     // split-point sharing (above): levels [g_lo, g_hi) share; partial-record ring of SHARE_R
@@ -188,7 +192,12 @@ int ccjk_init2d(const ccj::DevTables *T, void *stream);
 int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
 int ccjk_build_il(const ccj::DevTables *T, void *stream);
 int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, int G, int rank, void *stream);
-int ccjk_diag2d(const ccj::DevTables *T, int sigma, void *stream);
+int ccjk_ie_blocks(const ccj::DevTables *T, void *stream);
+int ccjk_iltile(const ccj::DevTables *T, int t, long long first_tile, int ntiles, int G, int rank, void *stream);
+int ccjk_diag2d(const ccj::DevTables *T, int sigma, int G, int rank, void *stream);
+int ccjk_dtail_pack(const ccj::DevTables *T, int sigma, int G, int rank, int16_t *tail, void *stream);
+int ccjk_dtail_unpack(const ccj::DevTables *T, int sigma, const int16_t *recv, size_t slice, size_t off, int G, int rank,
+                      void *stream);
 int ccjk_level4d(const ccj::DevTables *T, int t, int G, int rank, int copies, void *stream);
 int ccjk_level_split(int n, int t, int nblk, int split_target);
 int ccjk_level4d_lead(const ccj::DevTables *T, int t, int G, int rank, void *stream);

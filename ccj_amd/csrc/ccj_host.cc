@@ -144,6 +144,12 @@ struct ccj_ctx {
     uint2 *d_il = nullptr, *d_ilm = nullptr;
     int16_t *d_dummy = nullptr;
     uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
+    uint32_t *d_tiles = nullptr;          // k_iltile tiles, all levels back to back (sequence-independent)
+    unsigned long long *d_pb = nullptr;   // pairability bits [w][pbw] (k_iltile)
+    int16_t *d_ieO = nullptr, *d_ieI = nullptr;  // k_iltile loop-energy blocks [w][p][848]
+    int pbw = 0;
+    std::vector<long long> tl_off;        // first tile of (level t, shard r) at t*world + r
+    bool il_tiles = false;                // CCJ_ILOOP_TILES=1: interior loops as LDS tiles (k_iltile, slower)
     size_t items_cap = 0;
     int16_t *d_send = nullptr, *d_recv = nullptr;  // band-sharded exchange: own slice, world slices
     std::vector<int> xnmax;               // per level: the largest rank's block count (slice = 22 x nmax x M)
@@ -1417,6 +1423,8 @@ static thread_local std::string g_create_err;
 // int16 elements of the exchange slice's P tail: one 64-bit (value, first split) word per interval
 // start i = 0..n
 #define PTAIL_ELEMS(n) (4 * ((size_t)(n) + 1))
+// span tail (k_dtail_pack): 10 int32 planes of n+1 entries, the 2-D values of the span the level carries
+#define DTAIL_ELEMS(n) (2 * 10 * ((size_t)(n) + 1))
 
 // The exchange of one level through the in-process group: every member pulls each member's
 // packed slice into its own receive buffer (same device), between two barriers, so no slice is
@@ -1453,6 +1461,51 @@ static int local_allgather(ccj_ctx *c, size_t slice) {
     HIPCHK(c, e2);
     if (!g->barrier()) return set_err(c, CCJ_E_STATE, "local exchange: a group member failed");
     return CCJ_OK;
+}
+
+// k_iltile's tiles (ccj_kernels.hip), per level t and shard r in that order: one 32-bit word per
+// tile, role << 30 | block << 20 | first key << 10 | cell chunk (TL_NK keys x 64 cells):
+//   PL: own a in [6, t], keys i from 1 by 16 (i <= m), chunks of h over [0, m-i]
+//   PR: own a in [0, t-6], keys q from 0 by 16 (q <= m-1), chunks of i over [1, q+1]
+//   PM: h in [2, m-1], keys j from 1 by 16 (j+h+2 <= n), chunks of a over the keys' [alo, ahi]
+//       (every rank walks every a; each stores only its own)
+// They depend only on n and the sharding, so they are built once per context.
+static void build_tiles(int n, int nlev, int G, int rank, bool simulate, std::vector<uint32_t> &tiles,
+                        std::vector<long long> &off) {
+    constexpr int NK = 16, NC = 64;
+    tiles.clear();
+    off.assign((size_t)n * G + 1, 0);
+    auto push = [&](int role, int blk, int K0, int xc) {
+        tiles.push_back(((uint32_t)role << 30) | ((uint32_t)blk << 20) | ((uint32_t)K0 << 10) | (uint32_t)xc);
+    };
+    for (int t = 0; t < n; ++t)
+        for (int r = 0; r < G; ++r) {
+            off[(size_t)t * G + r] = (long long)tiles.size();
+            if (!(simulate || r == rank) || t < 4 || t >= nlev) continue;
+            const int m = n - t - 2;
+            for (int a = 6; a <= t; ++a) {
+                if (shard_owner(a, G) != r) continue;
+                for (int K0 = 1; K0 <= m; K0 += NK)
+                    for (int xc = 0; xc * NC <= m - K0; ++xc) push(0, a, K0, xc);
+            }
+            for (int a = 0; a <= t - 6; ++a) {
+                if (shard_owner(a, G) != r) continue;
+                for (int K0 = 0; K0 <= m - 1; K0 += NK) {
+                    const int imax = std::min(K0 + NK - 1, m - 1) + 1;
+                    for (int xc = 0; 1 + xc * NC <= imax; ++xc) push(1, a, K0, xc);
+                }
+            }
+            for (int h = 2; h <= m - 1; ++h) {
+                const int g = h + 2;
+                for (int K0 = 1; K0 + g <= n; K0 += NK) {
+                    const int Kend = std::min(K0 + NK - 1, n - g);
+                    const int amin = std::max(2, t - (n - (K0 + g))), amax = std::min(t - 2, Kend - 1);
+                    if (amin > amax) continue;
+                    for (int xc = (amin - 2) / NC; xc <= (amax - 2) / NC; ++xc) push(2, h, K0, xc);
+                }
+            }
+        }
+    off[(size_t)n * G] = (long long)tiles.size();
 }
 
 // Everything that depends on the sequence itself (not only on n): the encoding, the pair-type,
@@ -1508,7 +1561,13 @@ static int seq_setup(ccj_ctx *c) {
     lap("tables");
     // the sequence tables go up asynchronously on st from pinned staging (a reset never blocks on
     // work another context has running on the GPU); the fill's launches follow on st
-    const size_t stage_bytes = plane * (1 + sizeof(int) + sizeof(int16_t)) + 2 * (size_t)(n + 2) * sizeof(short);
+    // pairability bits (k_iltile): row w, bit p = pair (p, p+w) can pair
+    std::vector<unsigned long long> pb((size_t)(n + 1) * c->pbw + 2, 0ull);
+    for (int w = 0; w < n; ++w)
+        for (int p = 1; p + w <= n; ++p)
+            if (pt[(size_t)w * c->rs + p] > 0) pb[(size_t)w * c->pbw + (p >> 6)] |= 1ull << (p & 63);
+    const size_t pb_bytes = pb.size() * sizeof(unsigned long long);
+    const size_t stage_bytes = plane * (1 + sizeof(int) + sizeof(int16_t)) + 2 * (size_t)(n + 2) * sizeof(short) + pb_bytes;
     if (!c->h_stage) {
         HIPCHK(cp, hipHostMalloc(&c->h_stage, stage_bytes, hipHostMallocDefault));
         HIPCHK(cp, hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
@@ -1523,14 +1582,16 @@ static int seq_setup(ccj_ctx *c) {
         return e;
     };
     HIPCHK(cp, up(c->d_pt, pt.data(), plane));
+    HIPCHK(cp, up(c->d_pb, pb.data(), pb_bytes));
     // ---- k_iloop work items (one per wave), counted per (level, shard), then written by k_items
     // on the GPU at the prefix offsets.  By default the count pass runs on the GPU too (k_items
     // pass 0 on st) and the host WAITS for it (hipStreamSynchronize): the offsets are needed on
     // the host to size the k_iloop launches, so ccj_reset blocks until the context's stream has
     // run it.  CCJ_HOST_COUNT=1 counts on host threads instead (the same enumeration, ccj_items.h;
+    // (only for the k_iloop path: the k_iltile tiles do not depend on the sequence)
     // slower, ~1.3 ms at n=200, but no device round trip).
-    {
-        if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
+    if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
+    if (!c->il_tiles) {
         const int G = c->world;
         const int nb = n * G;
         const int rs = c->rs;
@@ -1623,8 +1684,11 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         const char *lt = getenv("CCJ_LEVEL_TIMING");
         if (lt) c->level_timing = std::max(0, std::min(2, atoi(lt)));
         // k_diag2d(t-1) behind k_iloop(t) on one side stream, so each level waits on one event
-        // (fill -0.25 ms at n=200 in 3/3 alternating runs)
-        c->join_diag = true;
+        // (fill -0.25 ms at n=200 in 3/3 alternating runs); band-sharded fills with an exchange
+        // partition each span instead, and the level-t exchange carries span t
+        c->join_diag = !(c->world > 1 && !c->simulate);
+        const char *ii = getenv("CCJ_ILOOP_TILES");
+        c->il_tiles = ii && atoi(ii) != 0;
         const char *g = getenv("CCJ_SHARE_SPLITS");
         c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
     }
@@ -1773,10 +1837,12 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
             return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for split-sharing records failed",
                            SHARE_SLOTS * SHARE_NACC * accC * 16e-9);
     }
-    HIPCHK(cp, hipMalloc(&c->d_ie, ie_elems * sizeof(int16_t)));
+    HIPCHK(cp, hipMalloc(&c->d_ie, (ie_elems + 64) * sizeof(int16_t)));  // + k_iltile's 16-byte tail reads
     HIPCHK(cp, hipMalloc(&c->d_est, plane * sizeof(int16_t)));
     HIPCHK(cp, hipMalloc(&c->d_hp, plane * sizeof(int)));
     HIPCHK(cp, hipMalloc(&c->d_pt, plane));
+    c->pbw = (n + 2 + 63) / 64 + 1;
+    HIPCHK(cp, hipMalloc(&c->d_pb, ((size_t)(n + 1) * c->pbw + 2) * sizeof(unsigned long long)));
     HIPCHK(cp, hipMalloc(&c->d_pair, 64));
     HIPCHK(cp, hipMalloc(&c->d_rtype, 8));
     HIPCHK(cp, hipMalloc(&c->d_lx, c->lx.size() * sizeof(int)));
@@ -1806,6 +1872,15 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         c->pmx = c->pmx_alloc;
         HIPCHK(cp, hipMalloc(&c->d_ldx, ldx.size() * sizeof(LvlX)));
         HIPCHK(cp, hipMemcpy(c->d_ldx, ldx.data(), ldx.size() * sizeof(LvlX), hipMemcpyHostToDevice));
+        if (c->il_tiles) {
+            const size_t eb = (size_t)(n + 1) * c->rs * 848;
+            if (hipMalloc(&c->d_ieO, eb * sizeof(int16_t)) != hipSuccess || hipMalloc(&c->d_ieI, eb * sizeof(int16_t)) != hipSuccess)
+                return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for the interior-loop energy blocks failed", eb * 4e-9);
+            std::vector<uint32_t> tiles;
+            build_tiles(n, c->nlev, c->world, c->rank, c->simulate, tiles, c->tl_off);
+            HIPCHK(cp, hipMalloc(&c->d_tiles, std::max<size_t>(tiles.size(), 1) * sizeof(uint32_t)));
+            HIPCHK(cp, hipMemcpy(c->d_tiles, tiles.data(), tiles.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
         const size_t pairs = (size_t)(n + 1) * c->rs;
         const size_t ents = pairs * IL_CAP;
         HIPCHK(cp, hipMalloc(&c->d_il, ents * sizeof(uint2)));
@@ -1904,6 +1979,11 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.ilm = c->d_ilm;
     T.dummy = c->d_dummy;
     T.items = c->d_items;
+    T.tiles = c->d_tiles;
+    T.pb = c->d_pb;
+    T.ieO = c->d_ieO;
+    T.ieI = c->d_ieI;
+    T.pbw = c->pbw;
     T.ilseg = c->d_ilseg;
     T.ilmseg = c->d_ilmseg;
     T.err = c->d_err;
@@ -1927,7 +2007,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
                 int nm = 0;
                 for (int r = 0; r < G; ++r) nm = std::max(nm, shard_count(t, G, r));
                 c->xnmax[t] = nm;
-                slice = std::max(slice, (((size_t)NMAT4 * nm * c->lv_host[t].M + 3) & ~(size_t)3) + PTAIL_ELEMS(n));
+                slice = std::max(slice, (((size_t)NMAT4 * nm * c->lv_host[t].M + 3) & ~(size_t)3) + PTAIL_ELEMS(n) +
+                                            DTAIL_ELEMS(n));
             }
             if (hipMalloc(&c->d_send, std::max<size_t>(slice, 1) * sizeof(int16_t)) != hipSuccess ||
                 hipMalloc(&c->d_recv, std::max<size_t>(slice * G, 1) * sizeof(int16_t)) != hipSuccess)
@@ -2005,7 +2086,8 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     HIPCHK(c, hipEventRecord(c->ev_start, st));
     HIPCHK(c, (hipError_t)ccjk_init2d(&c->T, st));
     HIPCHK(c, (hipError_t)ccjk_precompute_ie(&c->T, st));
-    HIPCHK(c, (hipError_t)ccjk_build_il(&c->T, st));
+    if (!c->il_tiles) HIPCHK(c, (hipError_t)ccjk_build_il(&c->T, st));
+    else HIPCHK(c, (hipError_t)ccjk_ie_blocks(&c->T, st));
     HIPCHK(c, hipEventRecord(c->ev_pre, st));
     // Four streams:
     //   st_d : k_diag2d(s)  needs P(s) (p_done) and spans < s (stream order)
@@ -2023,11 +2105,20 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
         auto trec = [&](int x, hipStream_t q) { return c->level_timing == 2 ? hipEventRecord(ev[x], q) : hipSuccess; };
         // k_diag2d(sigma) on st_d; or, joined (c->join_diag), on st_il right after k_iloop(sigma+1),
         // so that level sigma+1 waits on one event that covers both
+        const bool xchg = c->world > 1 && !c->simulate;
         auto enqueue_diag = [&](int sg, hipStream_t q) -> int {
             hipEvent_t *evd = &c->tev[7 * (size_t)sg];
             if (sg >= 3) HIPCHK(c, hipStreamWaitEvent(q, c->p_done[sg], 0));
+            // band-sharded: span sg-1 is complete on this rank only after the level-(sg-1) exchange
+            if (xchg && sg >= 1 && sg - 1 < c->nlev) HIPCHK(c, hipStreamWaitEvent(q, c->lev_done[sg - 1], 0));
             if (c->level_timing == 2) HIPCHK(c, hipEventRecord(evd[0], q));
-            HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, sg, q));
+            if (c->simulate) {  // every rank's share of the span, in one context
+                for (int r = 0; r < c->world; ++r) HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, sg, c->world, r, q));
+            } else if (xchg && sg < c->nlev) {  // this rank's intervals; the exchange of level sg brings the rest
+                HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, sg, c->world, c->rank, q));
+            } else {  // unsharded, or the spans past the last 4-D level (no exchange left): every interval
+                HIPCHK(c, (hipError_t)ccjk_diag2d(&c->T, sg, 1, 0, q));
+            }
             if (c->level_timing == 2) HIPCHK(c, hipEventRecord(evd[1], q));
             HIPCHK(c, hipEventRecord(c->dg_done[sg], q));
             return CCJ_OK;
@@ -2046,8 +2137,12 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
             for (int r = 0; r < G; ++r) {  // every rank's launches in simulation, else this rank's
                 if (!c->simulate && r != c->rank) continue;
                 const size_t tr = (size_t)s * G + r;
-                HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[tr], (int)(c->it_off[tr + 1] - c->it_off[tr]), G, r,
-                                                 c->st_il));
+                if (c->il_tiles)
+                    HIPCHK(c, (hipError_t)ccjk_iltile(&c->T, s, c->tl_off[tr], (int)(c->tl_off[tr + 1] - c->tl_off[tr]), G, r,
+                                                      c->st_il));
+                else
+                    HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[tr], (int)(c->it_off[tr + 1] - c->it_off[tr]), G, r,
+                                                     c->st_il));
             }
             HIPCHK(c, trec(3, c->st_il));
             if (joined) {
@@ -2076,7 +2171,11 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                 // extra collective.
                 const int nmax = c->xnmax[s];
                 const size_t slice4 = ((size_t)NMAT4 * nmax * c->lv_host[s].M + 3) & ~(size_t)3;
-                const size_t slice = slice4 + PTAIL_ELEMS(n);
+                const size_t dt_off = slice4 + PTAIL_ELEMS(n);
+                const size_t slice = dt_off + DTAIL_ELEMS(n);
+                // span s (this rank's intervals) rides the same slice
+                HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s], 0));
+                HIPCHK(c, (hipError_t)ccjk_dtail_pack(&c->T, s, G, c->rank, c->d_send + dt_off, st));
                 const int sig = s + 2;
                 const bool ptail = s >= 1 && sig <= n - 1;
                 if (ptail) {
@@ -2092,6 +2191,7 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                         return set_err(c, CCJ_E_COMM, "ncclAllGather failed at level %d", s);
                 }
                 HIPCHK(c, (hipError_t)ccjk_unpack(&c->T, s, G, c->rank, nmax, c->d_recv, slice, st));
+                HIPCHK(c, (hipError_t)ccjk_dtail_unpack(&c->T, s, c->d_recv, slice, dt_off, G, c->rank, st));
                 if (ptail) {
                     HIPCHK(c, (hipError_t)ccjk_ptail_unpack(&c->T, sig, c->d_recv, slice, slice4, G, st));
                     HIPCHK(c, hipEventRecord(c->p_done[sig], st));  // P(sig) final on every rank
@@ -2778,6 +2878,10 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_ilm);
     hipFree(c->d_dummy);
     hipFree(c->d_items);
+    hipFree(c->d_tiles);
+    hipFree(c->d_pb);
+    hipFree(c->d_ieO);
+    hipFree(c->d_ieI);
     hipFree(c->d_send);
     hipFree(c->d_recv);
     if (c->h_stage) hipHostFree(c->h_stage);

@@ -191,14 +191,16 @@ __global__ void k_precompute_ie(DevTables T) {
 // ------------------------------------------------------------------------------------------
 // 2-D anti-diagonal sigma: one 256-thread workgroup per interval (i, l = i+sigma).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma) {
+// Band-sharded fills partition each span: interval i belongs to rank (i-1) % G, and
+// the level-sigma exchange carries the span's values to the other ranks (k_dtail_pack / _unpack).
+__global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma, int G, int rank) {
 #ifdef CCJ_DEBUG_BOUNDS
     g_dbg_err = T.err;
 #endif
     __shared__ int red[4];
     __shared__ int sh_v, sh_p;
     const int n = T.n, rs = T.rs;
-    const int i = blockIdx.x + 1;
+    const int i = (int)blockIdx.x * G + rank + 1;
     const int l = i + sigma;
     if (l > n) return;
     const int tid = threadIdx.x;
@@ -1046,6 +1048,396 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
 }
 
 // ------------------------------------------------------------------------------------------
+// Interior loops as LDS-staged tiles (k_iltile).  Same minima as k_iloop
+// (get_PLiloop / get_PRiloop / get_PMiloop, pseudo_loop.cc:682-773), organised so that a partner
+// value is fetched once per tile instead of once per closing pair that reads it.  A tile is one
+// 256-thread workgroup: TL_NK consecutive "keys" (closing pairs for PL/PR, the cell's own inner
+// pair for PM) of one role and block, times TL_NC consecutive cells (one per lane):
+//   PL: block a, keys i (pair (i, i+a)),          cells h, partner PLx column  c  = i+1+u1, element h+dt-1-u1
+//   PR: block a, keys q (pair (k, l), k = q+a+3), cells i, partner PRx row     q' = q+1+u1, element i-1
+//   PM: row h,   keys j (pair (j, j+h+2)),        cells a, partner PMx row (h+dt, d = j-1-u1), element a-1-u1
+// For a source-level distance dt = 2+u1+u2 every candidate of every key reads one "source row" R
+// of that dt's copy (TL_NK + #u1 - 1 consecutive rows), and whether the candidate's other pair can
+// pair is a property of R alone (pairability bit table T.pb).  The workgroup stages, for every dt
+// at once (in chunks of dts that fit its LDS), the pairable rows its keys read, 64 + 15 elements
+// each, plus one 29 x 29 loop-energy block per pairable key (T.ieO / T.ieI), so the loads of a
+// whole chunk are in flight together: one memory round trip per chunk, not per dt.  Then each wave
+// walks its keys: per (dt, staged row) one ds_read_u16 (partner), one broadcast ds_read_u16
+// (energy), an add and a min per 64 cells.  Exactly the reference's candidate set: the key's pair
+// can pair, the partner's pair can pair, u1, u2 <= 28, dt <= a-4 / b-4 / t-2, and PM's per-cell
+// d > i, dp < l as a lane mask.  Min is order-independent: bit-identical minima.
+constexpr int TL_NK = 16;               // keys per tile
+constexpr int TL_NC = 64;               // cells per tile (one per lane)
+constexpr int TL_EB = 848;              // int16 per key energy block: 29 x 29 (u1 major) padded to 16 bytes
+constexpr int TL_DTN = 56;              // dt = 3 .. 58
+constexpr int TL_ROWMAX = TL_NK + IE_U - 1;  // 44 source rows per dt at most
+constexpr int TL_B = 8;                 // staging loads (16 bytes per lane) in flight per wave
+constexpr int TL_BIG = 1 << 28;
+constexpr int TL_LDS = 40 * 1024;       // dynamic LDS per tile workgroup (4 per CU)
+// LDS carve (bytes): dt table (+ one word: the number of dt chunks), row lists, the pairable keys'
+// energy blocks, then the staged rows of one dt chunk (the rest)
+constexpr int TL_OFF_NCH = TL_DTN * 16;                          // dt table: mask, first chunk, chunks/row, chunk id
+constexpr int TL_OFF_ROWL = TL_OFF_NCH + 16;
+constexpr int TL_OFF_EB = TL_OFF_ROWL + TL_DTN * 48;             // row list: slot -> row (int8), 48 per dt
+
+__device__ __forceinline__ uint4 ldg_u4(const int16_t *base, long long e, long long lim) {
+    // 16 bytes from element e (any 2-byte alignment; clamped into the allocation: the clamped
+    // values are never used)
+    e = e < 0 ? 0 : (e > lim - 8 ? lim - 8 : e);
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4 *)(const char *)(base + e);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+// bits r in [lo, hi] (lo, hi in [0, 63]; empty when lo > hi)
+__device__ __forceinline__ unsigned long long bit_range(int lo, int hi) {
+    if (lo > hi) return 0ull;
+    const unsigned long long up = hi >= 63 ? ~0ull : ((2ull << hi) - 1ull);
+    return up & ~((1ull << lo) - 1ull);
+}
+// pairability bits (T.pb: per span w a bit row over positions p, bit p = pair (p, p+w) can pair):
+// bit r of the result = pair (p0+r, p0+r+w) can pair; 0 outside the table.  Scalar loads.
+__device__ __forceinline__ unsigned long long pbits(const DevTables &T, int w, int p0) {
+    if (w < 0 || w > T.n || p0 > T.n + 1 || p0 <= -64) return 0ull;
+    typedef const __attribute__((address_space(4))) unsigned long long cu64;
+    cu64 *row = (cu64 *)(unsigned long long)(T.pb + (size_t)w * T.pbw);
+    if (p0 < 0) return row[0] << (-p0);
+    const int wi = p0 >> 6, sh = p0 & 63;
+    unsigned long long x = row[wi] >> sh;
+    if (sh) x |= row[wi + 1] << (64 - sh);
+    return x;
+}
+
+struct TlDt {                // one dt of a tile (LDS): 16 bytes
+    unsigned long long mask;  // staged rows r (row R = Rlo + r)
+    int first;                // first 16-byte chunk of the dt's rows inside its dt chunk's row area
+    short ch;                 // chunks per staged row
+    short cid;                // which dt chunk the dt belongs to
+};
+
+// a dt table entry as wave-uniform (scalar) values: every wave reads the same LDS word, and
+// readfirstlane lets the compiler keep the loop control and the level descriptors scalar
+__device__ __forceinline__ TlDt tl_dt(const TlDt *dtab, int di) {
+    const uint4 w = *(const uint4 *)(dtab + di);
+    TlDt d;
+    d.mask = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)w.y) << 32) |
+             (unsigned)__builtin_amdgcn_readfirstlane((int)w.x);
+    d.first = __builtin_amdgcn_readfirstlane((int)w.z);
+    const int hw = __builtin_amdgcn_readfirstlane((int)w.w);
+    d.ch = (short)(hw & 0xffff);
+    d.cid = (short)(hw >> 16);
+    return d;
+}
+
+template <int role>
+__device__ __forceinline__ void iltile_body(const DevTables &T, int t, uint32_t tw, int G_SH, int rank, char *smem) {
+    TlDt *dtab = (TlDt *)smem;
+    int8_t *rowl = (int8_t *)(smem + TL_OFF_ROWL);
+    int16_t *eb = (int16_t *)(smem + TL_OFF_EB);
+    const int n = T.n, rs = T.rs, m = n - t - 2;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int blk = (int)((tw >> 20) & 1023u), K0 = (int)((tw >> 10) & 1023u), xc = (int)(tw & 1023u);
+    int a = 0, b = 0, g = 0, X0, dtmax;
+    if (role == 0) {
+        a = blk; b = t - a; X0 = xc * TL_NC; dtmax = imin(2 * (IE_U - 1) + 2, a - 4);
+    } else if (role == 1) {
+        a = blk; b = t - a; X0 = 1 + xc * TL_NC; dtmax = imin(2 * (IE_U - 1) + 2, b - 4);
+    } else {
+        g = blk + 2; X0 = 2 + xc * TL_NC; dtmax = imin(2 * (IE_U - 1) + 2, t - 2);
+    }
+    const int x = X0 + lane;  // this lane's cell coordinate (h, i or a)
+    // ---- keys (every wave, the same): pair can pair and a cell in this tile
+    unsigned keymask;
+    {
+        const int K = K0 + lane;
+        bool ok = false;
+        if (lane < TL_NK) {
+            if (role == 0) ok = K >= 1 && K <= m && X0 <= m - K;
+            else if (role == 1) ok = K <= m - 1 && X0 <= K + 1;
+            else {
+                const int k = K + g;
+                if (K >= 1 && k <= n) {
+                    const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, K - 1);
+                    ok = alo <= ahi && X0 <= ahi && X0 + TL_NC - 1 >= alo;
+                }
+            }
+        }
+        const unsigned long long kp = role == 0 ? pbits(T, a, K0) : role == 1 ? pbits(T, b, K0 + a + 3) : pbits(T, g, K0);
+        keymask = (unsigned)(__ballot(ok) & kp) & 0xffffu;
+    }
+    if (keymask == 0) return;  // whole workgroup (uniform)
+    const int nkeys = __popc(keymask);
+    int16_t *rows = (int16_t *)(smem + TL_OFF_EB + nkeys * TL_EB * 2);
+    const int rowcap = (TL_LDS - (TL_OFF_EB + nkeys * TL_EB * 2)) / 16;  // 16-byte chunks per dt chunk
+    // ---- energy blocks of the pairable keys: key slot = rank of the key in keymask
+    {
+        const int16_t *src = role == 2 ? T.ieI : T.ieO;
+        const int pw = role == 0 ? a : role == 1 ? b : g, pp0 = role == 0 ? K0 : role == 1 ? K0 + a + 3 : K0;
+        const int per = TL_EB / 8;  // 106 chunks per block
+        for (int q = tid; q < nkeys * per; q += 256) {
+            const int ks = q / per, c = q - ks * per;
+            // ks-th set bit of keymask
+            unsigned mm = keymask;
+            for (int z = 0; z < ks; ++z) mm &= mm - 1;
+            const int kk = __ffs(mm) - 1;
+            const int16_t *blkp = src + ((size_t)pw * rs + pp0 + kk) * TL_EB;
+            *(uint4 *)(eb + ks * TL_EB + 8 * c) = *(const uint4 *)(blkp + 8 * c);
+        }
+    }
+    // ---- per-dt row masks, one dt per lane of wave 0 (vector loads of the pairability words: one
+    // round trip for every dt), row lists, and the dt chunks: contiguous dt ranges whose rows fit
+    // the row area (greedy, in dt order)
+    const int ndt = imax(0, dtmax - 2);  // dt = 3 .. dtmax
+    if (wv == 0) {
+        const int dt = lane + 3;
+        unsigned long long mask = 0;
+        int ch = 0;
+        if (lane < ndt) {
+            const int u1min = imax(0, dt - 2 - (IE_U - 1)), u1max = imin(IE_U - 1, dt - 2), cnt = u1max - u1min + 1;
+            const int nrows = TL_NK + cnt - 1;
+            const int Rlo = role == 2 ? K0 - 1 - u1max : K0 + 1 + u1min;
+            const int mp = m + dt;
+            unsigned long long used = keymask;
+            for (int len = 1; len < cnt;) {
+                const int st = imin(len, cnt - len);
+                used |= used << st;
+                len += st;
+            }
+            int rlo, rhi, w, p0;
+            if (role == 0) { w = a - dt; p0 = Rlo; rlo = 1 - Rlo; rhi = mp - Rlo; }
+            else if (role == 1) { w = b - dt; p0 = Rlo + a + 3; rlo = -Rlo; rhi = mp - 1 - Rlo; }
+            else { w = g + dt; p0 = Rlo; rlo = 1 - Rlo; rhi = n - g - dt - Rlo; }
+            unsigned long long pb = 0;
+            if (w >= 0 && w <= n && p0 <= n + 1 && p0 > -64) {
+                const unsigned long long *row = T.pb + (size_t)w * T.pbw;
+                if (p0 < 0) pb = row[0] << (-p0);
+                else {
+                    const int wi = p0 >> 6, sh = p0 & 63;
+                    pb = row[wi] >> sh;
+                    if (sh) pb |= row[wi + 1] << (64 - sh);
+                }
+            }
+            mask = used & pb & bit_range(imax(rlo, 0), imin(rhi, nrows - 1));
+            ch = (TL_NC + (role == 1 ? 0 : imin(TL_NK, cnt) - 1) + 7) >> 3;
+            int slot = 0;
+            for (unsigned long long mm = mask; mm; mm &= mm - 1) rowl[lane * 48 + slot++] = (int8_t)(__ffsll((long long)mm) - 1);
+        }
+        const int need = __popcll(mask) * ch;
+        // greedy chunking over the dts (scalar walk over the lanes' needs)
+        int cur = 0, cid = 0, myfirst = 0, mycid = 0;
+        for (int di = 0; di < ndt; ++di) {
+            const int nd = __builtin_amdgcn_readlane(need, di);
+            if (cur + nd > rowcap) { ++cid; cur = 0; }
+            if (lane == di) { myfirst = cur; mycid = cid; }
+            cur += nd;
+        }
+        if (lane < ndt) {
+            TlDt d;
+            d.mask = mask;
+            d.first = myfirst;
+            d.ch = (short)ch;
+            d.cid = (short)mycid;
+            dtab[lane] = d;
+        }
+        if (lane == 0) *(int *)(smem + TL_OFF_NCH) = cid + 1;
+    }
+    __syncthreads();
+    const int nchunk = ndt > 0 ? __builtin_amdgcn_readfirstlane(*(const volatile int *)(smem + TL_OFF_NCH)) : 0;
+    // ---- accumulators: wave wv takes the pairable keys of rank wv, wv+4, ... (at most 4)
+    int acc[4], kkz[4];
+    const int nz = (nkeys - wv + 3) >> 2;
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+        acc[z] = TL_BIG;
+        unsigned mm = keymask;
+        for (int y = 0; y < wv + 4 * z && mm; ++y) mm &= mm - 1;
+        kkz[z] = mm ? __ffs(mm) - 1 : 0;
+    }
+    const int16_t *cbase = role == 2 ? T.pmx : T.d4x;
+    const long long clim = role == 2 ? T.npm : T.nx;
+    int dlo = 0;  // first dt index of the chunk
+    for (int cc = 0; cc < nchunk; ++cc) {
+        int dhi = dlo;  // one past the chunk's last dt index
+        while (dhi < ndt && tl_dt(dtab, dhi).cid == cc) ++dhi;
+        // staging: wave wv takes dt indices dlo+wv, dlo+wv+4, ... of the chunk, TL_B loads in
+        // flight; the (dt, round) of each load of a batch is fixed first (scalar), then the loads
+        // are issued unconditionally (idle lanes re-read a valid chunk), so the compiler counts
+        // them and each store waits only for its own load
+        {
+            int di = dlo + wv, rd = 0;
+            auto skip = [&]() {
+                while (di < dhi && tl_dt(dtab, di).mask == 0) di += 4;
+            };
+            skip();
+            while (di < dhi) {
+                int bdi[TL_B], brd[TL_B];
+#pragma unroll
+                for (int u = 0; u < TL_B; ++u) {
+                    bdi[u] = di;
+                    brd[u] = rd;
+                    if (di < dhi) {
+                        const TlDt d = tl_dt(dtab, di);
+                        if (++rd * 64 >= __popcll(d.mask) * d.ch) {
+                            rd = 0;
+                            di += 4;
+                            skip();
+                        }
+                    } else {
+                        bdi[u] = bdi[0];  // a repeat of a live slot, never stored
+                        brd[u] = -1;
+                    }
+                }
+                uint4 reg[TL_B];
+                int dst[TL_B];
+#pragma unroll
+                for (int u = 0; u < TL_B; ++u) {
+                    const int bd = bdi[u];
+                    const TlDt d = tl_dt(dtab, bd);
+                    const int total = __popcll(d.mask) * d.ch;
+                    const int qq = imax(brd[u], 0) * 64 + lane;
+                    const bool live = brd[u] >= 0 && qq < total;
+                    const int q = live ? qq : 0;
+                    const int dt = bd + 3, tp = t - dt;
+                    // level descriptors of the source level through scalar loads
+                    typedef const __attribute__((address_space(4))) long long cll;
+                    typedef const __attribute__((address_space(4))) int cint;
+                    LvlDev Lp;
+                    Lp.C = *(cint *)(unsigned long long)&T.ld[tp].C;
+                    Lp.M = *(cint *)(unsigned long long)&T.ld[tp].M;
+                    LvlX Xp;
+                    Xp.lbx = *(cll *)(unsigned long long)&T.ldx[tp].lbx;
+                    Xp.pmb = *(cll *)(unsigned long long)&T.ldx[tp].pmb;
+                    const int s = q / d.ch, c = q - s * d.ch;
+                    const int r = rowl[bd * 48 + s];
+                    const int u1min = imax(0, dt - 2 - (IE_U - 1)), u1max = imin(IE_U - 1, dt - 2);
+                    long long src;
+                    if (role == 0) {
+                        const int R = K0 + 1 + u1min + r, mp = m + dt, ap = a - dt;
+                        const int u1hi = imin(u1max, R - 1 - K0);
+                        const long long y = R - 1;
+                        src = Xp.lbx + (long long)ap * Lp.M + y * mp - ((y * (y - 1)) >> 1) + (X0 + dt - 1 - u1hi);
+                    } else if (role == 1) {
+                        const int R = K0 + 1 + u1min + r;
+                        src = Xp.lbx + Lp.C + (long long)a * Lp.M + (((long long)R * (R + 1)) >> 1) + (X0 - 1);
+                    } else {
+                        const int R = K0 - 1 - u1max + r;
+                        const int u1hi = imin(u1max, K0 + TL_NK - 2 - R);
+                        src = Xp.pmb + ((long long)(g - 2 + dt) * n + R - 1) * (tp + 1) + (X0 - 1 - u1hi);
+                    }
+                    reg[u] = ldg_u4(cbase, src + 8 * c, clim);
+                    dst[u] = live ? (d.first + q) * 8 : -1;
+                }
+#pragma unroll
+                for (int u = 0; u < TL_B; ++u)
+                    if (dst[u] >= 0) *(uint4 *)(rows + dst[u]) = reg[u];
+            }
+        }
+        __syncthreads();
+        // walk: dt outer (one dt-table read), this wave's keys inner
+        for (int di = dlo; di < dhi; ++di) {
+            const TlDt d = tl_dt(dtab, di);
+            if (d.mask == 0) continue;
+            const int dt = di + 3;
+            const int u1min = imax(0, dt - 2 - (IE_U - 1)), u1max = imin(IE_U - 1, dt - 2), cnt = u1max - u1min + 1;
+            const int rbase = d.first * 8 + lane;
+#pragma unroll
+            for (int z = 0; z < 4; ++z) {
+                if (z >= nz) break;
+                const int kk = kkz[z];
+                const int16_t *ebk = eb + (wv + 4 * z) * TL_EB + (dt - 2);  // + u1 * (IE_U - 1): e(u1, dt-2-u1)
+                unsigned long long bits = (d.mask >> kk) & ((1ull << cnt) - 1ull);
+                int cur = acc[z];
+                while (bits) {
+                    int jj[4], pen[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        jj[u] = bits ? __ffsll((long long)bits) - 1 : 0;
+                        pen[u] = bits ? 0 : TL_BIG;
+                        bits &= bits - 1;
+                    }
+                    int v[4], e[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int r = kk + jj[u];
+                        const int sl = __popcll(d.mask & ((1ull << r) - 1ull));
+                        const int u1 = role == 2 ? u1max - jj[u] : u1min + jj[u];
+                        const int sh = role == 0 ? imin(cnt - 1 - jj[u], kk) : role == 2 ? imin(jj[u], TL_NK - 1 - kk) : 0;
+                        v[u] = rows[rbase + sl * d.ch * 8 + sh];
+                        e[u] = ebk[u1 * (IE_U - 1)];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        int c = v[u] + e[u] + pen[u];
+                        if (role == 2) {
+                            const int u1 = u1max - jj[u];
+                            c += ((unsigned)(x - (u1 + 2)) <= (unsigned)(t - dt - 2)) ? 0 : TL_BIG;
+                        }
+                        cur = imin(cur, c);
+                    }
+                }
+                acc[z] = cur;
+            }
+        }
+        __syncthreads();  // the next chunk overwrites the rows
+        dlo = dhi;
+    }
+    // ---- results: the interior-loop minimum of every cell of this wave's keys, clamped like a store
+    const LvlDev Lt = T.ld[t];
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+        if (z >= nz) break;
+        const int K = K0 + kkz[z];
+        const int v = clamp_store(acc[z]);
+        if (role == 0) {
+            const int h = x;
+            if (h <= m - K) T.d4[Lt.lb + (long long)PL * Lt.C + (long long)a * Lt.M + h * m - ((h * (h - 1)) >> 1) + K - 1] = (int16_t)v;
+        } else if (role == 1) {
+            const int i = x, h = K + 1 - i;
+            if (i <= K + 1) T.d4[Lt.lb + (long long)PR * Lt.C + (long long)a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)v;
+        } else {
+            const int k = K + g, h = g - 2, aa = x;
+            const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, K - 1);
+            if (aa >= alo && aa <= ahi && shard_owner(aa, G_SH) == rank)
+                T.d4[Lt.lb + (long long)PM * Lt.C + (long long)aa * Lt.M + h * m - ((h * (h - 1)) >> 1) + K - aa - 1] = (int16_t)v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_iltile(DevTables T, int t, long long first, int G_SH, int rank) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // XCD-contiguous mapping: workgroup b runs on XCD b % 8, so XCD x takes one contiguous run of
+    // tiles (neighbouring key ranges of one block read overlapping source rows: L2 reuse)
+    const int nb = (int)gridDim.x, q8 = nb >> 3, r8 = nb & 7, bid = (int)blockIdx.x, xcd = bid & 7, pos = bid >> 3;
+    const int tile = xcd < r8 ? xcd * (q8 + 1) + pos : r8 * (q8 + 1) + (xcd - r8) * q8 + pos;
+    const uint32_t tw = ld_const(T.tiles + first + tile);
+    const int role = (int)(tw >> 30);
+    if (role == 0) iltile_body<0>(T, t, tw, G_SH, rank, smem);
+    else if (role == 1) iltile_body<1>(T, t, tw, G_SH, rank, smem);
+    else iltile_body<2>(T, t, tw, G_SH, rank, smem);
+}
+
+// Per-key loop-energy blocks for k_iltile (from T.ie, once per fill): ieO[w][p] = the 29 x 29
+// get_e_intP window of the closing pair (p, p+w) (PL, PR); ieI[g][j] = the window of the loops
+// closed around the inner pair (j, j+g) (PM: outer pair (j-1-u1, j+g+1+u2)).  u1 major, 848 int16.
+__global__ __launch_bounds__(256) void k_ie_blocks(DevTables T) {
+    const int n = T.n, rs = T.rs;
+    const int w = blockIdx.y, p = blockIdx.x + 1;
+    if (p + w > n) return;
+    int16_t *o = T.ieO + ((size_t)w * rs + p) * TL_EB, *q = T.ieI + ((size_t)w * rs + p) * TL_EB;
+    for (int uu = threadIdx.x; uu < TL_EB; uu += 256) {
+        int16_t vo = INTERN_INF, vi = INTERN_INF;
+        if (uu < IE_U * IE_U) {
+            const int u1 = uu / IE_U, u2 = uu - u1 * IE_U;
+            vo = T.ie[((size_t)uu * (n + 1) + w) * rs + p];
+            const int d = p - 1 - u1, wo = w + 2 + u1 + u2;
+            if (d >= 1 && d + wo <= n) vi = T.ie[((size_t)uu * (n + 1) + wo) * rs + d];
+        }
+        o[uu] = vo;
+        q[uu] = vi;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // AoS loop records (ccj_engine.h RecType): pack / unpack int16 pairs
 __device__ __forceinline__ unsigned pk16(int lo, int hi) { return (unsigned)(uint16_t)lo | ((unsigned)(uint16_t)hi << 16); }
 __device__ __forceinline__ int lo16(unsigned w) { return (int)(int16_t)(w & 0xffffu); }
@@ -1389,6 +1781,9 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         pK1 = AJ_[0][6];
         }
         if (!lane_ok || part != 0) return;
+#ifdef CCJ_ABLATE_NOACC  // timing only: no partial-record stores (followers read stale partials)
+        return;
+#endif
 #pragma unroll
         for (int r = 0; r < SHARE_R; ++r) {
             if (r < r0) continue;
@@ -1598,6 +1993,9 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         fO2 = AL_[0][8];
         }
         if (!lane_ok || part != 0) return;
+#ifdef CCJ_ABLATE_NOACC
+        return;
+#endif
 #pragma unroll
         for (int r = 0; r < SHARE_R; ++r) {
             if (r < r0) continue;
@@ -1788,27 +2186,39 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     dst[PfromL * C] = (int16_t)clamp_store(vPfromL);
     dst[PfromR * C] = (int16_t)clamp_store(vPfromR);
     dst[PfromM * C] = (int16_t)clamp_store(vPfromM);
+#ifndef CCJ_ABLATE_NOMAT5  // timing only: the 5 matrices no fill kernel reads back (they live in the records)
     dst[PfromMprime * C] = (int16_t)clamp_store(vPfromMp);
+#endif
     dst[PfromO * C] = (int16_t)clamp_store(vPfromO);
+#ifndef CCJ_ABLATE_NOMAT5
     dst[PLmloop00 * C] = (int16_t)clamp_store(vPLm00);
+#endif
     dst[PLmloop01 * C] = (int16_t)clamp_store(vPLm01);
     dst[PLmloop10 * C] = (int16_t)clamp_store(vPLm10);
+#ifndef CCJ_ABLATE_NOMAT5
     dst[PRmloop00 * C] = (int16_t)clamp_store(vPRm00);
+#endif
     dst[PRmloop01 * C] = (int16_t)clamp_store(vPRm01);
     dst[PRmloop10 * C] = (int16_t)clamp_store(vPRm10);
+#ifndef CCJ_ABLATE_NOMAT5
     dst[PMmloop00 * C] = (int16_t)clamp_store(vPMm00);
+#endif
     dst[PMmloop01 * C] = (int16_t)clamp_store(vPMm01);
     dst[PMmloop10 * C] = (int16_t)clamp_store(vPMm10);
+#ifndef CCJ_ABLATE_NOMAT5
     dst[POmloop00 * C] = (int16_t)clamp_store(vPOm00);
+#endif
     dst[POmloop01 * C] = (int16_t)clamp_store(vPOm01);
     dst[POmloop10 * C] = (int16_t)clamp_store(vPOm10);
     // loop records and interior-loop copies (the copies only where a later k_iloop can read them:
     // its pair can pair); in sharded fills the other ranks' cells get both from k_unpack
     if (!copies) return;
+#ifndef CCJ_ABLATE_NOREC  // timing only: no loop-record stores (the split loops then read stale records)
     write_records(T, Lt.lr, C, (unsigned)(a * Mt) + L0, clamp_store(vPLm00), clamp_store(vPMm00), clamp_store(vPOm00),
                   clamp_store(vPfromL), clamp_store(vPfromO), clamp_store(vPLm10), clamp_store(vPfromMp),
                   clamp_store(vPK), clamp_store(vPRm00), clamp_store(vPfromR), imin(sPL, sPR), clamp_store(vPMm10),
                   clamp_store(vPOm10));
+#endif
 #ifdef CCJ_ABLATE_NOCOPY
     return;  // timing only: no interior-loop copies (k_iloop then reads stale values)
 #endif
@@ -1845,10 +2255,61 @@ extern "C" int ccjk_precompute_ie(const DevTables *T, void *stream) {
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_diag2d(const DevTables *T, int sigma, void *stream) {
-    const int nb = T->n - sigma;
+extern "C" int ccjk_diag2d(const DevTables *T, int sigma, int G, int rank, void *stream) {
+    const int nint = T->n - sigma;  // intervals of the span; rank takes i = rank+1, rank+1+G, ...
+    const int nb = nint > rank ? (nint - rank + G - 1) / G : 0;
     if (nb <= 0) return 0;
-    hipLaunchKernelGGL(k_diag2d, dim3(nb), dim3(256), 0, (hipStream_t)stream, *T, sigma);
+    hipLaunchKernelGGL(k_diag2d, dim3(nb), dim3(256), 0, (hipStream_t)stream, *T, sigma, G, rank);
+    return (int)hipGetLastError();
+}
+
+// The 2-D values of span sigma that k_diag2d writes, for the band-sharded exchange: DT_N int32 planes
+// of n+1 entries (V, Vt, P, WBP, WB, WPP, WP, WMv, WMp, WM) in the tail of the level-sigma slice.
+// Pack: this rank's intervals.  Unpack: every other rank's intervals (owner (i-1) % G), plus WBW.
+constexpr int DT_N = 10;
+__global__ __launch_bounds__(256) void k_dtail_pack(DevTables T, int sigma, int G, int rank, int *tail) {
+    const int i = 1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int n = T.n;
+    if (i + sigma > n || (i - 1) % G != rank) return;
+    const int cell = sigma * T.rs + i;
+    const int v[DT_N] = {T.V[cell], (int)T.Vt[cell], T.P[cell], T.WBP[cell], T.WB[cell],
+                         T.WPP[cell], T.WP[cell], T.WMv[cell], T.WMp[cell], T.WM[cell]};
+#pragma unroll
+    for (int x = 0; x < DT_N; ++x) tail[x * (n + 1) + i] = v[x];
+}
+__global__ __launch_bounds__(256) void k_dtail_unpack(DevTables T, int sigma, const int16_t *recv, size_t slice, size_t off,
+                                                      int G, int rank) {
+    const int i = 1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int n = T.n;
+    const int owner = (i - 1) % G;
+    if (i + sigma > n || owner == rank) return;
+    const int *tl = (const int *)(recv + (size_t)owner * slice + off);
+    const int cell = sigma * T.rs + i;
+    T.V[cell] = tl[0 * (n + 1) + i];
+    T.Vt[cell] = (int8_t)tl[1 * (n + 1) + i];
+    T.P[cell] = tl[2 * (n + 1) + i];
+    T.WBP[cell] = tl[3 * (n + 1) + i];
+    T.WB[cell] = tl[4 * (n + 1) + i];
+    T.WPP[cell] = tl[5 * (n + 1) + i];
+    T.WP[cell] = tl[6 * (n + 1) + i];
+    T.WMv[cell] = tl[7 * (n + 1) + i];
+    T.WMp[cell] = tl[8 * (n + 1) + i];
+    T.WM[cell] = tl[9 * (n + 1) + i];
+    T.WBW[cell] = make_int2(tl[3 * (n + 1) + i], tl[6 * (n + 1) + i]);
+}
+extern "C" int ccjk_dtail_pack(const DevTables *T, int sigma, int G, int rank, int16_t *tail, void *stream) {
+    const int cnt = T->n - sigma;
+    if (cnt <= 0) return 0;
+    hipLaunchKernelGGL(k_dtail_pack, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, sigma, G, rank,
+                       (int *)tail);
+    return (int)hipGetLastError();
+}
+extern "C" int ccjk_dtail_unpack(const DevTables *T, int sigma, const int16_t *recv, size_t slice, size_t off, int G, int rank,
+                                 void *stream) {
+    const int cnt = T->n - sigma;
+    if (cnt <= 0) return 0;
+    hipLaunchKernelGGL(k_dtail_unpack, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, sigma, recv,
+                       slice, off, G, rank);
     return (int)hipGetLastError();
 }
 
@@ -1889,6 +2350,22 @@ extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int n
     if (nitems <= 0) return 0;
     hipLaunchKernelGGL(k_iloop, dim3((unsigned)((nitems + IL_WPB - 1) / IL_WPB)), dim3(64 * IL_WPB), 0, (hipStream_t)stream, *T, t, first_item,
                        nitems, G, rank);
+    return (int)hipGetLastError();
+}
+
+extern "C" int ccjk_ie_blocks(const DevTables *T, void *stream) {
+    const int n = T->n;
+    if (n < 1) return 0;
+    hipLaunchKernelGGL(k_ie_blocks, dim3(n, n + 1), dim3(256), 0, (hipStream_t)stream, *T);
+    return (int)hipGetLastError();
+}
+
+extern "C" int ccjk_iltile(const DevTables *T, int t, long long first_tile, int ntiles, int G, int rank, void *stream) {
+#ifdef CCJ_ABLATE_ILOOP
+    return 0;
+#endif
+    if (ntiles <= 0) return 0;
+    hipLaunchKernelGGL(k_iltile, dim3((unsigned)ntiles), dim3(256), TL_LDS, (hipStream_t)stream, *T, t, first_tile, G, rank);
     return (int)hipGetLastError();
 }
 

@@ -80,7 +80,7 @@ def run(case):
         cmd += ["-P", os.path.join(PARDIR, "rna_%s.par" % params)]
     if xs:
         cmd += ["--samples", "5", "--srand", str(xs)]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=3600)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=4 * 3600)
     if p.returncode != 0:
         raise RuntimeError("%s: rc %d %s" % (name, p.returncode, p.stderr[-400:]))
     rec = {"name": name, "seq": seq, "params": params, "dangles": dangles, "h2": {}, "h4": {}, "exp": {}}

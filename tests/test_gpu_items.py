@@ -1,4 +1,7 @@
-"""The k_iloop work-item enumeration (ccj_items.h, 128-cell items) checked three ways (-m gpu).
+"""The interior-loop work decompositions checked against the reference (-m gpu): the default k_iloop
+work items (ccj_items.h, 128-cell items), enumerated three ways, and the opt-in LDS-staged k_iltile
+tiles (CCJ_ILOOP_TILES=1: 16 keys x 64 cells, sequence-independent; slower), each
+unsharded and band-sharded.
 
 ccj_reset sizes the k_iloop launches from per-(level, shard) item counts made on the GPU by k_items;
 the host holds the same enumeration twice (count_level_items, the fast row walk, and the generic
@@ -40,8 +43,10 @@ print(json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("mode", [{"CCJ_CHECK_ITEMS": "1"}, {"CCJ_HOST_COUNT": "1", "CCJ_CHECK_ITEMS": "1"}],
-                         ids=["gpu-count-checked", "host-count"])
+@pytest.mark.parametrize("mode", [{"CCJ_CHECK_ITEMS": "1"},
+                                  {"CCJ_HOST_COUNT": "1", "CCJ_CHECK_ITEMS": "1"},
+                                  {"CCJ_ILOOP_TILES": "1"}],
+                         ids=["items-gpu-count-checked", "items-host-count", "tiles"])
 def test_item_counts_agree_and_fold_matches_reference(mode):
     env = dict(os.environ, **mode)
     cases = [{k: c[k] for k in ("tag", "seq", "dangles", "params", "noGU")} for c in CASES]

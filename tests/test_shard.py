@@ -8,6 +8,9 @@
   (nmax = the largest rank's block count), the slices are all-gathered as ONE collective per level
   (the RCCL path does the same on the GPU), and unpacking the other ranks' slices must rebuild the
   level exactly as one process writes it.
+* 2-D spans: interval i of every span belongs to rank (i-1) % world (k_diag2d); the exchange of
+  level t also carries span t (k_dtail_pack / k_dtail_unpack: V, Vt, P, WBP, WPP, WM, WMv, WMp ... of
+  the rank's own intervals), and unpacking must give every rank the whole span.
 * P terms: each rank pushes only its share of the terms of P(i, i+sigma) (k_ppush outer index
   jo / d-j-1 taken r, r+G, ...), as (value + 2^31) << 32 | first-split key words; the tail of the
   exchange of level sigma-2 carries them and the minimum over the ranks must be the reference's P
@@ -139,6 +142,15 @@ def _p_partials(fold, n, sigma, world, rank):
     return out
 
 
+def _span_tail(fold, n, sigma, world, rank):
+    """k_dtail_pack: the 2-D values (oracle get2 ids 0..7) of this rank's intervals of span sigma."""
+    tail = np.zeros((8, n + 1), dtype=np.int32)
+    for i in range(1, n - sigma + 1):
+        if (i - 1) % world == rank:
+            tail[:, i] = [fold.get2(x, i, i + sigma) for x in range(8)]
+    return tail
+
+
 def _gloo_body(rank, world, n, seq, torch, dist):
     from ccj_amd import shard_blocks
     fold = OracleFold(seq, blob("Turner04"), 2, 0)
@@ -150,14 +162,22 @@ def _gloo_body(rank, world, n, seq, torch, dist):
         sig = t + 2  # the P span whose partials ride this exchange (pushed after level t-1)
         tail = _p_partials(fold, n, sig, world, rank) if 1 <= t and sig <= n - 1 else np.zeros(n + 1, np.uint64)
         body = _pack(level, C, M, mine, nmax).view(np.uint8)
-        own = torch.from_numpy(np.concatenate([body, np.zeros((-len(body)) % 8, np.uint8), tail.view(np.uint8)]))
+        span = _span_tail(fold, n, t, world, rank)
+        own = torch.from_numpy(np.concatenate([body, np.zeros((-len(body)) % 8, np.uint8), tail.view(np.uint8),
+                                               span.reshape(-1).view(np.uint8)]))
         parts = [torch.empty_like(own) for _ in range(world)]
-        dist.all_gather(parts, own)  # ONE collective per level: cells + P tail
+        dist.all_gather(parts, own)  # ONE collective per level: cells + P tail + span t
         nb = len(body) + (-len(body)) % 8
         slices = [p[:len(body)].numpy().view(np.int16) for p in parts]
         _unpack(level, C, M, slices, world, rank, t, nmax, shard_blocks, n)
         full, _, _ = _level(n, t, fold, range(t + 1))
         ok &= bool(np.array_equal(level, full))
+        # k_dtail_unpack: each interval from its owner's slice; the whole span on every rank
+        st = nb + 8 * (n + 1)
+        spans = [p[st:].numpy().view(np.int32).reshape(8, n + 1) for p in parts]
+        for i in range(1, n - t + 1):
+            got = spans[(i - 1) % world][:, i]
+            ok &= all(int(got[x]) == fold.get2(x, i, i + t) for x in range(8))
         if 1 <= t and sig <= n - 1:
             comb = np.minimum.reduce([p[nb:].numpy().view(np.uint64) for p in parts])
             for i in range(1, n - sig + 1):
