@@ -66,7 +66,9 @@ struct DV {
         }
         const int t = (j - i) + (l - k), m = n - t - 2, h = k - j - 2, a = j - i;
         const LvlDev L = T.ld[t];
-        return (int)T.d4[L.lb + (long long)x * L.C + (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) + i - 1];
+        const long long cell = (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) + i - 1;
+        if (!T.mat5 && rec_only(x)) return rec_get(T, x, L, cell);  // record-only matrix (ccj_engine.h)
+        return (int)T.d4[L.lb + (long long)x * L.C + cell];
     }
     __device__ __forceinline__ bool can_pair(int i, int j) const { return (j - i > TURN) && pr(i, j) > 0; }  // pseudo_loop.hh:131-135
     // pseudo_loop.cc:822-840 (lrint = round-half-even in double)

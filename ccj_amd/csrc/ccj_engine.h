@@ -163,6 +163,7 @@ struct DevTables {
     const unsigned long long *pb;  // pairability bits: [w][pbw words], bit p of row w = pt(p, p+w) > 0
     int pbw;                       // 64-bit words per row (positions 0 .. n+1, plus one zero word)
     int16_t *ieO, *ieI;            // k_iltile energy blocks: [w][p][848] by closing pair / by inner pair
+    int mat5;                      // 1: the 5 record-only matrices are stored in d4 too (band-sharded exchange)
     uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
     int *err;                      // device error word
     // split-point sharing (above): levels [g_lo, g_hi) share; partial-record ring of SHARE_R
@@ -178,6 +179,23 @@ struct DevTables {
     uint4 *acc;
     long long accC;
 };
+
+// The 5 matrices no fill kernel reads back as matrices (PLmloop00, PMmloop00, POmloop00, PfromMprime,
+// PRmloop00) live only in the loop records (RA / RK), unless DevTables::mat5: the level kernel skips
+// their d4 stores.  rec_get reads one from the record of the cell at in-level offset
+// cell (a*M + G(h) + i-1); k_mat5 writes them into d4 where a host mirror needs them.
+__host__ __device__ __forceinline__ bool rec_only(int x) {
+    return x == PLmloop00 || x == PMmloop00 || x == POmloop00 || x == PfromMprime || x == PRmloop00;
+}
+__device__ __forceinline__ int rec_get(const DevTables &T, int x, const LvlDev &L, long long cell) {
+    const uint4 *rp = T.rec + L.lr;
+    if (x == PRmloop00) return (int)(int16_t)(rp[L.C + cell].x & 0xffffu);  // RK: Rm00 | Mm00
+    const uint4 r = rp[cell];                                                // RA: Lm00|Mm00, Om00|fL, fO|Lm10, fMp|K
+    if (x == PLmloop00) return (int)(int16_t)(r.x & 0xffffu);
+    if (x == PMmloop00) return (int)(int16_t)(r.x >> 16);
+    if (x == POmloop00) return (int)(int16_t)(r.y & 0xffffu);
+    return (int)(int16_t)(r.w & 0xffffu);                                    // PfromMprime
+}
 
 // element offset of cell (a,h,i) of matrix x inside level t (relative to lv[t].base)
 inline int64_t cell_offset_host(const LevelDesc &L, int x, int a, int h, int i) {
@@ -210,4 +228,5 @@ int ccjk_ptail_unpack(const ccj::DevTables *T, int sigma, const int16_t *recv, s
 int ccjk_items(const ccj::DevTables *T, int G, int rank, int simulate, long long *counts, const long long *offs,
                uint32_t *items, int pass, void *stream);
 int ccjk_canon(const ccj::DevTables *T, int x, const long long *offij, int16_t *out, void *stream);
+int ccjk_mat5(const ccj::DevTables *T, int t, void *stream);
 }

@@ -1981,6 +1981,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.items = c->d_items;
     T.tiles = c->d_tiles;
     T.pb = c->d_pb;
+    // the exchange packs all 22 matrices from d4; CCJ_MAT5=1 stores them in every fill (A/B timing)
+    T.mat5 = ((c->world > 1 && !c->simulate) || (getenv("CCJ_MAT5") && atoi(getenv("CCJ_MAT5")) != 0)) ? 1 : 0;
     T.ieO = c->d_ieO;
     T.ieI = c->d_ieI;
     T.pbw = c->pbw;
@@ -2198,6 +2200,7 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                 }
             }
             HIPCHK(c, trec(5, st));
+            if (c->overlap && c->h4 && !c->T.mat5) HIPCHK(c, (hipError_t)ccjk_mat5(&c->T, s, st));  // for the mirror copy
             HIPCHK(c, hipEventRecord(c->lev_done[s], st));
             if (c->overlap && c->h4) {
                 // stream the finished level to the pinned host mirror while later levels run
@@ -2334,6 +2337,10 @@ extern "C" int ccj_sync_host(ccj_ctx *c) {
     } else if (c->total4 > 0) {
         if (!c->h4 && hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
             return set_err(c, CCJ_E_OOM, "pinned host allocation of %.2f GB failed", c->total4 * 2e-9);
+        if (!c->T.mat5) {  // the record-only matrices into d4 first (ccj_engine.h rec_only)
+            for (int t = 0; t < c->nlev; ++t) HIPCHK(c, (hipError_t)ccjk_mat5(&c->T, t, c->st));
+            HIPCHK(c, hipStreamSynchronize(c->st));
+        }
         HIPCHK(c, hipMemcpy(c->h4, c->d4, (size_t)c->total4 * sizeof(int16_t), hipMemcpyDeviceToHost));
     }
     HIPCHK(c, hipMemcpy(c->h2i.data(), c->d2i, A2_N * plane * sizeof(int), hipMemcpyDeviceToHost));

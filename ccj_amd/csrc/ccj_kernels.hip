@@ -392,16 +392,19 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
     const int partB = (int)blockIdx.x >= blocksA;
     // wave-uniform (readfirstlane: lets the compiler keep every index below in SGPRs)
     const int item = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - (partB ? blocksA : 0)) * 4 + (int)(threadIdx.x >> 6));
-    // item = (pair * ngrp + g) * nout + own outer; outer = jo (part A) / a2 (part B), rank r of G
+    // item = (pair * nout + own outer) * ngrp + g; outer = jo (part A) / a2 (part B), rank r of G
     // taking outer = r, r+G, ... (band sharding: every rank pushes its share of the terms into its
     // own T.Pk and the P spans are min-combined in the level exchange); pair = one
     // (chunk c of PP_S spans, slice hs = [hs*hs_len, +hs_len) of the inner loop h1 / h2), so long
     // loops spread over waves.  Chunk c's inner loop runs over h < min((c+1)*PP_S, nmax), so it has
     // ceil(that / hs_len) slices; the pairs are enumerated chunk by chunk (part A's count, nmax).
-    const int outer = rank + G * (item % nout);
-    int pr = item / nout;
-    const int g = pr % ngrp;
-    pr /= ngrp;
+    // g (64 consecutive intervals) varies fastest, so the 4 waves of a workgroup read adjacent
+    // segments of the same operand rows: the 128-byte lines a misaligned segment straddles are
+    // shared inside one CU (and its XCD's L2) instead of fetched by two XCDs.
+    const int g = item % ngrp;
+    int pr = item / ngrp;
+    const int outer = rank + G * (pr % nout);
+    pr /= nout;
     if (pr >= npairs) return;  // whole wave
     const int nmax = imin(lev, n - 4 - lev) + 1;
     int c = 0;
@@ -2186,28 +2189,18 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     dst[PfromL * C] = (int16_t)clamp_store(vPfromL);
     dst[PfromR * C] = (int16_t)clamp_store(vPfromR);
     dst[PfromM * C] = (int16_t)clamp_store(vPfromM);
-#ifndef CCJ_ABLATE_NOMAT5  // timing only: the 5 matrices no fill kernel reads back (they live in the records)
-    dst[PfromMprime * C] = (int16_t)clamp_store(vPfromMp);
-#endif
+    if (T.mat5) dst[PfromMprime * C] = (int16_t)clamp_store(vPfromMp);  // record-only (ccj_engine.h rec_only)
     dst[PfromO * C] = (int16_t)clamp_store(vPfromO);
-#ifndef CCJ_ABLATE_NOMAT5
-    dst[PLmloop00 * C] = (int16_t)clamp_store(vPLm00);
-#endif
+    if (T.mat5) dst[PLmloop00 * C] = (int16_t)clamp_store(vPLm00);  // record-only (ccj_engine.h rec_only)
     dst[PLmloop01 * C] = (int16_t)clamp_store(vPLm01);
     dst[PLmloop10 * C] = (int16_t)clamp_store(vPLm10);
-#ifndef CCJ_ABLATE_NOMAT5
-    dst[PRmloop00 * C] = (int16_t)clamp_store(vPRm00);
-#endif
+    if (T.mat5) dst[PRmloop00 * C] = (int16_t)clamp_store(vPRm00);  // record-only (ccj_engine.h rec_only)
     dst[PRmloop01 * C] = (int16_t)clamp_store(vPRm01);
     dst[PRmloop10 * C] = (int16_t)clamp_store(vPRm10);
-#ifndef CCJ_ABLATE_NOMAT5
-    dst[PMmloop00 * C] = (int16_t)clamp_store(vPMm00);
-#endif
+    if (T.mat5) dst[PMmloop00 * C] = (int16_t)clamp_store(vPMm00);  // record-only (ccj_engine.h rec_only)
     dst[PMmloop01 * C] = (int16_t)clamp_store(vPMm01);
     dst[PMmloop10 * C] = (int16_t)clamp_store(vPMm10);
-#ifndef CCJ_ABLATE_NOMAT5
-    dst[POmloop00 * C] = (int16_t)clamp_store(vPOm00);
-#endif
+    if (T.mat5) dst[POmloop00 * C] = (int16_t)clamp_store(vPOm00);  // record-only (ccj_engine.h rec_only)
     dst[POmloop01 * C] = (int16_t)clamp_store(vPOm01);
     dst[POmloop10 * C] = (int16_t)clamp_store(vPOm10);
     // loop records and interior-loop copies (the copies only where a later k_iloop can read them:
@@ -2512,7 +2505,25 @@ __global__ __launch_bounds__(256) void k_canon(DevTables T, int x, int t, const 
     const int i = c - Gh + 1, j = i + a, k = j + h + 2, l = k + (t - a);
     const long long u = k - (j + 2);
     const long long pos = offij[(long long)i * (n + 1) + j] + u * (n + 1) - u * (2LL * j + 3 + u) / 2 + (l - k);
-    out[pos] = T.d4[L.lb + (long long)x * L.C + cidx];
+    out[pos] = (int16_t)((!T.mat5 && rec_only(x)) ? rec_get(T, x, L, cidx) : (int)T.d4[L.lb + (long long)x * L.C + cidx]);
+}
+
+// the record-only matrices of level t written into d4 (for a host mirror of d4)
+__global__ __launch_bounds__(256) void k_mat5(DevTables T, int t) {
+    const LvlDev L = T.ld[t];
+    const long long cidx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cidx >= (long long)L.C) return;
+    const int xs[5] = {PLmloop00, PMmloop00, POmloop00, PfromMprime, PRmloop00};
+#pragma unroll
+    for (int q = 0; q < 5; ++q) T.d4[L.lb + (long long)xs[q] * L.C + cidx] = (int16_t)rec_get(T, xs[q], L, cidx);
+}
+
+extern "C" int ccjk_mat5(const DevTables *T, int t, void *stream) {
+    const int m = T->n - t - 2;
+    if (m <= 0 || t >= T->nlev) return 0;
+    const long long C = (long long)(t + 1) * (m * (m + 1) / 2);
+    hipLaunchKernelGGL(k_mat5, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t);
+    return (int)hipGetLastError();
 }
 
 extern "C" int ccjk_canon(const DevTables *T, int x, const long long *offij, int16_t *out, void *stream) {

@@ -179,6 +179,31 @@ __device__ __forceinline__ double ordered_sum(double acc, int N, int lane, F ter
     return acc;
 }
 
+// The same ordered sum with the terms of PF_DR rounds (PF_DR x 64 terms) evaluated first, so
+// their loads are in flight together; then the serial additions in term order (identical bits).
+#ifndef CCJ_PF_DR
+#define CCJ_PF_DR 8
+#endif
+constexpr int PF_DR = CCJ_PF_DR;
+template <class F>
+__device__ __forceinline__ double ordered_sum_deep(double acc, int N, int lane, F term) {
+    for (int q0 = 0; q0 < N; q0 += 64 * PF_DR) {
+        double x[PF_DR];
+#pragma unroll
+        for (int r = 0; r < PF_DR; ++r) {
+            const int q = q0 + r * 64 + lane;
+            x[r] = q < N ? term(q) : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < PF_DR; ++r) {
+            const int base = q0 + r * 64;
+            const int cnt = imin(64, N - base);
+            for (int u = 0; u < cnt; ++u) acc += rdlane(x[r], u);
+        }
+    }
+    return acc;
+}
+
 __global__ __launch_bounds__(64) void k_pf_diag(PfDev D, int s) {
     const PfG G{D};
     const PfExp &E = *D.E;
@@ -193,24 +218,28 @@ __global__ __launch_bounds__(64) void k_pf_diag(PfDev D, int s) {
     // compute_energy (part_func.cc:290-300): V = hairpin + interior loops + VM
     double v_ij;
     {
-        double vi = 0;  // compute_internal :222-240: k = i+1..max_k, l = j-1 down to min_l
+        // compute_internal :222-240: k = i+1..max_k, l = j-1 down to min_l, as ONE ordered sum over
+        // the flattened (k, l) terms (k-major; for k = i+1+kk there are s-1-c0-kk of them,
+        // c0 = max(TURN+1, s-MAXLOOP-2)), so every term's loads go out before the serial additions
         const int max_k = imin(j - TURN - 2, i + MAXLOOP + 1);
         const int tc = G.pt(i, j);
-        for (int k = i + 1; k <= max_k; ++k) {
-            const int min_l = imax(k + TURN + 1 + MAXLOOP + 2, k + j - i) - MAXLOOP - 2;
-            vi = ordered_sum(vi, j - min_l, lane, [&](int u) {
-                const int l = j - 1 - u;
-                double x = G.d2(D.V, k, l) *
-                           exp_E_IntLoop_pf(E, k - i - 1, j - l - 1, tc, D.rtype[G.pt(k, l)], S1[i + 1], S1[j - 1], S1[k - 1], S1[l + 1]);
-                x *= 1.0;  // scale[u1+u2+2]
-                return x;
-            });
-        }
+        const int c0 = imax(TURN + 1, s - MAXLOOP - 2), nkk = imax(0, max_k - i), c1 = s - 1 - c0;
+        int nterm = 0;
+        for (int kk = 0; kk < nkk && c1 - kk > 0; ++kk) nterm += c1 - kk;
+        const double vi = ordered_sum_deep(0.0, nterm, lane, [&](int q) {
+            int kk = 0;
+            while (q >= c1 - kk) { q -= c1 - kk; ++kk; }
+            const int k = i + 1 + kk, l = j - 1 - q;
+            double x = G.d2(D.V, k, l) *
+                       exp_E_IntLoop_pf(E, k - i - 1, j - l - 1, tc, D.rtype[G.pt(k, l)], S1[i + 1], S1[j - 1], S1[k - 1], S1[l + 1]);
+            x *= 1.0;  // scale[u1+u2+2]
+            return x;
+        });
         // compute_energy_VM :276-288, exp_Mbloop :203-212; three terms per k, in order
         const int tt = D.pair[S[j] * 8 + S[i]];
         const double mb = dang ? exp_E_MLstem_pf(E, tt, j < n ? S[j - 1] : -1, i > 1 ? S[i + 1] : -1) : exp_E_MLstem_pf(E, tt, -1, -1);
         const int nk = imax(0, j - TURN - 1 - i);  // k = i+1 .. j-TURN-1
-        double vm = ordered_sum(0.0, 3 * nk, lane, [&](int q) {
+        double vm = ordered_sum_deep(0.0, 3 * nk, lane, [&](int q) {
             const int k = i + 1 + q / 3, w = q % 3;
             const double wmp = G.g2(D.WMp, k, j - 1);
             if (w == 0) return G.g2(D.WM, i + 1, k - 1) * G.g2(D.WMv, k, j - 1) * mb * E.MLclosing;
@@ -234,7 +263,7 @@ __global__ __launch_bounds__(64) void k_pf_diag(PfDev D, int s) {
     const int nd = j - i;  // d = i .. j-1, two terms each
     double wbp;
     {   // compute_WBP :361-370
-        double c = ordered_sum(0.0, 2 * nd, lane, [&](int q) {
+        double c = ordered_sum_deep(0.0, 2 * nd, lane, [&](int q) {
             const int d = i + q / 2;
             if ((q & 1) == 0) return (d == i ? v_ij : G.d2(D.V, d, j)) * E.bp * E.PPS;
             return (d == i ? p : G.d2(D.P, d, j)) * E.PSM * E.PPS;
@@ -244,7 +273,7 @@ __global__ __launch_bounds__(64) void k_pf_diag(PfDev D, int s) {
         if (lane == 0) D.WBP[ij] = c;
     }
     {   // compute_WPP :372-381 (its last term reads WBP)
-        double w = ordered_sum(0.0, 2 * nd, lane, [&](int q) {
+        double w = ordered_sum_deep(0.0, 2 * nd, lane, [&](int q) {
             const int d = i + q / 2;
             const double wp = G.WP(i, d - 1);
             if ((q & 1) == 0) return wp * (d == i ? v_ij : G.d2(D.V, d, j)) * 1.0 * E.PPS;
@@ -269,7 +298,7 @@ __global__ __launch_bounds__(64) void k_pf_diag(PfDev D, int s) {
     // compute_energy_WM (:258-274): k = i .. j-TURN-1, four terms each
     if (!(j - i + 1 < 4)) {
         const int nk = j - TURN - i;
-        double c = ordered_sum(0.0, 4 * nk, lane, [&](int q) {
+        double c = ordered_sum_deep(0.0, 4 * nk, lane, [&](int q) {
             const int k = i + q / 4, w = q % 4;
             const int tk = G.pt(k, j);
             const double mls = k == i ? mls_ij
