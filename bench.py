@@ -241,11 +241,21 @@ def pf_bench(a, rank, world, dist, barrier, dev=0):
     nl = {"k_pf_iloop": max(a.n - 2, 1), "k_pf_level": max(a.n - 2, 1), "k_pf_pterm": max(a.n - 3, 1),
           "k_pf_diag": a.n}
 
+    # HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this workload
+    # (tools/gpu_pf_prof.sh -> tools/make_profiles.py --pf), when committed
+    tj, tname = find_traffic(a.n, a.seed, a.params, pf=True) if world == 1 else (None, None)
+
     def roof(k):
         ms = kms[k]
         gbs = work[k] / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+        avg_s = ms / 1e3 / nl[k]
+        tk = tj["kernels"].get(k) if tj else None
+        traffic = tk["hbm_bytes_per_launch"] if tk else None
         return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-                "traffic": None, "kernel": k, "launches_per_fold": nl[k], "avg_launch_us": ms * 1e3 / nl[k],
+                "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": f"profiles/{tname}" if tk else None,
+                "frac_counter": traffic / avg_s / 1e9 / HBM_PEAK_GBS if traffic and avg_s > 0 else None,
+                "kernel": k, "launches_per_fold": nl[k], "avg_launch_us": avg_s * 1e6,
                 "algorithmic_bytes_per_fold": work[k], "kernel_ms_per_fold": ms}
     dom = max(kms, key=kms.get)
     out = {
@@ -301,16 +311,16 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-def find_traffic(n, seed, params):
+def find_traffic(n, seed, params, pf=False):
     """The committed rocprofv3 FETCH_SIZE/WRITE_SIZE summary (tools/make_profiles.py) of this exact
-    workload: profiles/traffic*.json whose "config" is (n, seed, params); the untagged
-    profiles/traffic.json of rounds 1-3 is the headline n=200 seed 5 Turner04 fold."""
+    workload: profiles/traffic*.json whose "config" is (n, seed, params) and whose "pf" flag is pf;
+    the untagged profiles/traffic.json of rounds 1-3 is the headline n=200 seed 5 Turner04 fold."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic*.json"))):
         with open(path) as f:
             tj = json.load(f)
         cfg = tj.get("config", {"n": 200, "seed": 5, "params": "Turner04"})
-        if (cfg.get("n"), cfg.get("seed"), cfg.get("params")) == (n, seed, params) and not tj.get("pf"):
+        if (cfg.get("n"), cfg.get("seed"), cfg.get("params")) == (n, seed, params) and bool(tj.get("pf")) == pf:
             return tj, os.path.basename(path)
     return None, None
 

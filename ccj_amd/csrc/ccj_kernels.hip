@@ -2017,7 +2017,9 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 const unsigned idx = (unsigned)(a * Mf) + L0 - (unsigned)(h * r);
                 CHKA(idx);
                 ring[(long long)AL * T.accC + idx] = pack_acc(AL_[r], 8);
-                ((int16_t *)(ring + (long long)AK * T.accC + idx))[6] = (int16_t)clamp_store(AL_[r][8]);
+                // bytes 12..15 of AK (slot 6 and the unused slot 7): with the k side's 12 bytes the
+                // whole 16-byte record is written (measured equal to a 2-byte store of slot 6)
+                ((unsigned *)(ring + (long long)AK * T.accC + idx))[3] = pk16(clamp_store(AL_[r][8]), INTERN_INF);
             }
         }
     };

@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--params", default="Turner04")
     ap.add_argument("--traffic-only", action="store_true", help="only the PMC summary (no stats/bench/spans)")
+    ap.add_argument("--pf", action="store_true", help="the partition-function fill (bench.py --pf)")
     a = ap.parse_args()
     rnd, prof = a.round, a.prof
     out = os.path.join(ROOT, "profiles")
@@ -98,11 +99,11 @@ def main():
             f.write(line + "\n")
     fe = pmc(os.path.join(prof, "fetch", "f_counter_collection.csv"), "FETCH_SIZE")
     wr = pmc(os.path.join(prof, "write", "w_counter_collection.csv"), "WRITE_SIZE")
-    cmd = "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+    cmd = "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline" + (" --pf" if a.pf else "")
     if not headline:
         cmd += f" --n {a.n} --seed {a.seed} --params {a.params}"
     traffic = {"round": rnd, "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- " + cmd,
-               "config": {"n": a.n, "seed": a.seed, "params": a.params},
+               "config": {"n": a.n, "seed": a.seed, "params": a.params}, "pf": a.pf,
                "fetch_factor": FETCH_FACTOR, "write_factor": WRITE_FACTOR, "kernels": {}}
     for k in sorted(set(fe) | set(wr)):
         fb, fl = fe.get(k, (0.0, 1))
@@ -110,7 +111,8 @@ def main():
         traffic["kernels"][k] = {"launches": fl, "read_bytes_per_launch": FETCH_FACTOR * fb / max(fl, 1),
                                  "write_bytes_per_launch": WRITE_FACTOR * wb / max(wl, 1),
                                  "hbm_bytes_per_launch": FETCH_FACTOR * fb / max(fl, 1) + WRITE_FACTOR * wb / max(wl, 1)}
-    name = "traffic.json" if headline else f"traffic_n{a.n}_s{a.seed}_{a.params}.json"
+    name = ("traffic.json" if headline else f"traffic_n{a.n}_s{a.seed}_{a.params}.json") if not a.pf else \
+        f"traffic_pf_n{a.n}_s{a.seed}_{a.params}.json"
     with open(os.path.join(out, name), "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(traffic, indent=1))
