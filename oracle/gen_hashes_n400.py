@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from tests.oracle_lib import HASH_NAMES, blob, oracle_lib  # noqa: E402
 
-CASES = [("t04_400_seed6", 6, 400, "Turner04")]
+CASES = [("t04_400_seed6", 6, 400, "Turner04"), ("t04_400_seed7", 7, 400, "Turner04")]
 
 
 def seq(seed, n):
@@ -31,14 +31,23 @@ def seq(seed, n):
 
 
 def main():
+    """python oracle/gen_hashes_n400.py [tag ...]: (re)computes the named cases (default: all) and
+    keeps the other cases already in the fixture."""
     L = oracle_lib()
     os.environ["CCJ_ORACLE_PROGRESS"] = "1"
     out_path = os.path.join(ROOT, "tests", "golden", "hashes_n400.json")
+    want = sys.argv[1:] or [c[0] for c in CASES]
     out = []
+    if os.path.exists(out_path):
+        with open(out_path) as f:
+            out = [c for c in json.load(f) if c["tag"] not in want]
+    nthr = int(os.environ.get("CCJ_ORACLE_THREADS", "0")) or os.cpu_count() or 8
     for tag, s, n, params in CASES:
+        if tag not in want:
+            continue
         b = ctypes.create_string_buffer(blob(params))
         t0 = time.time()
-        h = L.ccj_oracle_fold_par(seq(s, n).encode(), b, 2, 0, os.cpu_count() or 8)
+        h = L.ccj_oracle_fold_par(seq(s, n).encode(), b, 2, 0, nthr)
         if not h:
             raise MemoryError("oracle allocation failed")
         t1 = time.time()
@@ -47,11 +56,12 @@ def main():
         out.append({"tag": tag, "seed": s, "n": n, "seq": seq(s, n), "params": params, "dangles": 2, "noGU": 0,
                     "source": "oracle/ccj_oracle.c ccj_oracle_fold_par (restatement-pinned, not a reference run)",
                     "hashes": {HASH_NAMES[i]: "%016x" % hv[i] for i in range(31)},
-                    "mfe": L.ccj_oracle_W(h, n), "oracle_seconds": t1 - t0, "threads": os.cpu_count()})
+                    "mfe": L.ccj_oracle_W(h, n), "oracle_seconds": t1 - t0, "threads": nthr})
         L.ccj_oracle_free(h)
         print(tag, "done in %.0f s, mfe %d" % (t1 - t0, out[-1]["mfe"]), flush=True)
-    with open(out_path, "w") as f:
-        json.dump(out, f, indent=1)
+        out.sort(key=lambda c: c["seed"])
+        with open(out_path, "w") as f:
+            json.dump(out, f, indent=1)
     print("wrote", out_path)
 
 
