@@ -9,6 +9,9 @@ import csv, glob
 for f in sorted(glob.glob("gpurun_out/calib/*/*_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         kb = float(r["Counter_Value"])
-        print(f'{r["Kernel_Name"][:40]:40s} {r["Counter_Name"]:11s} {kb*1024/2**30:.3f} x 1GiB')
+        if r["Kernel_Name"].startswith("k_window"):
+            print(f'{r["Kernel_Name"][:40]:40s} {r["Counter_Name"]:11s} {kb*1024/262144:.1f} bytes per wave')
+        else:
+            print(f'{r["Kernel_Name"][:40]:40s} {r["Counter_Name"]:11s} {kb*1024/2**30:.3f} x 1GiB')
 PY
 exit $rc
