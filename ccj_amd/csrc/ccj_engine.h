@@ -111,6 +111,26 @@ __host__ __device__ __forceinline__ int shard_ceil(int x, int G, int r) {
     return (q / G) * SHARD_GRP + off;
 }
 
+// k_iltile: a tile is TL_NK consecutive keys x 64 cells, one cell per lane.  The PM
+// tiles are skewed: key kk (J = K0+kk) of tile x holds a = x0 + 64x + lane + kk, so that every key
+// of the tile reads the same 64-element source segment per row.  pm_tile_span: x0 = the smallest
+// a - kk over the tile's keys (J+g <= n, [alo, ahi] non-empty), xn = the number of 64-wide chunks
+// up to the largest a - kk.  Host (build_tiles) and kernel share it.
+constexpr int TL_NK = 16;
+__host__ __device__ inline void pm_tile_span(int n, int t, int g, int K0, int &x0, int &xn) {
+    int lo = 1 << 20, hi = -(1 << 20);
+    for (int kk = 0; kk < TL_NK; ++kk) {
+        const int J = K0 + kk, k = J + g;
+        if (J < 1 || k > n) continue;
+        const int alo = (t - (n - k)) > 2 ? t - (n - k) : 2, ahi = (t - 2) < (J - 1) ? t - 2 : J - 1;
+        if (alo > ahi) continue;
+        lo = (alo - kk) < lo ? alo - kk : lo;
+        hi = (ahi - kk) > hi ? ahi - kk : hi;
+    }
+    x0 = lo;
+    xn = hi >= lo ? (hi - lo) / 64 + 1 : 0;
+}
+
 struct LvlX {        // per-level bases of the interior-loop copies
     long long lbx;  // element offset of level t in d4x: PLx (C_t elements) then PRx (C_t)
     long long pmb;  // element offset of level t in pmx: m_t * n * (t+1) elements
@@ -162,7 +182,7 @@ struct DevTables {
     const uint32_t *tiles;         // k_iltile tiles (role << 30 | block << 20 | first key << 10 | cell chunk)
     const unsigned long long *pb;  // pairability bits: [w][pbw words], bit p of row w = pt(p, p+w) > 0
     int pbw;                       // 64-bit words per row (positions 0 .. n+1, plus one zero word)
-    int16_t *ieO, *ieI;            // k_iltile energy blocks: [w][p][848] by closing pair / by inner pair
+    int *ied;                      // k_iltile energies [type][w][p][dt-3][32] (k_ie_tiles)
     int mat5;                      // 1: the 5 record-only matrices are stored in d4 too (band-sharded exchange)
     uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
     int *err;                      // device error word
@@ -210,7 +230,7 @@ int ccjk_init2d(const ccj::DevTables *T, void *stream);
 int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
 int ccjk_build_il(const ccj::DevTables *T, void *stream);
 int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, int G, int rank, void *stream);
-int ccjk_ie_blocks(const ccj::DevTables *T, void *stream);
+int ccjk_ie_tiles(const ccj::DevTables *T, void *stream);
 int ccjk_iltile(const ccj::DevTables *T, int t, long long first_tile, int ntiles, int G, int rank, void *stream);
 int ccjk_diag2d(const ccj::DevTables *T, int sigma, int G, int rank, void *stream);
 int ccjk_dtail_pack(const ccj::DevTables *T, int sigma, int G, int rank, int16_t *tail, void *stream);

@@ -146,7 +146,7 @@ struct ccj_ctx {
     uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
     uint32_t *d_tiles = nullptr;          // k_iltile tiles, all levels back to back (sequence-independent)
     unsigned long long *d_pb = nullptr;   // pairability bits [w][pbw] (k_iltile)
-    int16_t *d_ieO = nullptr, *d_ieI = nullptr;  // k_iltile loop-energy blocks [w][p][848]
+    int *d_ied = nullptr;                 // k_iltile energies [type][w][p][dt-3][32] (k_ie_tiles)
     int pbw = 0;
     std::vector<long long> tl_off;        // first tile of (level t, shard r) at t*world + r
     bool il_tiles = false;                // CCJ_ILOOP_TILES=1: interior loops as LDS tiles (k_iltile, slower)
@@ -1465,14 +1465,16 @@ static int local_allgather(ccj_ctx *c, size_t slice) {
 
 // k_iltile's tiles (ccj_kernels.hip), per level t and shard r in that order: one 32-bit word per
 // tile, role << 30 | block << 20 | first key << 10 | cell chunk (TL_NK keys x 64 cells):
-//   PL: own a in [6, t], keys i from 1 by 16 (i <= m), chunks of h over [0, m-i]
+//   PL: own a in [6, t], keys i from 1 by 16 (i <= m), chunks of h over [0, m-i] (skewed: key kk
+//       of chunk x holds h = 64x + lane - kk)
 //   PR: own a in [0, t-6], keys q from 0 by 16 (q <= m-1), chunks of i over [1, q+1]
-//   PM: h in [2, m-1], keys j from 1 by 16 (j+h+2 <= n), chunks of a over the keys' [alo, ahi]
+//   PM: h in [2, m-1], keys j from 1 by 16 (j+h+2 <= n), skewed chunks of a over the keys' [alo, ahi]
 //       (every rank walks every a; each stores only its own)
-// They depend only on n and the sharding, so they are built once per context.
+// Within a (level, shard) the tiles run longest first.  They depend only on n and the sharding, so
+// they are built once per context.
 static void build_tiles(int n, int nlev, int G, int rank, bool simulate, std::vector<uint32_t> &tiles,
                         std::vector<long long> &off) {
-    constexpr int NK = 16, NC = 64;
+    constexpr int NK = TL_NK, NC = 64;
     tiles.clear();
     off.assign((size_t)n * G + 1, 0);
     auto push = [&](int role, int blk, int K0, int xc) {
@@ -1498,12 +1500,20 @@ static void build_tiles(int n, int nlev, int G, int rank, bool simulate, std::ve
             for (int h = 2; h <= m - 1; ++h) {
                 const int g = h + 2;
                 for (int K0 = 1; K0 + g <= n; K0 += NK) {
-                    const int Kend = std::min(K0 + NK - 1, n - g);
-                    const int amin = std::max(2, t - (n - (K0 + g))), amax = std::min(t - 2, Kend - 1);
-                    if (amin > amax) continue;
-                    for (int xc = (amin - 2) / NC; xc <= (amax - 2) / NC; ++xc) push(2, h, K0, xc);
+                    int x0, xn;  // skewed chunks (ccj_engine.h pm_tile_span)
+                    pm_tile_span(n, t, g, K0, x0, xn);
+                    for (int xc = 0; xc < xn; ++xc) push(2, h, K0, xc);
                 }
             }
+            // longest first (the number of source-level distances a tile walks), so the short
+            // tiles fill in behind the long ones
+            auto ndt = [&](uint32_t w) {
+                const int role = (int)(w >> 30), blk = (int)((w >> 20) & 1023u);
+                const int hi = role == 0 ? blk - 4 : role == 1 ? t - blk - 4 : t - 2;
+                return std::max(0, std::min(58, hi) - 2);
+            };
+            std::stable_sort(tiles.begin() + off[(size_t)t * G + r], tiles.end(),
+                             [&](uint32_t x, uint32_t y) { return ndt(x) > ndt(y); });
         }
     off[(size_t)n * G] = (long long)tiles.size();
 }
@@ -1865,17 +1875,19 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         const size_t pad = 256;
         c->nx = ox;
         c->npm = op;
-        if (hipMalloc(&c->d4x_alloc, ((size_t)ox + pad) * sizeof(int16_t)) != hipSuccess ||
-            hipMalloc(&c->pmx_alloc, ((size_t)op + pad) * sizeof(int16_t)) != hipSuccess)
+        // pad elements on both sides: k_iltile's row loads start up to ~50 elements before a
+        // copy's first row and end up to 63 past its last (those lanes' values are never used)
+        if (hipMalloc(&c->d4x_alloc, ((size_t)ox + 2 * pad) * sizeof(int16_t)) != hipSuccess ||
+            hipMalloc(&c->pmx_alloc, ((size_t)op + 2 * pad) * sizeof(int16_t)) != hipSuccess)
             return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for interior-loop copies failed", (ox + op) * 2e-9);
-        c->d4x = c->d4x_alloc;
-        c->pmx = c->pmx_alloc;
+        c->d4x = c->d4x_alloc + pad;
+        c->pmx = c->pmx_alloc + pad;
         HIPCHK(cp, hipMalloc(&c->d_ldx, ldx.size() * sizeof(LvlX)));
         HIPCHK(cp, hipMemcpy(c->d_ldx, ldx.data(), ldx.size() * sizeof(LvlX), hipMemcpyHostToDevice));
         if (c->il_tiles) {
-            const size_t eb = (size_t)(n + 1) * c->rs * 848;
-            if (hipMalloc(&c->d_ieO, eb * sizeof(int16_t)) != hipSuccess || hipMalloc(&c->d_ieI, eb * sizeof(int16_t)) != hipSuccess)
-                return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for the interior-loop energy blocks failed", eb * 4e-9);
+            const size_t eb = 2 * (size_t)(n + 1) * c->rs * 56 * 32;  // ccj_kernels.hip TL_KEYW per key
+            if (hipMalloc(&c->d_ied, eb * sizeof(int)) != hipSuccess)
+                return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for the interior-loop energy rows failed", eb * 4e-9);
             std::vector<uint32_t> tiles;
             build_tiles(n, c->nlev, c->world, c->rank, c->simulate, tiles, c->tl_off);
             HIPCHK(cp, hipMalloc(&c->d_tiles, std::max<size_t>(tiles.size(), 1) * sizeof(uint32_t)));
@@ -1983,8 +1995,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.pb = c->d_pb;
     // the exchange packs all 22 matrices from d4; CCJ_MAT5=1 stores them in every fill (A/B timing)
     T.mat5 = ((c->world > 1 && !c->simulate) || (getenv("CCJ_MAT5") && atoi(getenv("CCJ_MAT5")) != 0)) ? 1 : 0;
-    T.ieO = c->d_ieO;
-    T.ieI = c->d_ieI;
+    T.ied = c->d_ied;
     T.pbw = c->pbw;
     T.ilseg = c->d_ilseg;
     T.ilmseg = c->d_ilmseg;
@@ -2089,7 +2100,7 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     HIPCHK(c, (hipError_t)ccjk_init2d(&c->T, st));
     HIPCHK(c, (hipError_t)ccjk_precompute_ie(&c->T, st));
     if (!c->il_tiles) HIPCHK(c, (hipError_t)ccjk_build_il(&c->T, st));
-    else HIPCHK(c, (hipError_t)ccjk_ie_blocks(&c->T, st));
+    else HIPCHK(c, (hipError_t)ccjk_ie_tiles(&c->T, st));
     HIPCHK(c, hipEventRecord(c->ev_pre, st));
     // Four streams:
     //   st_d : k_diag2d(s)  needs P(s) (p_done) and spans < s (stream order)
@@ -2887,8 +2898,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_items);
     hipFree(c->d_tiles);
     hipFree(c->d_pb);
-    hipFree(c->d_ieO);
-    hipFree(c->d_ieI);
+    hipFree(c->d_ied);
     hipFree(c->d_send);
     hipFree(c->d_recv);
     if (c->h_stage) hipHostFree(c->h_stage);

@@ -1051,46 +1051,43 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
 }
 
 // ------------------------------------------------------------------------------------------
-// Interior loops as LDS-staged tiles (k_iltile).  Same minima as k_iloop
-// (get_PLiloop / get_PRiloop / get_PMiloop, pseudo_loop.cc:682-773), organised so that a partner
-// value is fetched once per tile instead of once per closing pair that reads it.  A tile is one
-// 256-thread workgroup: TL_NK consecutive "keys" (closing pairs for PL/PR, the cell's own inner
-// pair for PM) of one role and block, times TL_NC consecutive cells (one per lane):
-//   PL: block a, keys i (pair (i, i+a)),          cells h, partner PLx column  c  = i+1+u1, element h+dt-1-u1
-//   PR: block a, keys q (pair (k, l), k = q+a+3), cells i, partner PRx row     q' = q+1+u1, element i-1
-//   PM: row h,   keys j (pair (j, j+h+2)),        cells a, partner PMx row (h+dt, d = j-1-u1), element a-1-u1
-// For a source-level distance dt = 2+u1+u2 every candidate of every key reads one "source row" R
-// of that dt's copy (TL_NK + #u1 - 1 consecutive rows), and whether the candidate's other pair can
-// pair is a property of R alone (pairability bit table T.pb).  The workgroup stages, for every dt
-// at once (in chunks of dts that fit its LDS), the pairable rows its keys read, 64 + 15 elements
-// each, plus one 29 x 29 loop-energy block per pairable key (T.ieO / T.ieI), so the loads of a
-// whole chunk are in flight together: one memory round trip per chunk, not per dt.  Then each wave
-// walks its keys: per (dt, staged row) one ds_read_u16 (partner), one broadcast ds_read_u16
-// (energy), an add and a min per 64 cells.  Exactly the reference's candidate set: the key's pair
-// can pair, the partner's pair can pair, u1, u2 <= 28, dt <= a-4 / b-4 / t-2, and PM's per-cell
-// d > i, dp < l as a lane mask.  Min is order-independent: bit-identical minima.
-constexpr int TL_NK = 16;               // keys per tile
-constexpr int TL_NC = 64;               // cells per tile (one per lane)
-constexpr int TL_EB = 848;              // int16 per key energy block: 29 x 29 (u1 major) padded to 16 bytes
-constexpr int TL_DTN = 56;              // dt = 3 .. 58
-constexpr int TL_ROWMAX = TL_NK + IE_U - 1;  // 44 source rows per dt at most
-constexpr int TL_B = 8;                 // staging loads (16 bytes per lane) in flight per wave
-constexpr int TL_BIG = 1 << 28;
-constexpr int TL_LDS = 40 * 1024;       // dynamic LDS per tile workgroup (4 per CU)
-// LDS carve (bytes): dt table (+ one word: the number of dt chunks), row lists, the pairable keys'
-// energy blocks, then the staged rows of one dt chunk (the rest)
-constexpr int TL_OFF_NCH = TL_DTN * 16;                          // dt table: mask, first chunk, chunks/row, chunk id
-constexpr int TL_OFF_ROWL = TL_OFF_NCH + 16;
-constexpr int TL_OFF_EB = TL_OFF_ROWL + TL_DTN * 48;             // row list: slot -> row (int8), 48 per dt
+// Interior loops as tiles (k_iltile).  The same minima as k_iloop (get_PLiloop /
+// get_PRiloop / get_PMiloop, pseudo_loop.cc:682-773, source-level distances dt = 3..58; dt = 2 is
+// k_level4d's), organised so that a partner value is fetched once per tile and dt instead of once
+// per closing pair that reads it.  A tile is TL_NK consecutive keys of one role and block times 64
+// cells, one cell per lane:
+//   PL: block a, keys K = i (pair (i, i+a)),           cell h = X0 + lane - kk   (skewed)
+//   PR: block a, keys K = q (pair (k, l), k = q+a+3),  cell i = X0 + lane
+//   PM: row h,   keys K = j (pair (j, j+h+2)),         cell a = X0 + lane + kk   (skewed)
+// For one dt the candidate (key kk, window position j) reads source row r = kk + j of that dt's
+// copy (PL: column i+1+u1, PR: row q+1+u1, PM: row d = j-1-u1; PM numbers j from u1 = u1max
+// down), and with the skew every key reads the SAME 64 elements of a row (PL: h' = X0+lane+dt-1-
+// u1min-r, PR: i-1, PM: a-1-u1 = X0+lane-1-u1max+r).  So a wave stages, per dt, the <= TL_ROWS
+// rows its keys read into LDS with 16-byte loads (only rows whose pair can pair: the reference's
+// can_pair(d, dp) is a property of the row), together with the keys' energies e(kk, dt, j)
+// (T.ied: int32, TL_BIG where the candidate does not exist: the inner pair cannot pair or j is past
+// the window), and then walks acc[kk] = min_j row[kk+j][lane] + e(kk, dt, j): one LDS read, an add
+// and a min per candidate and 64 cells, with no per-candidate bookkeeping.  Rows not staged hold
+// stale int16 values, and their energies are TL_BIG, so they never win.  The TL_W waves of a tile
+// take dt = 3+w, 3+w+TL_W, ... (each stages and walks its own dts, the next dt's loads in flight
+// during the walk) and meet in LDS at the end.  PM's per-cell window (d > i, dp < l, i.e. u1 <=
+// a-2, u2 <= b-2) is a lane mask over rows.  Min is order-independent: bit-identical minima.
+// ------------------------------------------------------------------------------------------
+constexpr int TL_W = 4;                                 // waves per tile
+constexpr int TL_ROWS = TL_NK + IE_U - 1;               // 44 source rows per dt at most
+constexpr int TL_DT0 = 3, TL_DT1 = 2 * (IE_U - 1) + 2;  // dt = 3 .. 58
+constexpr int TL_DTN = TL_DT1 - TL_DT0 + 1;             // 56
+constexpr int TL_EJ = 32;                               // energies per (key, dt); j = 0..28 used
+constexpr int TL_KEYW = TL_DTN * TL_EJ;                 // int32 per key in T.ied
+constexpr int TL_BIG = 1 << 20;
+constexpr int TL_OFF_E = TL_ROWS * 128;                 // per wave: rows [44][64] int16, then
+constexpr int TL_OFF_A = TL_OFF_E + TL_NK * 128;        //   energies [16][32] int32, acc [16][64] int16
+constexpr int TL_WB = TL_OFF_A + TL_NK * 128;           // 9728 bytes per wave
+constexpr int TL_LDS = TL_W * TL_WB;
+constexpr int TL_NLR = (TL_ROWS * 8 + 63) / 64;          // 6 row loads per dt (8 x 16 B per row)
+constexpr int TL_NLE = TL_NK * 8 / 64;                   // 2 energy loads per dt (8 x 16 B per key)
+constexpr int TL_PAD = 128;                              // slack (elements) in front of the copies
 
-__device__ __forceinline__ uint4 ldg_u4(const int16_t *base, long long e, long long lim) {
-    // 16 bytes from element e (any 2-byte alignment; clamped into the allocation: the clamped
-    // values are never used)
-    e = e < 0 ? 0 : (e > lim - 8 ? lim - 8 : e);
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = *(const __attribute__((address_space(1))) u32x4 *)(const char *)(base + e);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
 // bits r in [lo, hi] (lo, hi in [0, 63]; empty when lo > hi)
 __device__ __forceinline__ unsigned long long bit_range(int lo, int hi) {
     if (lo > hi) return 0ull;
@@ -1110,295 +1107,315 @@ __device__ __forceinline__ unsigned long long pbits(const DevTables &T, int w, i
     return x;
 }
 
-struct TlDt {                // one dt of a tile (LDS): 16 bytes
-    unsigned long long mask;  // staged rows r (row R = Rlo + r)
-    int first;                // first 16-byte chunk of the dt's rows inside its dt chunk's row area
-    short ch;                 // chunks per staged row
-    short cid;                // which dt chunk the dt belongs to
+typedef unsigned tl_u32x4 __attribute__((ext_vector_type(4)));
+typedef int tl_i32x4 __attribute__((ext_vector_type(4)));
+
+// One dt of a wave's walk (scalar): the rows to stage and where they come from.
+struct TlDt {
+    unsigned long long mask;  // rows r staged (pair can pair, inside the copy, read by a live key)
+    int nrows, cnt, u1max;
+    long long rbase;          // element index of (row 0, lane 0) minus the row's own offset (below)
+    long long ebase;          // element index in T.ied of key 0's energies for this dt
+    int Rlo, mp, tp1;         // row-offset parameters
 };
 
-// a dt table entry as wave-uniform (scalar) values: every wave reads the same LDS word, and
-// readfirstlane lets the compiler keep the loop control and the level descriptors scalar
-__device__ __forceinline__ TlDt tl_dt(const TlDt *dtab, int di) {
-    const uint4 w = *(const uint4 *)(dtab + di);
+// pairability bits as above, per lane (vector loads)
+__device__ __forceinline__ unsigned long long pbits_v(const DevTables &T, int w, int p0) {
+    if (w < 0 || w > T.n || p0 > T.n + 1 || p0 <= -64) return 0ull;
+    const unsigned long long *row = T.pb + (size_t)w * T.pbw;
+    if (p0 < 0) return row[0] << (-p0);
+    const int wi = p0 >> 6, sh = p0 & 63;
+    unsigned long long x = row[wi] >> sh;
+    if (sh) x |= row[wi + 1] << (64 - sh);
+    return x;
+}
+
+// The dts of a wave, one per lane: lane z describes dt = TL_DT0 + wv + TL_W*z.  Computed once per
+// tile with vector loads (one memory round trip for all of them, instead of scalar loads in front
+// of every dt's row loads); tl_dt_pick reads the z-th one out with readlanes.
+template <int role>
+__device__ __forceinline__ TlDt tl_dt_setup(const DevTables &T, int t, int dt, int a, int b, int g, int K0, int X0,
+                                            unsigned keymask) {
     TlDt d;
-    d.mask = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)w.y) << 32) |
-             (unsigned)__builtin_amdgcn_readfirstlane((int)w.x);
-    d.first = __builtin_amdgcn_readfirstlane((int)w.z);
-    const int hw = __builtin_amdgcn_readfirstlane((int)w.w);
-    d.ch = (short)(hw & 0xffff);
-    d.cid = (short)(hw >> 16);
+    const int n = T.n, rs = T.rs, m = n - t - 2, tp = t - dt;
+    const int u1min = imax(0, dt - 2 - (IE_U - 1)), u1max = imin(IE_U - 1, dt - 2), cnt = u1max - u1min + 1;
+    d.nrows = TL_NK + cnt - 1;
+    d.cnt = cnt;
+    d.u1max = u1max;
+    d.mp = m + dt;
+    d.tp1 = tp + 1;
+    // rows read by a live key: keymask spread over cnt consecutive bits
+    unsigned long long used = keymask;
+    for (int len = 1; len < cnt;) {
+        const int st = imin(len, cnt - len);
+        used |= used << st;
+        len += st;
+    }
+    const long long lbx = T.ldx[tp].lbx;
+    int w, p0, rlo, rhi;
+    if (role == 0) {
+        const int Mp = T.ld[tp].M;
+        d.Rlo = K0 + 1 + u1min;  // column c = Rlo + r
+        w = a - dt; p0 = d.Rlo; rlo = 1 - d.Rlo; rhi = d.mp - d.Rlo;
+        d.rbase = lbx + (long long)(a - dt) * Mp + (X0 + dt - 1 - u1min) - TL_PAD;
+        d.ebase = (((long long)0 * (n + 1) + a) * rs + K0) * TL_KEYW;
+    } else if (role == 1) {
+        const int Mp = T.ld[tp].M, Cp = T.ld[tp].C;
+        d.Rlo = K0 + 1 + u1min;  // PRx row q' = Rlo + r
+        w = b - dt; p0 = d.Rlo + a + 3; rlo = -d.Rlo; rhi = d.mp - 1 - d.Rlo;
+        d.rbase = lbx + Cp + (long long)a * Mp + (X0 - 1);
+        d.ebase = (((long long)0 * (n + 1) + b) * rs + K0 + a + 3) * TL_KEYW;
+    } else {
+        const long long pmb = T.ldx[tp].pmb;
+        d.Rlo = K0 - 1 - u1max;  // PMx row d = Rlo + r (at h' = h + dt)
+        w = g + dt; p0 = d.Rlo; rlo = 1 - d.Rlo; rhi = n - g - dt - d.Rlo;
+        d.rbase = pmb + (long long)(g - 2 + dt) * n * (tp + 1) + (X0 - 1 - u1max) - TL_PAD;
+        d.ebase = (((long long)1 * (n + 1) + g) * rs + K0) * TL_KEYW;
+    }
+    d.ebase += (long long)(dt - TL_DT0) * TL_EJ;
+    d.mask = used & pbits_v(T, w, p0) & bit_range(imax(rlo, 0), imin(rhi, d.nrows - 1));
     return d;
+}
+
+__device__ __forceinline__ TlDt tl_dt_pick(const TlDt &v, int z) {
+    TlDt d;
+    d.mask = rdl64(v.mask, z);
+    d.rbase = (long long)rdl64((unsigned long long)v.rbase, z);
+    d.ebase = (long long)rdl64((unsigned long long)v.ebase, z);
+    d.nrows = __builtin_amdgcn_readlane(v.nrows, z);
+    d.cnt = __builtin_amdgcn_readlane(v.cnt, z);
+    d.u1max = __builtin_amdgcn_readlane(v.u1max, z);
+    d.Rlo = __builtin_amdgcn_readlane(v.Rlo, z);
+    d.mp = __builtin_amdgcn_readlane(v.mp, z);
+    d.tp1 = __builtin_amdgcn_readlane(v.tp1, z);
+    return d;
+}
+
+// element offset of row r (lane 0, chunk 0) relative to d.rbase (>= 0 for every staged row)
+template <int role>
+__device__ __forceinline__ int tl_row_off(const TlDt &d, int r) {
+    if (role == 0) {
+        const int c1 = d.Rlo + r - 1;  // column c - 1
+        return c1 * d.mp - ((c1 * (c1 - 1)) >> 1) - r + TL_PAD;
+    } else if (role == 1) {
+        const int q = d.Rlo + r;
+        return (q * (q + 1)) >> 1;
+    } else {
+        return (d.Rlo + r - 1) * d.tp1 + r + TL_PAD;
+    }
+}
+
+// issue the 16-byte loads of one dt: rows (TL_NLR loads, 8 lanes per row) and energies (TL_NLE
+// loads, 8 lanes per key); lanes of rows / keys not staged load nothing.  (Buffer loads with
+// out-of-range offsets for those lanes, so that every load is issued and two dts can be in flight
+// with exact waits, measured slower in the fill: 42.1 vs 39.1 ms, the same 111 us per launch.)
+template <int role>
+__device__ __forceinline__ void tl_issue_e(const DevTables &T, const TlDt &d, unsigned keymask, int lane, uint4 *E);
+template <int role>
+__device__ __forceinline__ void tl_issue(const DevTables &T, const TlDt &d, unsigned keymask, int lane, uint4 *R, uint4 *E) {
+    tl_issue_e<role>(T, d, keymask, lane, E);
+    const char *cb = (const char *)((role == 2 ? T.pmx : T.d4x) + d.rbase);
+#pragma unroll
+    for (int s = 0; s < TL_NLR; ++s) {
+        const int idx = s * 64 + lane, r = idx >> 3, ch = idx & 7;
+        if (r < d.nrows && ((d.mask >> r) & 1ull)) {
+            const unsigned off = 2u * (unsigned)(tl_row_off<role>(d, r) + 8 * ch);
+            const tl_u32x4 v = *(const __attribute__((address_space(1))) tl_u32x4 *)(cb + off);
+            R[s] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+    }
+}
+
+// LDS byte offset of the chunk a lane of row load s stores: staged row r goes to slot
+// popcount(mask below r) (the compacted order the energies of T.ied follow); -1: not staged
+__device__ __forceinline__ int tl_slot_off(unsigned long long mask, int nrows, int s, int lane) {
+    const int idx = s * 64 + lane, r = idx >> 3, ch = idx & 7;
+    if (r >= nrows || !((mask >> r) & 1ull)) return -1;
+    return __popcll(mask & ((1ull << r) - 1ull)) * 128 + ch * 16;
+}
+
+template <int role>
+__device__ __forceinline__ void tl_issue_e(const DevTables &T, const TlDt &d, unsigned keymask, int lane, uint4 *E) {
+    const char *eb = (const char *)(T.ied + d.ebase);
+#pragma unroll
+    for (int s = 0; s < TL_NLE; ++s) {
+        const int idx = s * 64 + lane, kk = idx >> 3, ch = idx & 7;
+        if ((keymask >> kk) & 1u) {
+            const unsigned off = (unsigned)(kk * TL_KEYW * 4 + ch * 16);
+            const tl_u32x4 v = *(const __attribute__((address_space(1))) tl_u32x4 *)(eb + off);
+            E[s] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+    }
+}
+
+// the walk of NK keys (kk[0..NK-1]) over one dt: acc[q] = min over the key's candidates of
+// staged row + energy.  A key's candidate rows kk..kk+cnt-1 that can pair are the consecutive LDS
+// slots P[q] .. P[q]+n[q]-1 (compacted staging), and T.ied holds the key's energies in the same
+// compacted order (TL_BIG past n[q]), so the walk is 4 slots per step with affine addresses.
+#ifndef CCJ_TLK
+#define CCJ_TLK 1
+#endif
+constexpr int TL_K = CCJ_TLK;  // keys walked together
+template <bool PMMASK, int NK>
+__device__ __forceinline__ void tl_walk_keys(const char *wl, const int *kk, const int *P, const int *nk, int *acc, int lane,
+                                             int SPlo, unsigned SPn) {
+    int nmax = nk[0];
+#pragma unroll
+    for (int q = 1; q < NK; ++q) nmax = imax(nmax, nk[q]);
+#pragma unroll
+    for (int gp = 0; gp < TL_EJ / 4; ++gp) {
+        if (4 * gp >= nmax) break;
+        tl_i32x4 e[NK];
+        int x[NK][4];
+#pragma unroll
+        for (int q = 0; q < NK; ++q) {
+            e[q] = *(const tl_i32x4 *)(wl + TL_OFF_E + kk[q] * 128 + 16 * gp);
+            const char *rb = wl + (P[q] + 4 * gp) * 128 + lane * 2;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[q][u] = (int)*(const int16_t *)(rb + u * 128);
+        }
+#pragma unroll
+        for (int q = 0; q < NK; ++q)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                int c = x[q][u] + e[q][u];
+                if (PMMASK) c = ((unsigned)(P[q] + 4 * gp + u - SPlo) < SPn) ? c : TL_BIG;
+                acc[q] = imin(acc[q], c);
+            }
+    }
+}
+
+// every live key of one dt, TL_K at a time (accumulators in LDS, clamped like a store: the clamp
+// commutes with min).  mask: the staged rows; a key's slots start at popcount(mask below kk).
+template <bool PMMASK>
+__device__ __forceinline__ void tl_walk(char *wl, unsigned km, int lane, unsigned long long mask, int cnt, int SPlo,
+                                        unsigned SPn) {
+    const unsigned long long win = (1ull << cnt) - 1ull;
+#pragma unroll 1
+    while (km) {
+        int kk[2], P[2], nk[2], acc[2];
+        kk[0] = __builtin_ctz(km);
+        km &= km - 1u;
+        P[0] = __popcll(mask & ((1ull << kk[0]) - 1ull));
+        nk[0] = __popcll(mask & (win << kk[0]));
+        if (nk[0] == 0) continue;
+        int16_t *ap0 = (int16_t *)(wl + TL_OFF_A + kk[0] * 128 + lane * 2);
+        acc[0] = *ap0;
+        if (TL_K == 2 && km) {
+            kk[1] = __builtin_ctz(km);
+            km &= km - 1u;
+            P[1] = __popcll(mask & ((1ull << kk[1]) - 1ull));
+            nk[1] = __popcll(mask & (win << kk[1]));
+            int16_t *ap1 = (int16_t *)(wl + TL_OFF_A + kk[1] * 128 + lane * 2);
+            acc[1] = *ap1;
+            tl_walk_keys<PMMASK, 2>(wl, kk, P, nk, acc, lane, SPlo, SPn);
+            *ap1 = (int16_t)clamp_store(acc[1]);
+        } else {
+            tl_walk_keys<PMMASK, 1>(wl, kk, P, nk, acc, lane, SPlo, SPn);
+        }
+        *ap0 = (int16_t)clamp_store(acc[0]);
+    }
 }
 
 template <int role>
 __device__ __forceinline__ void iltile_body(const DevTables &T, int t, uint32_t tw, int G_SH, int rank, char *smem) {
-    TlDt *dtab = (TlDt *)smem;
-    int8_t *rowl = (int8_t *)(smem + TL_OFF_ROWL);
-    int16_t *eb = (int16_t *)(smem + TL_OFF_EB);
-    const int n = T.n, rs = T.rs, m = n - t - 2;
+    const int n = T.n, m = n - t - 2;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int blk = (int)((tw >> 20) & 1023u), K0 = (int)((tw >> 10) & 1023u), xc = (int)(tw & 1023u);
     int a = 0, b = 0, g = 0, X0, dtmax;
     if (role == 0) {
-        a = blk; b = t - a; X0 = xc * TL_NC; dtmax = imin(2 * (IE_U - 1) + 2, a - 4);
+        a = blk; b = t - a; X0 = xc * 64; dtmax = imin(TL_DT1, a - 4);
     } else if (role == 1) {
-        a = blk; b = t - a; X0 = 1 + xc * TL_NC; dtmax = imin(2 * (IE_U - 1) + 2, b - 4);
+        a = blk; b = t - a; X0 = 1 + xc * 64; dtmax = imin(TL_DT1, b - 4);
     } else {
-        g = blk + 2; X0 = 2 + xc * TL_NC; dtmax = imin(2 * (IE_U - 1) + 2, t - 2);
+        g = blk + 2;
+        int x0, xn;
+        pm_tile_span(n, t, g, K0, x0, xn);
+        X0 = x0 + xc * 64; dtmax = imin(TL_DT1, t - 2);
     }
-    const int x = X0 + lane;  // this lane's cell coordinate (h, i or a)
-    // ---- keys (every wave, the same): pair can pair and a cell in this tile
+    // ---- keys (lanes 0..15, the same in every wave): the pair can pair and owns a cell in this tile
     unsigned keymask;
     {
-        const int K = K0 + lane;
+        const int kk = lane, K = K0 + kk;
         bool ok = false;
-        if (lane < TL_NK) {
-            if (role == 0) ok = K >= 1 && K <= m && X0 <= m - K;
+        if (kk < TL_NK) {
+            if (role == 0) ok = K >= 1 && K <= m;
             else if (role == 1) ok = K <= m - 1 && X0 <= K + 1;
             else {
                 const int k = K + g;
                 if (K >= 1 && k <= n) {
                     const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, K - 1);
-                    ok = alo <= ahi && X0 <= ahi && X0 + TL_NC - 1 >= alo;
+                    ok = alo <= ahi && X0 + kk <= ahi && X0 + kk + 63 >= alo;
                 }
             }
         }
         const unsigned long long kp = role == 0 ? pbits(T, a, K0) : role == 1 ? pbits(T, b, K0 + a + 3) : pbits(T, g, K0);
-        keymask = (unsigned)(__ballot(ok) & kp) & 0xffffu;
+        keymask = (unsigned)(__ballot(ok) & kp) & ((1u << TL_NK) - 1u);
+        keymask = (unsigned)__builtin_amdgcn_readfirstlane((int)keymask);
     }
-    if (keymask == 0) return;  // whole workgroup (uniform)
-    const int nkeys = __popc(keymask);
-    int16_t *rows = (int16_t *)(smem + TL_OFF_EB + nkeys * TL_EB * 2);
-    const int rowcap = (TL_LDS - (TL_OFF_EB + nkeys * TL_EB * 2)) / 16;  // 16-byte chunks per dt chunk
-    // ---- energy blocks of the pairable keys: key slot = rank of the key in keymask
+    if (keymask == 0) return;  // the whole workgroup (uniform)
+    char *wl = smem + wv * TL_WB;
+    // accumulators: 32767 (the clamp of "no candidate")
     {
-        const int16_t *src = role == 2 ? T.ieI : T.ieO;
-        const int pw = role == 0 ? a : role == 1 ? b : g, pp0 = role == 0 ? K0 : role == 1 ? K0 + a + 3 : K0;
-        const int per = TL_EB / 8;  // 106 chunks per block
-        for (int q = tid; q < nkeys * per; q += 256) {
-            const int ks = q / per, c = q - ks * per;
-            // ks-th set bit of keymask
-            unsigned mm = keymask;
-            for (int z = 0; z < ks; ++z) mm &= mm - 1;
-            const int kk = __ffs(mm) - 1;
-            const int16_t *blkp = src + ((size_t)pw * rs + pp0 + kk) * TL_EB;
-            *(uint4 *)(eb + ks * TL_EB + 8 * c) = *(const uint4 *)(blkp + 8 * c);
-        }
+        uint4 *ap = (uint4 *)(wl + TL_OFF_A) + lane * 2;
+        const unsigned inf2 = ((unsigned)INTERN_INF << 16) | (unsigned)INTERN_INF;
+        ap[0] = make_uint4(inf2, inf2, inf2, inf2);
+        ap[1] = make_uint4(inf2, inf2, inf2, inf2);
     }
-    // ---- per-dt row masks, one dt per lane of wave 0 (vector loads of the pairability words: one
-    // round trip for every dt), row lists, and the dt chunks: contiguous dt ranges whose rows fit
-    // the row area (greedy, in dt order)
-    const int ndt = imax(0, dtmax - 2);  // dt = 3 .. dtmax
-    if (wv == 0) {
-        const int dt = lane + 3;
-        unsigned long long mask = 0;
-        int ch = 0;
-        if (lane < ndt) {
-            const int u1min = imax(0, dt - 2 - (IE_U - 1)), u1max = imin(IE_U - 1, dt - 2), cnt = u1max - u1min + 1;
-            const int nrows = TL_NK + cnt - 1;
-            const int Rlo = role == 2 ? K0 - 1 - u1max : K0 + 1 + u1min;
-            const int mp = m + dt;
-            unsigned long long used = keymask;
-            for (int len = 1; len < cnt;) {
-                const int st = imin(len, cnt - len);
-                used |= used << st;
-                len += st;
+    const int nz = dtmax >= TL_DT0 + wv ? (dtmax - TL_DT0 - wv) / TL_W + 1 : 0;  // this wave's dts
+    if (nz > 0) {
+        const TlDt dv = tl_dt_setup<role>(T, t, imin(TL_DT0 + wv + TL_W * lane, dtmax), a, b, g, K0, X0, keymask);
+        uint4 R[TL_NLR], E[TL_NLE];
+#pragma unroll
+        for (int s = 0; s < TL_NLR; ++s) R[s] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int s = 0; s < TL_NLE; ++s) E[s] = make_uint4(0u, 0u, 0u, 0u);
+        tl_issue<role>(T, tl_dt_pick(dv, 0), keymask, lane, R, E);
+#pragma unroll 1
+        for (int z = 0; z < nz; ++z) {
+            // the pending dt's rows and energies into LDS (every slot: rows not staged keep stale
+            // values), the next dt's loads into the freed registers, then the walk
+            const TlDt d = tl_dt_pick(dv, z);
+#pragma unroll
+            for (int s = 0; s < TL_NLR; ++s) {
+                const int so = tl_slot_off(d.mask, d.nrows, s, lane);
+                if (so >= 0) *(uint4 *)(wl + so) = R[s];
             }
-            int rlo, rhi, w, p0;
-            if (role == 0) { w = a - dt; p0 = Rlo; rlo = 1 - Rlo; rhi = mp - Rlo; }
-            else if (role == 1) { w = b - dt; p0 = Rlo + a + 3; rlo = -Rlo; rhi = mp - 1 - Rlo; }
-            else { w = g + dt; p0 = Rlo; rlo = 1 - Rlo; rhi = n - g - dt - Rlo; }
-            unsigned long long pb = 0;
-            if (w >= 0 && w <= n && p0 <= n + 1 && p0 > -64) {
-                const unsigned long long *row = T.pb + (size_t)w * T.pbw;
-                if (p0 < 0) pb = row[0] << (-p0);
-                else {
-                    const int wi = p0 >> 6, sh = p0 & 63;
-                    pb = row[wi] >> sh;
-                    if (sh) pb |= row[wi + 1] << (64 - sh);
-                }
-            }
-            mask = used & pb & bit_range(imax(rlo, 0), imin(rhi, nrows - 1));
-            ch = (TL_NC + (role == 1 ? 0 : imin(TL_NK, cnt) - 1) + 7) >> 3;
-            int slot = 0;
-            for (unsigned long long mm = mask; mm; mm &= mm - 1) rowl[lane * 48 + slot++] = (int8_t)(__ffsll((long long)mm) - 1);
+#pragma unroll
+            for (int s = 0; s < TL_NLE; ++s) *(uint4 *)(wl + TL_OFF_E + (s * 64 + lane) * 16) = E[s];
+            const int dt = TL_DT0 + wv + TL_W * z;
+            if (z + 1 < nz) tl_issue<role>(T, tl_dt_pick(dv, z + 1), keymask, lane, R, E);
+            // PM's window as a row mask per lane: row r is a candidate of cell a = X0+lane+kk iff
+            // u1 = kk+u1max-r in [a-t+dt, a-2]  <=>  r in [BL, BL + t-dt-2], BL = u1max+2-X0-lane; in
+            // slots: [SPlo, SPlo + SPn)
+            const int BL = d.u1max + 2 - X0 - lane, BH = BL + (t - dt - 2) + 1;
+            auto below = [&](int x) { return x <= 0 ? 0 : x >= 64 ? __popcll(d.mask) : __popcll(d.mask & ((1ull << x) - 1ull)); };
+            const int SPlo = below(BL);
+            const unsigned SPn = (unsigned)(below(BH) - SPlo);
+            const bool pmmask = role == 2 && !(d.u1max + 2 - X0 <= 0 && d.u1max + 2 - X0 - 63 + (t - dt - 2) >= d.nrows - 1);
+            if (pmmask) tl_walk<true>(wl, keymask, lane, d.mask, d.cnt, SPlo, SPn);
+            else tl_walk<false>(wl, keymask, lane, d.mask, d.cnt, SPlo, SPn);
         }
-        const int need = __popcll(mask) * ch;
-        // greedy chunking over the dts (scalar walk over the lanes' needs)
-        int cur = 0, cid = 0, myfirst = 0, mycid = 0;
-        for (int di = 0; di < ndt; ++di) {
-            const int nd = __builtin_amdgcn_readlane(need, di);
-            if (cur + nd > rowcap) { ++cid; cur = 0; }
-            if (lane == di) { myfirst = cur; mycid = cid; }
-            cur += nd;
-        }
-        if (lane < ndt) {
-            TlDt d;
-            d.mask = mask;
-            d.first = myfirst;
-            d.ch = (short)ch;
-            d.cid = (short)mycid;
-            dtab[lane] = d;
-        }
-        if (lane == 0) *(int *)(smem + TL_OFF_NCH) = cid + 1;
     }
     __syncthreads();
-    const int nchunk = ndt > 0 ? __builtin_amdgcn_readfirstlane(*(const volatile int *)(smem + TL_OFF_NCH)) : 0;
-    // ---- accumulators: wave wv takes the pairable keys of rank wv, wv+4, ... (at most 4)
-    int acc[4], kkz[4];
-    const int nz = (nkeys - wv + 3) >> 2;
-#pragma unroll
-    for (int z = 0; z < 4; ++z) {
-        acc[z] = TL_BIG;
-        unsigned mm = keymask;
-        for (int y = 0; y < wv + 4 * z && mm; ++y) mm &= mm - 1;
-        kkz[z] = mm ? __ffs(mm) - 1 : 0;
-    }
-    const int16_t *cbase = role == 2 ? T.pmx : T.d4x;
-    const long long clim = role == 2 ? T.npm : T.nx;
-    int dlo = 0;  // first dt index of the chunk
-    for (int cc = 0; cc < nchunk; ++cc) {
-        int dhi = dlo;  // one past the chunk's last dt index
-        while (dhi < ndt && tl_dt(dtab, dhi).cid == cc) ++dhi;
-        // staging: wave wv takes dt indices dlo+wv, dlo+wv+4, ... of the chunk, TL_B loads in
-        // flight; the (dt, round) of each load of a batch is fixed first (scalar), then the loads
-        // are issued unconditionally (idle lanes re-read a valid chunk), so the compiler counts
-        // them and each store waits only for its own load
-        {
-            int di = dlo + wv, rd = 0;
-            auto skip = [&]() {
-                while (di < dhi && tl_dt(dtab, di).mask == 0) di += 4;
-            };
-            skip();
-            while (di < dhi) {
-                int bdi[TL_B], brd[TL_B];
-#pragma unroll
-                for (int u = 0; u < TL_B; ++u) {
-                    bdi[u] = di;
-                    brd[u] = rd;
-                    if (di < dhi) {
-                        const TlDt d = tl_dt(dtab, di);
-                        if (++rd * 64 >= __popcll(d.mask) * d.ch) {
-                            rd = 0;
-                            di += 4;
-                            skip();
-                        }
-                    } else {
-                        bdi[u] = bdi[0];  // a repeat of a live slot, never stored
-                        brd[u] = -1;
-                    }
-                }
-                uint4 reg[TL_B];
-                int dst[TL_B];
-#pragma unroll
-                for (int u = 0; u < TL_B; ++u) {
-                    const int bd = bdi[u];
-                    const TlDt d = tl_dt(dtab, bd);
-                    const int total = __popcll(d.mask) * d.ch;
-                    const int qq = imax(brd[u], 0) * 64 + lane;
-                    const bool live = brd[u] >= 0 && qq < total;
-                    const int q = live ? qq : 0;
-                    const int dt = bd + 3, tp = t - dt;
-                    // level descriptors of the source level through scalar loads
-                    typedef const __attribute__((address_space(4))) long long cll;
-                    typedef const __attribute__((address_space(4))) int cint;
-                    LvlDev Lp;
-                    Lp.C = *(cint *)(unsigned long long)&T.ld[tp].C;
-                    Lp.M = *(cint *)(unsigned long long)&T.ld[tp].M;
-                    LvlX Xp;
-                    Xp.lbx = *(cll *)(unsigned long long)&T.ldx[tp].lbx;
-                    Xp.pmb = *(cll *)(unsigned long long)&T.ldx[tp].pmb;
-                    const int s = q / d.ch, c = q - s * d.ch;
-                    const int r = rowl[bd * 48 + s];
-                    const int u1min = imax(0, dt - 2 - (IE_U - 1)), u1max = imin(IE_U - 1, dt - 2);
-                    long long src;
-                    if (role == 0) {
-                        const int R = K0 + 1 + u1min + r, mp = m + dt, ap = a - dt;
-                        const int u1hi = imin(u1max, R - 1 - K0);
-                        const long long y = R - 1;
-                        src = Xp.lbx + (long long)ap * Lp.M + y * mp - ((y * (y - 1)) >> 1) + (X0 + dt - 1 - u1hi);
-                    } else if (role == 1) {
-                        const int R = K0 + 1 + u1min + r;
-                        src = Xp.lbx + Lp.C + (long long)a * Lp.M + (((long long)R * (R + 1)) >> 1) + (X0 - 1);
-                    } else {
-                        const int R = K0 - 1 - u1max + r;
-                        const int u1hi = imin(u1max, K0 + TL_NK - 2 - R);
-                        src = Xp.pmb + ((long long)(g - 2 + dt) * n + R - 1) * (tp + 1) + (X0 - 1 - u1hi);
-                    }
-                    reg[u] = ldg_u4(cbase, src + 8 * c, clim);
-                    dst[u] = live ? (d.first + q) * 8 : -1;
-                }
-#pragma unroll
-                for (int u = 0; u < TL_B; ++u)
-                    if (dst[u] >= 0) *(uint4 *)(rows + dst[u]) = reg[u];
-            }
-        }
-        __syncthreads();
-        // walk: dt outer (one dt-table read), this wave's keys inner
-        for (int di = dlo; di < dhi; ++di) {
-            const TlDt d = tl_dt(dtab, di);
-            if (d.mask == 0) continue;
-            const int dt = di + 3;
-            const int u1min = imax(0, dt - 2 - (IE_U - 1)), u1max = imin(IE_U - 1, dt - 2), cnt = u1max - u1min + 1;
-            const int rbase = d.first * 8 + lane;
-#pragma unroll
-            for (int z = 0; z < 4; ++z) {
-                if (z >= nz) break;
-                const int kk = kkz[z];
-                const int16_t *ebk = eb + (wv + 4 * z) * TL_EB + (dt - 2);  // + u1 * (IE_U - 1): e(u1, dt-2-u1)
-                unsigned long long bits = (d.mask >> kk) & ((1ull << cnt) - 1ull);
-                int cur = acc[z];
-                while (bits) {
-                    int jj[4], pen[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        jj[u] = bits ? __ffsll((long long)bits) - 1 : 0;
-                        pen[u] = bits ? 0 : TL_BIG;
-                        bits &= bits - 1;
-                    }
-                    int v[4], e[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int r = kk + jj[u];
-                        const int sl = __popcll(d.mask & ((1ull << r) - 1ull));
-                        const int u1 = role == 2 ? u1max - jj[u] : u1min + jj[u];
-                        const int sh = role == 0 ? imin(cnt - 1 - jj[u], kk) : role == 2 ? imin(jj[u], TL_NK - 1 - kk) : 0;
-                        v[u] = rows[rbase + sl * d.ch * 8 + sh];
-                        e[u] = ebk[u1 * (IE_U - 1)];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        int c = v[u] + e[u] + pen[u];
-                        if (role == 2) {
-                            const int u1 = u1max - jj[u];
-                            c += ((unsigned)(x - (u1 + 2)) <= (unsigned)(t - dt - 2)) ? 0 : TL_BIG;
-                        }
-                        cur = imin(cur, c);
-                    }
-                }
-                acc[z] = cur;
-            }
-        }
-        __syncthreads();  // the next chunk overwrites the rows
-        dlo = dhi;
-    }
-    // ---- results: the interior-loop minimum of every cell of this wave's keys, clamped like a store
+    // ---- results: wave wv finishes keys kk = wv, wv+TL_W, ... (min over the waves' accumulators)
     const LvlDev Lt = T.ld[t];
+    for (int kk = wv; kk < TL_NK; kk += TL_W) {
+        if (!((keymask >> kk) & 1u)) continue;
+        int v = INTERN_INF;
 #pragma unroll
-    for (int z = 0; z < 4; ++z) {
-        if (z >= nz) break;
-        const int K = K0 + kkz[z];
-        const int v = clamp_store(acc[z]);
+        for (int w2 = 0; w2 < TL_W; ++w2) v = imin(v, (int)*(const int16_t *)(smem + w2 * TL_WB + TL_OFF_A + kk * 128 + lane * 2));
+        const int K = K0 + kk;
         if (role == 0) {
-            const int h = x;
-            if (h <= m - K) T.d4[Lt.lb + (long long)PL * Lt.C + (long long)a * Lt.M + h * m - ((h * (h - 1)) >> 1) + K - 1] = (int16_t)v;
+            const int h = X0 + lane - kk;
+            if (h >= 0 && h <= m - K)
+                T.d4[Lt.lb + (long long)PL * Lt.C + (long long)a * Lt.M + h * m - ((h * (h - 1)) >> 1) + K - 1] = (int16_t)v;
         } else if (role == 1) {
-            const int i = x, h = K + 1 - i;
+            const int i = X0 + lane, h = K + 1 - i;
             if (i <= K + 1) T.d4[Lt.lb + (long long)PR * Lt.C + (long long)a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)v;
         } else {
-            const int k = K + g, h = g - 2, aa = x;
+            const int k = K + g, h = g - 2, aa = X0 + lane + kk;
             const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, K - 1);
             if (aa >= alo && aa <= ahi && shard_owner(aa, G_SH) == rank)
                 T.d4[Lt.lb + (long long)PM * Lt.C + (long long)aa * Lt.M + h * m - ((h * (h - 1)) >> 1) + K - aa - 1] = (int16_t)v;
@@ -1406,37 +1423,65 @@ __device__ __forceinline__ void iltile_body(const DevTables &T, int t, uint32_t 
     }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_iltile(DevTables T, int t, long long first, int G_SH, int rank) {
+__global__ __launch_bounds__(64 * TL_W) void k_iltile(DevTables T, int t, long long first, int G_SH, int rank) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    // XCD-contiguous mapping: workgroup b runs on XCD b % 8, so XCD x takes one contiguous run of
-    // tiles (neighbouring key ranges of one block read overlapping source rows: L2 reuse)
-    const int nb = (int)gridDim.x, q8 = nb >> 3, r8 = nb & 7, bid = (int)blockIdx.x, xcd = bid & 7, pos = bid >> 3;
-    const int tile = xcd < r8 ? xcd * (q8 + 1) + pos : r8 * (q8 + 1) + (xcd - r8) * q8 + pos;
-    const uint32_t tw = ld_const(T.tiles + first + tile);
+    // tiles in the host's order (longest first, build_tiles), dealt round-robin over the XCDs
+    const uint32_t tw = ld_const(T.tiles + first + blockIdx.x);
     const int role = (int)(tw >> 30);
     if (role == 0) iltile_body<0>(T, t, tw, G_SH, rank, smem);
     else if (role == 1) iltile_body<1>(T, t, tw, G_SH, rank, smem);
     else iltile_body<2>(T, t, tw, G_SH, rank, smem);
 }
 
-// Per-key loop-energy blocks for k_iltile (from T.ie, once per fill): ieO[w][p] = the 29 x 29
-// get_e_intP window of the closing pair (p, p+w) (PL, PR); ieI[g][j] = the window of the loops
-// closed around the inner pair (j, j+g) (PM: outer pair (j-1-u1, j+g+1+u2)).  u1 major, 848 int16.
-__global__ __launch_bounds__(256) void k_ie_blocks(DevTables T) {
+// Per-(key, dt) energy rows for k_iltile (from T.ie, once per fill): T.ied[type][w][p][dt-3][.], int32,
+// for the keys whose pair (p, p+w) can pair, the candidates that exist in window order (the same
+// order as k_iltile's compacted row slots), then TL_BIG.  Window position j:
+//   type 0, the pair closes the loop (PL, PR): j-th window position u1 = u1min + j;
+//   type 1, the pair is the loop's inner pair (PM): u1 = u1max - j, outer pair (p-1-u1, p+w+1+u2);
+// e = lrint(e_intP * E_IntLoop) (pseudo_loop.cc:836-840), TL_BIG where the reference skips the
+// candidate (the other pair cannot pair: T.ie holds 32767) or j is past the window.
+__global__ __launch_bounds__(256) void k_ie_tiles(DevTables T) {
+    __shared__ int buf[TL_NK][8 * TL_EJ + 1];
     const int n = T.n, rs = T.rs;
-    const int w = blockIdx.y, p = blockIdx.x + 1;
-    if (p + w > n) return;
-    int16_t *o = T.ieO + ((size_t)w * rs + p) * TL_EB, *q = T.ieI + ((size_t)w * rs + p) * TL_EB;
-    for (int uu = threadIdx.x; uu < TL_EB; uu += 256) {
-        int16_t vo = INTERN_INF, vi = INTERN_INF;
-        if (uu < IE_U * IE_U) {
-            const int u1 = uu / IE_U, u2 = uu - u1 * IE_U;
-            vo = T.ie[((size_t)uu * (n + 1) + w) * rs + p];
-            const int d = p - 1 - u1, wo = w + 2 + u1 + u2;
-            if (d >= 1 && d + wo <= n) vi = T.ie[((size_t)uu * (n + 1) + wo) * rs + d];
+    const int p0 = (int)blockIdx.x * TL_NK, w = (int)blockIdx.y, type = (int)blockIdx.z;
+    for (int dc = 0; dc < TL_DTN / 8; ++dc) {
+        for (int idx = threadIdx.x; idx < TL_NK * 8 * TL_EJ; idx += 256) {
+            const int kk = idx & (TL_NK - 1), e = idx >> 4;
+            const int dt = TL_DT0 + dc * 8 + (e >> 5), j = e & (TL_EJ - 1);
+            const int p = p0 + kk;
+            const int u1min = imax(0, dt - 2 - (IE_U - 1)), u1max = imin(IE_U - 1, dt - 2), cnt = u1max - u1min + 1;
+            int v = TL_BIG;
+            if (j < cnt && p >= 1 && p + w <= n) {
+                int u1, ws, ps;
+                if (type == 0) { u1 = u1min + j; ws = w; ps = p; }
+                else { u1 = u1max - j; ws = w + dt; ps = p - 1 - u1; }
+                const int u2 = dt - 2 - u1;
+                if (ps >= 1 && ps + ws <= n) {
+                    const int x = T.ie[((size_t)(u1 * IE_U + u2) * (n + 1) + ws) * rs + ps];
+                    v = x >= INTERN_INF ? TL_BIG : x;
+                }
+            }
+            buf[kk][e] = v;
         }
-        o[uu] = vo;
-        q[uu] = vi;
+        __syncthreads();
+        // each (key, dt) row in compacted order: the candidates that exist, in window order, then TL_BIG
+        if (threadIdx.x < TL_NK * 8) {
+            int *row = &buf[threadIdx.x >> 3][(threadIdx.x & 7) * TL_EJ];
+            int q = 0;
+            for (int j = 0; j < TL_EJ; ++j) {
+                const int v = row[j];
+                if (v != TL_BIG) row[q++] = v;
+            }
+            for (; q < TL_EJ; ++q) row[q] = TL_BIG;
+        }
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < TL_NK * 8 * TL_EJ; idx += 256) {
+            const int kk = idx >> 8, e = idx & 255;
+            const int p = p0 + kk;
+            if (p >= 1 && p + w <= n && T.pt[(size_t)w * rs + p] > 0)
+                T.ied[(((size_t)type * (n + 1) + w) * rs + p) * TL_KEYW + dc * 8 * TL_EJ + e] = buf[kk][e];
+        }
+        __syncthreads();
     }
 }
 
@@ -2348,10 +2393,11 @@ extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int n
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_ie_blocks(const DevTables *T, void *stream) {
+extern "C" int ccjk_ie_tiles(const DevTables *T, void *stream) {
     const int n = T->n;
     if (n < 1) return 0;
-    hipLaunchKernelGGL(k_ie_blocks, dim3(n, n + 1), dim3(256), 0, (hipStream_t)stream, *T);
+    hipLaunchKernelGGL(k_ie_tiles, dim3((unsigned)((T->rs + TL_NK - 1) / TL_NK), (unsigned)(n + 1), 2u), dim3(256), 0,
+                       (hipStream_t)stream, *T);
     return (int)hipGetLastError();
 }
 
