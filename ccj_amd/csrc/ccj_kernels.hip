@@ -1073,7 +1073,10 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
 // during the walk) and meet in LDS at the end.  PM's per-cell window (d > i, dp < l, i.e. u1 <=
 // a-2, u2 <= b-2) is a lane mask over rows.  Min is order-independent: bit-identical minima.
 // ------------------------------------------------------------------------------------------
-constexpr int TL_W = 4;                                 // waves per tile
+#ifndef CCJ_TLW
+#define CCJ_TLW 4
+#endif
+constexpr int TL_W = CCJ_TLW;                           // waves per tile
 constexpr int TL_ROWS = TL_NK + IE_U - 1;               // 44 source rows per dt at most
 constexpr int TL_DT0 = 3, TL_DT1 = 2 * (IE_U - 1) + 2;  // dt = 3 .. 58
 constexpr int TL_DTN = TL_DT1 - TL_DT0 + 1;             // 56
@@ -1211,27 +1214,24 @@ __device__ __forceinline__ int tl_row_off(const TlDt &d, int r) {
 // with exact waits, measured slower in the fill: 42.1 vs 39.1 ms, the same 111 us per launch.)
 template <int role>
 __device__ __forceinline__ void tl_issue_e(const DevTables &T, const TlDt &d, unsigned keymask, int lane, uint4 *E);
+// so[s]: the LDS byte offset the lane's chunk goes to (staged row r -> slot popcount(mask below r),
+// the compacted order the energies of T.ied follow), -1 when the row is not staged
 template <int role>
-__device__ __forceinline__ void tl_issue(const DevTables &T, const TlDt &d, unsigned keymask, int lane, uint4 *R, uint4 *E) {
+__device__ __forceinline__ void tl_issue(const DevTables &T, const TlDt &d, unsigned keymask, int lane, uint4 *R, uint4 *E,
+                                         int *so) {
     tl_issue_e<role>(T, d, keymask, lane, E);
     const char *cb = (const char *)((role == 2 ? T.pmx : T.d4x) + d.rbase);
 #pragma unroll
     for (int s = 0; s < TL_NLR; ++s) {
         const int idx = s * 64 + lane, r = idx >> 3, ch = idx & 7;
-        if (r < d.nrows && ((d.mask >> r) & 1ull)) {
+        const bool on = r < d.nrows && ((d.mask >> r) & 1ull);
+        so[s] = on ? __popcll(d.mask & ((1ull << r) - 1ull)) * 128 + ch * 16 : -1;
+        if (on) {
             const unsigned off = 2u * (unsigned)(tl_row_off<role>(d, r) + 8 * ch);
             const tl_u32x4 v = *(const __attribute__((address_space(1))) tl_u32x4 *)(cb + off);
             R[s] = make_uint4(v.x, v.y, v.z, v.w);
         }
     }
-}
-
-// LDS byte offset of the chunk a lane of row load s stores: staged row r goes to slot
-// popcount(mask below r) (the compacted order the energies of T.ied follow); -1: not staged
-__device__ __forceinline__ int tl_slot_off(unsigned long long mask, int nrows, int s, int lane) {
-    const int idx = s * 64 + lane, r = idx >> 3, ch = idx & 7;
-    if (r >= nrows || !((mask >> r) & 1ull)) return -1;
-    return __popcll(mask & ((1ull << r) - 1ull)) * 128 + ch * 16;
 }
 
 template <int role>
@@ -1367,35 +1367,40 @@ __device__ __forceinline__ void iltile_body(const DevTables &T, int t, uint32_t 
     if (nz > 0) {
         const TlDt dv = tl_dt_setup<role>(T, t, imin(TL_DT0 + wv + TL_W * lane, dtmax), a, b, g, K0, X0, keymask);
         uint4 R[TL_NLR], E[TL_NLE];
+        int so[TL_NLR];
 #pragma unroll
         for (int s = 0; s < TL_NLR; ++s) R[s] = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (int s = 0; s < TL_NLE; ++s) E[s] = make_uint4(0u, 0u, 0u, 0u);
-        tl_issue<role>(T, tl_dt_pick(dv, 0), keymask, lane, R, E);
+        tl_issue<role>(T, tl_dt_pick(dv, 0), keymask, lane, R, E, so);
 #pragma unroll 1
         for (int z = 0; z < nz; ++z) {
             // the pending dt's rows and energies into LDS (every slot: rows not staged keep stale
             // values), the next dt's loads into the freed registers, then the walk
-            const TlDt d = tl_dt_pick(dv, z);
 #pragma unroll
-            for (int s = 0; s < TL_NLR; ++s) {
-                const int so = tl_slot_off(d.mask, d.nrows, s, lane);
-                if (so >= 0) *(uint4 *)(wl + so) = R[s];
-            }
+            for (int s = 0; s < TL_NLR; ++s)
+                if (so[s] >= 0) *(uint4 *)(wl + so[s]) = R[s];
 #pragma unroll
             for (int s = 0; s < TL_NLE; ++s) *(uint4 *)(wl + TL_OFF_E + (s * 64 + lane) * 16) = E[s];
+            const TlDt d = tl_dt_pick(dv, z);
             const int dt = TL_DT0 + wv + TL_W * z;
-            if (z + 1 < nz) tl_issue<role>(T, tl_dt_pick(dv, z + 1), keymask, lane, R, E);
+            if (z + 1 < nz) tl_issue<role>(T, tl_dt_pick(dv, z + 1), keymask, lane, R, E, so);
             // PM's window as a row mask per lane: row r is a candidate of cell a = X0+lane+kk iff
             // u1 = kk+u1max-r in [a-t+dt, a-2]  <=>  r in [BL, BL + t-dt-2], BL = u1max+2-X0-lane; in
             // slots: [SPlo, SPlo + SPn)
-            const int BL = d.u1max + 2 - X0 - lane, BH = BL + (t - dt - 2) + 1;
-            auto below = [&](int x) { return x <= 0 ? 0 : x >= 64 ? __popcll(d.mask) : __popcll(d.mask & ((1ull << x) - 1ull)); };
-            const int SPlo = below(BL);
-            const unsigned SPn = (unsigned)(below(BH) - SPlo);
             const bool pmmask = role == 2 && !(d.u1max + 2 - X0 <= 0 && d.u1max + 2 - X0 - 63 + (t - dt - 2) >= d.nrows - 1);
-            if (pmmask) tl_walk<true>(wl, keymask, lane, d.mask, d.cnt, SPlo, SPn);
-            else tl_walk<false>(wl, keymask, lane, d.mask, d.cnt, SPlo, SPn);
+            if (pmmask) {
+                auto below = [&](int x) {  // staged rows below row x (branch-free)
+                    const unsigned xc = (unsigned)imin(imax(x, 0), 64);
+                    const unsigned long long lm = ((1ull << (xc & 63u)) - 1ull) | ((xc >> 6) ? ~0ull : 0ull);
+                    return __popcll(d.mask & lm);
+                };
+                const int BL = d.u1max + 2 - X0 - lane, BH = BL + (t - dt - 2) + 1;
+                const int SPlo = below(BL);
+                tl_walk<true>(wl, keymask, lane, d.mask, d.cnt, SPlo, (unsigned)(below(BH) - SPlo));
+            } else {
+                tl_walk<false>(wl, keymask, lane, d.mask, d.cnt, 0, 0u);
+            }
         }
     }
     __syncthreads();
@@ -2406,7 +2411,7 @@ extern "C" int ccjk_iltile(const DevTables *T, int t, long long first_tile, int 
     return 0;
 #endif
     if (ntiles <= 0) return 0;
-    hipLaunchKernelGGL(k_iltile, dim3((unsigned)ntiles), dim3(256), TL_LDS, (hipStream_t)stream, *T, t, first_tile, G, rank);
+    hipLaunchKernelGGL(k_iltile, dim3((unsigned)ntiles), dim3(64 * TL_W), TL_LDS, (hipStream_t)stream, *T, t, first_tile, G, rank);
     return (int)hipGetLastError();
 }
 
