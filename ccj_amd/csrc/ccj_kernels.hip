@@ -1248,72 +1248,45 @@ __device__ __forceinline__ void tl_issue_e(const DevTables &T, const TlDt &d, un
     }
 }
 
-// the walk of NK keys (kk[0..NK-1]) over one dt: acc[q] = min over the key's candidates of
-// staged row + energy.  A key's candidate rows kk..kk+cnt-1 that can pair are the consecutive LDS
-// slots P[q] .. P[q]+n[q]-1 (compacted staging), and T.ied holds the key's energies in the same
-// compacted order (TL_BIG past n[q]), so the walk is 4 slots per step with affine addresses.
-#ifndef CCJ_TLK
-#define CCJ_TLK 1
-#endif
-constexpr int TL_K = CCJ_TLK;  // keys walked together
-template <bool PMMASK, int NK>
-__device__ __forceinline__ void tl_walk_keys(const char *wl, const int *kk, const int *P, const int *nk, int *acc, int lane,
-                                             int SPlo, unsigned SPn) {
-    int nmax = nk[0];
-#pragma unroll
-    for (int q = 1; q < NK; ++q) nmax = imax(nmax, nk[q]);
+// the walk of key kk over one dt: acc = min over the key's candidates of staged row + energy.  The
+// key's candidate rows kk..kk+cnt-1 that can pair are the consecutive LDS slots P .. P+nk-1
+// (compacted staging), and T.ied holds its energies in the same compacted order (TL_BIG past nk),
+// so the walk is 4 slots per step with affine addresses.  (Two keys per step, or 8 slots per step,
+// measured slower: DESIGN.md §4.)
+template <bool PMMASK>
+__device__ __forceinline__ int tl_walk_key(const char *wl, int kk, int P, int nk, int acc, int lane, int SPlo, unsigned SPn) {
 #pragma unroll
     for (int gp = 0; gp < TL_EJ / 4; ++gp) {
-        if (4 * gp >= nmax) break;
-        tl_i32x4 e[NK];
-        int x[NK][4];
+        if (4 * gp >= nk) break;
+        const tl_i32x4 e = *(const tl_i32x4 *)(wl + TL_OFF_E + kk * 128 + 16 * gp);
+        const char *rb = wl + (P + 4 * gp) * 128 + lane * 2;
+        int x[4];
 #pragma unroll
-        for (int q = 0; q < NK; ++q) {
-            e[q] = *(const tl_i32x4 *)(wl + TL_OFF_E + kk[q] * 128 + 16 * gp);
-            const char *rb = wl + (P[q] + 4 * gp) * 128 + lane * 2;
+        for (int u = 0; u < 4; ++u) x[u] = (int)*(const int16_t *)(rb + u * 128);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) x[q][u] = (int)*(const int16_t *)(rb + u * 128);
+        for (int u = 0; u < 4; ++u) {
+            int c = x[u] + e[u];
+            if (PMMASK) c = ((unsigned)(P + 4 * gp + u - SPlo) < SPn) ? c : TL_BIG;
+            acc = imin(acc, c);
         }
-#pragma unroll
-        for (int q = 0; q < NK; ++q)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                int c = x[q][u] + e[q][u];
-                if (PMMASK) c = ((unsigned)(P[q] + 4 * gp + u - SPlo) < SPn) ? c : TL_BIG;
-                acc[q] = imin(acc[q], c);
-            }
     }
+    return acc;
 }
 
-// every live key of one dt, TL_K at a time (accumulators in LDS, clamped like a store: the clamp
-// commutes with min).  mask: the staged rows; a key's slots start at popcount(mask below kk).
+// every live key of one dt (accumulators in LDS, clamped like a store: the clamp commutes with
+// min).  mask: the staged rows; a key's slots start at popcount(mask below kk).
 template <bool PMMASK>
 __device__ __forceinline__ void tl_walk(char *wl, unsigned km, int lane, unsigned long long mask, int cnt, int SPlo,
                                         unsigned SPn) {
     const unsigned long long win = (1ull << cnt) - 1ull;
 #pragma unroll 1
     while (km) {
-        int kk[2], P[2], nk[2], acc[2];
-        kk[0] = __builtin_ctz(km);
+        const int kk = __builtin_ctz(km);
         km &= km - 1u;
-        P[0] = __popcll(mask & ((1ull << kk[0]) - 1ull));
-        nk[0] = __popcll(mask & (win << kk[0]));
-        if (nk[0] == 0) continue;
-        int16_t *ap0 = (int16_t *)(wl + TL_OFF_A + kk[0] * 128 + lane * 2);
-        acc[0] = *ap0;
-        if (TL_K == 2 && km) {
-            kk[1] = __builtin_ctz(km);
-            km &= km - 1u;
-            P[1] = __popcll(mask & ((1ull << kk[1]) - 1ull));
-            nk[1] = __popcll(mask & (win << kk[1]));
-            int16_t *ap1 = (int16_t *)(wl + TL_OFF_A + kk[1] * 128 + lane * 2);
-            acc[1] = *ap1;
-            tl_walk_keys<PMMASK, 2>(wl, kk, P, nk, acc, lane, SPlo, SPn);
-            *ap1 = (int16_t)clamp_store(acc[1]);
-        } else {
-            tl_walk_keys<PMMASK, 1>(wl, kk, P, nk, acc, lane, SPlo, SPn);
-        }
-        *ap0 = (int16_t)clamp_store(acc[0]);
+        const int nk = __popcll(mask & (win << kk));
+        if (nk == 0) continue;
+        int16_t *ap = (int16_t *)(wl + TL_OFF_A + kk * 128 + lane * 2);
+        *ap = (int16_t)clamp_store(tl_walk_key<PMMASK>(wl, kk, __popcll(mask & ((1ull << kk) - 1ull)), nk, (int)*ap, lane, SPlo, SPn));
     }
 }
 
