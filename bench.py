@@ -458,7 +458,8 @@ def main(argv=None):
     structure, energy = acc["last"].structure, acc["last"].energy
     wf = ctxs[0]
     # after the timed region: one fold with marker events around every launch (per-kernel-family
-    # times for k_iloop / k_diag2d; the markers slow that fold down, so it is not part of `value`)
+    # times for the interior loops (k_iltile, or k_iloop with CCJ_ILOOP_TILES=0) / k_diag2d; the
+    # markers slow that fold down, so it is not part of `value`)
     wf.set_timing(2)
     wf.ccj()
     tmi = wf.timing()
@@ -549,8 +550,9 @@ def main(argv=None):
                      "frac_counter": (traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS) if traffic and avg_launch_s > 0 else None,
                      "achieved_counter_gbs": (traffic / avg_launch_s / 1e9) if traffic and avg_launch_s > 0 else None},
         "roofline_iloop": {"bound": "hbm", "achieved": il_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": il_achieved / HBM_PEAK_GBS, "kernel": "k_iloop (one instrumented fold after "
-                                                                         "the timed region)",
+                           "frac": il_achieved / HBM_PEAK_GBS,
+                           "kernel": ("k_iloop" if os.environ.get("CCJ_ILOOP_TILES") == "0" else "k_iltile")
+                                     + " (one instrumented fold after the timed region)",
                            "launches_per_fold": max(a.n - 6, 1), "avg_launch_us": il_launch_s * 1e6,
                            "algorithmic_bytes_per_fold": bytes_il},
     }

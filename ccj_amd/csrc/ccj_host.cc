@@ -149,7 +149,7 @@ struct ccj_ctx {
     int *d_ied = nullptr;                 // k_iltile energies [type][w][p][dt-3][32] (k_ie_tiles)
     int pbw = 0;
     std::vector<long long> tl_off;        // first tile of (level t, shard r) at t*world + r
-    bool il_tiles = false;                // CCJ_ILOOP_TILES=1: interior loops as LDS tiles (k_iltile, slower)
+    bool il_tiles = true;                 // interior loops as LDS tiles (k_iltile); CCJ_ILOOP_TILES=0: k_iloop work items
     size_t items_cap = 0;
     int16_t *d_send = nullptr, *d_recv = nullptr;  // band-sharded exchange: own slice, world slices
     std::vector<int> xnmax;               // per level: the largest rank's block count (slice = 22 x nmax x M)
@@ -1698,7 +1698,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         // partition each span instead, and the level-t exchange carries span t
         c->join_diag = !(c->world > 1 && !c->simulate);
         const char *ii = getenv("CCJ_ILOOP_TILES");
-        c->il_tiles = ii && atoi(ii) != 0;
+        c->il_tiles = !(ii && atoi(ii) == 0);
         const char *g = getenv("CCJ_SHARE_SPLITS");
         c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
     }
@@ -1893,17 +1893,19 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
             HIPCHK(cp, hipMalloc(&c->d_tiles, std::max<size_t>(tiles.size(), 1) * sizeof(uint32_t)));
             HIPCHK(cp, hipMemcpy(c->d_tiles, tiles.data(), tiles.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         }
-        const size_t pairs = (size_t)(n + 1) * c->rs;
-        const size_t ents = pairs * IL_CAP;
-        HIPCHK(cp, hipMalloc(&c->d_il, ents * sizeof(uint2)));
-        HIPCHK(cp, hipMalloc(&c->d_ilm, ents * sizeof(uint2)));
         std::vector<int16_t> dummy((size_t)n + 64, (int16_t)INTERN_INF);
         HIPCHK(cp, hipMalloc(&c->d_dummy, dummy.size() * sizeof(int16_t)));
         HIPCHK(cp, hipMemcpy(c->d_dummy, dummy.data(), dummy.size() * sizeof(int16_t), hipMemcpyHostToDevice));
-        HIPCHK(cp, hipMalloc(&c->d_ilseg, pairs * IL_SEG * sizeof(uint32_t)));
-        HIPCHK(cp, hipMalloc(&c->d_ilmseg, pairs * IL_SEG * sizeof(uint32_t)));
-        HIPCHK(cp, hipMemset(c->d_ilseg, 0, pairs * IL_SEG * sizeof(uint32_t)));
-        HIPCHK(cp, hipMemset(c->d_ilmseg, 0, pairs * IL_SEG * sizeof(uint32_t)));
+        if (!c->il_tiles) {  // the k_iloop work items' candidate lists (k_build_il)
+            const size_t pairs = (size_t)(n + 1) * c->rs;
+            const size_t ents = pairs * IL_CAP;
+            HIPCHK(cp, hipMalloc(&c->d_il, ents * sizeof(uint2)));
+            HIPCHK(cp, hipMalloc(&c->d_ilm, ents * sizeof(uint2)));
+            HIPCHK(cp, hipMalloc(&c->d_ilseg, pairs * IL_SEG * sizeof(uint32_t)));
+            HIPCHK(cp, hipMalloc(&c->d_ilmseg, pairs * IL_SEG * sizeof(uint32_t)));
+            HIPCHK(cp, hipMemset(c->d_ilseg, 0, pairs * IL_SEG * sizeof(uint32_t)));
+            HIPCHK(cp, hipMemset(c->d_ilmseg, 0, pairs * IL_SEG * sizeof(uint32_t)));
+        }
     }
     HIPCHK(cp, hipMalloc(&c->d2i, A2_N * plane * sizeof(int)));
     HIPCHK(cp, hipMalloc(&c->d_wbw, plane * sizeof(int2)));

@@ -4,7 +4,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/ilpmc
 C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_SMEM"
 for v in tile items; do
-  [ $v = tile ] && export CCJ_ILOOP_TILES=1; [ $v = items ] && unset CCJ_ILOOP_TILES
+  [ $v = tile ] && export CCJ_ILOOP_TILES=1; [ $v = items ] && export CCJ_ILOOP_TILES=0
   timeout -k 10 -s KILL 200 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex "k_iltile|k_iloop" --pmc $C -d gpurun_out/ilpmc/$v -o p -- python3 tools/fold_once.py 200 > gpurun_out/ilpmc/$v.log 2>&1 || exit 1
   f=$(find gpurun_out/ilpmc/$v -name "*counter_collection.csv" | head -1)
   python3 - "$f" <<'PY'

@@ -3,7 +3,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 rm -rf gpurun_out/tlev; mkdir -p gpurun_out/tlev
 for v in items tile; do
-  [ $v = tile ] && export CCJ_ILOOP_TILES=1
+  [ $v = tile ] && export CCJ_ILOOP_TILES=1; [ $v = items ] && export CCJ_ILOOP_TILES=0
   timeout -k 10 -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tlev/$v -o p -- python3 tools/fold_once.py 200 > gpurun_out/tlev/$v.log 2>&1 || { echo "FAIL $v"; tail -5 gpurun_out/tlev/$v.log; exit 1; }
 done
 python3 - <<'PY'
