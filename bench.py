@@ -484,12 +484,17 @@ def main(argv=None):
     # (tools/gpu_profile.sh -> tools/make_profiles.py -> profiles/traffic.json); null when no
     # profile of this configuration is committed (it is not measured inside this run)
     traffic = traffic_src = None
+    il_kernel = "k_iloop" if os.environ.get("CCJ_ILOOP_TILES") == "0" else "k_iltile"
+    il_traffic = None
     tj, tname = find_traffic(a.n, a.seed, a.params) if world == 1 or not shard else (None, None)
     if tj:
         tk = tj["kernels"].get("k_level4d_level")
         if tk:
             traffic = tk["hbm_bytes_per_launch"]
             traffic_src = f"profiles/{tname} (" + tj.get("source", "rocprofv3 PMC passes") + ")"
+        ti = tj["kernels"].get(il_kernel)
+        if ti:
+            il_traffic = ti["hbm_bytes_per_launch"]
 
     if rank != 0:
         if dist is not None:
@@ -551,10 +556,10 @@ def main(argv=None):
                      "achieved_counter_gbs": (traffic / avg_launch_s / 1e9) if traffic and avg_launch_s > 0 else None},
         "roofline_iloop": {"bound": "hbm", "achieved": il_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": il_achieved / HBM_PEAK_GBS,
-                           "kernel": ("k_iloop" if os.environ.get("CCJ_ILOOP_TILES") == "0" else "k_iltile")
-                                     + " (one instrumented fold after the timed region)",
+                           "kernel": il_kernel + " (one instrumented fold after the timed region)",
                            "launches_per_fold": max(a.n - 6, 1), "avg_launch_us": il_launch_s * 1e6,
-                           "algorithmic_bytes_per_fold": bytes_il},
+                           "algorithmic_bytes_per_fold": bytes_il, "traffic": il_traffic, "traffic_unit": "bytes/launch",
+                           "frac_counter": (il_traffic / il_launch_s / 1e9 / HBM_PEAK_GBS) if il_traffic and il_launch_s > 0 else None},
     }
     # the algorithmic model charges every operand read (split-sharing and the caches serve many of
     # them); when its bytes per fold exceed what HBM could move in the fold's time it is an
