@@ -149,7 +149,7 @@ struct ccj_ctx {
     int *d_ied = nullptr;                 // k_iltile energies [type][w][p][dt-3][32] (k_ie_tiles)
     int pbw = 0;
     std::vector<long long> tl_off;        // first tile of (level t, shard r) at t*world + r
-    bool il_tiles = true;                 // interior loops as LDS tiles (k_iltile); CCJ_ILOOP_TILES=0: k_iloop work items
+    bool il_tiles = false;                // CCJ_ILOOP_TILES=1: interior loops as LDS tiles (k_iltile) instead of k_iloop work items
     size_t items_cap = 0;
     int16_t *d_send = nullptr, *d_recv = nullptr;  // band-sharded exchange: own slice, world slices
     std::vector<int> xnmax;               // per level: the largest rank's block count (slice = 22 x nmax x M)
@@ -1610,14 +1610,14 @@ static int seq_setup(ccj_ctx *c) {
             int rs;
             int operator()(int i, int j) const { return pt[(size_t)(j - i) * rs + i]; }
         } hpt{pt.data(), rs};
-        std::vector<long long> cnt((size_t)nb, 0);
-        // default: counted on the GPU by k_items (0.2 ms + one round trip; 0.5 ms setup at n=200);
-        // CCJ_HOST_COUNT=1: on host threads (≈1 ms, but no device round trip, so a reset never
-        // waits behind another context's fill on a shared hardware queue)
+        std::vector<long long> cnt((size_t)nb, 0), cnt2((size_t)nb * KI_SPLIT, 0);  // per (t, r) / per split
+        // default: counted on the GPU by k_items (KI_SPLIT workgroups per level, then one round
+        // trip); CCJ_HOST_COUNT=1: on host threads (slower, but no device round trip, so a reset
+        // never waits behind another context's fill on a shared hardware queue)
         static const bool host_count = getenv("CCJ_HOST_COUNT") && atoi(getenv("CCJ_HOST_COUNT")) != 0;
         if (!host_count) {
             HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, nullptr, nullptr, 0, c->st));
-            HIPCHK(cp, hipMemcpyAsync(cnt.data(), c->d_icount, nb * sizeof(long long), hipMemcpyDeviceToHost, c->st));
+            HIPCHK(cp, hipMemcpyAsync(cnt2.data(), c->d_icount, cnt2.size() * sizeof(long long), hipMemcpyDeviceToHost, c->st));
             HIPCHK(cp, hipStreamSynchronize(c->st));
         }
         std::atomic<int> next{0};
@@ -1628,20 +1628,27 @@ static int seq_setup(ccj_ctx *c) {
                 const int t = b / G, r = b % G;
                 if (!(c->simulate || r == c->rank) || t < 4 || t >= c->nlev) continue;
                 const long long hc = count_level_items(pt.data(), rs, n, t, G, r, IL_CW);
-                if (!host_count && hc != cnt[b]) bad = true;  // check mode: host and GPU counts agree
-                cnt[b] = hc;
-                if (check) {  // CCJ_CHECK_ITEMS=1: the generic enumeration must agree
+                long long gpu = 0;
+                for (int s = 0; s < KI_SPLIT; ++s) gpu += cnt2[(size_t)b * KI_SPLIT + s];
+                if (!host_count && hc != gpu) bad = true;  // check mode: host and GPU counts agree
+                if (host_count || check) {  // the generic enumeration per split (host mode sizes the splits with it)
                     const ItemRows R = item_rows(n, t, G, r);
                     long long sum = 0;
                     uint32_t it0;
-                    for (int x = 0; x < R.nPL + R.nPR + R.nPM; ++x) sum += item_row(hpt, n, t, R, x, G, r, it0, IL_CW);
-                    if (sum != cnt[b]) bad = true;
+                    for (int s = 0; s < KI_SPLIT; ++s) {
+                        int lo, hi;
+                        ki_split_rows(R.nPL + R.nPR + R.nPM, s, lo, hi);
+                        long long cs = 0;
+                        for (int x = lo; x < hi; ++x) cs += item_row(hpt, n, t, R, x, G, r, it0, IL_CW);
+                        if (host_count) cnt2[(size_t)b * KI_SPLIT + s] = cs;
+                        else if (cs != cnt2[(size_t)b * KI_SPLIT + s]) bad = true;
+                        sum += cs;
+                    }
+                    if (sum != hc) bad = true;
                 }
             }
         };
         if (host_count || check) {
-            if (!host_count) next = nb;  // check mode only: the GPU counts stay
-            if (check) next = 0;
             const int nth = std::max(1, std::min<int>(8, (int)std::thread::hardware_concurrency()));
             std::vector<std::thread> pool;
             for (int x = 1; x < nth; ++x) pool.emplace_back(worker);
@@ -1649,6 +1656,8 @@ static int seq_setup(ccj_ctx *c) {
             for (auto &th : pool) th.join();
         }
         if (bad) return set_err(cp, CCJ_E_STATE, "k_iloop item count pass disagrees with the enumeration");
+        for (int b = 0; b < nb; ++b)
+            for (int s = 0; s < KI_SPLIT; ++s) cnt[b] += cnt2[(size_t)b * KI_SPLIT + s];
         c->it_off.assign((size_t)nb + 1, 0);
         for (int x = 0; x < nb; ++x) c->it_off[x + 1] = c->it_off[x] + cnt[x];
         const size_t total = (size_t)c->it_off[nb];
@@ -1660,10 +1669,18 @@ static int seq_setup(ccj_ctx *c) {
             HIPCHK(cp, hipMalloc(&c->d_items, c->items_cap * sizeof(uint32_t)));
         }
         c->T.items = c->d_items;
-        // pinned staging so the upload is asynchronous on st (the fill's first launches follow it)
-        if (!c->h_ioff) HIPCHK(cp, hipHostMalloc(&c->h_ioff, ((size_t)nb + 1) * sizeof(long long), hipHostMallocDefault));
-        memcpy(c->h_ioff, c->it_off.data(), ((size_t)nb + 1) * sizeof(long long));
-        HIPCHK(cp, hipMemcpyAsync(c->d_ioff, c->h_ioff, (nb + 1) * sizeof(long long), hipMemcpyHostToDevice, c->st));
+        // the first item of every split, through pinned staging so the upload is asynchronous on st
+        // (the fill's first launches follow it)
+        const size_t nsp = (size_t)nb * KI_SPLIT;
+        if (!c->h_ioff) HIPCHK(cp, hipHostMalloc(&c->h_ioff, nsp * sizeof(long long), hipHostMallocDefault));
+        for (int b = 0; b < nb; ++b) {
+            long long o = c->it_off[b];
+            for (int s = 0; s < KI_SPLIT; ++s) {
+                c->h_ioff[(size_t)b * KI_SPLIT + s] = o;
+                o += cnt2[(size_t)b * KI_SPLIT + s];
+            }
+        }
+        HIPCHK(cp, hipMemcpyAsync(c->d_ioff, c->h_ioff, nsp * sizeof(long long), hipMemcpyHostToDevice, c->st));
         HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, c->d_ioff, c->d_items, 1, c->st));
     }
     HIPCHK(cp, up(c->d_hp, hp.data(), plane * sizeof(int)));
@@ -1698,7 +1715,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         // partition each span instead, and the level-t exchange carries span t
         c->join_diag = !(c->world > 1 && !c->simulate);
         const char *ii = getenv("CCJ_ILOOP_TILES");
-        c->il_tiles = !(ii && atoi(ii) == 0);
+        c->il_tiles = ii && atoi(ii) != 0;
         const char *g = getenv("CCJ_SHARE_SPLITS");
         c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
     }
@@ -2012,8 +2029,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.accC = accC;
     {
         const int G = c->world;
-        HIPCHK(cp, hipMalloc(&c->d_icount, (size_t)n * G * sizeof(long long)));
-        HIPCHK(cp, hipMalloc(&c->d_ioff, ((size_t)n * G + 1) * sizeof(long long)));
+        HIPCHK(cp, hipMalloc(&c->d_icount, (size_t)n * G * KI_SPLIT * sizeof(long long)));
+        HIPCHK(cp, hipMalloc(&c->d_ioff, (size_t)n * G * KI_SPLIT * sizeof(long long)));
         if (G > 1 && !c->simulate) {
             // exchange slices: per level, 22 matrices x the largest rank's blocks x M
             c->xnmax.assign(n, 0);

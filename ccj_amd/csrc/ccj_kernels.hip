@@ -542,9 +542,12 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
 //         u2 <= b-2 are checked per lane by k_iloop).
 // Only candidates whose other pair can pair are kept (the reference skips the rest: can_pair),
 // in order of dt = 2+u1+u2 (the source level distance), u1 ascending; seg[dt] is the first entry
-// of dt.  One wave per pair: lane = u1, ballot compaction.
+// of dt.  One wave per pair: the window's validity and energies are gathered at once (lane = u1)
+// into LDS, then compacted per dt (lane = u1, ballot).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
+    __shared__ int16_t es[IE_U][IE_U + 1];  // [u1][u2]: the window's energies
+    __shared__ uint32_t vb[IE_U];            // [u1]: bit u2 = the candidate is kept
     const int n = T.n, rs = T.rs;
     const int p = blockIdx.x + 1, w = blockIdx.y, kind = blockIdx.z;
     const int q = p + w;
@@ -553,13 +556,14 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
     const size_t pidx = (size_t)w * rs + p;
     uint32_t *seg = (kind ? T.ilmseg : T.ilseg) + pidx * IL_SEG;
     uint2 *ent = (kind ? T.ilm : T.il) + pidx * IL_CAP;
-    int cnt = 0;
-    for (int dt = 0; dt < IL_SEG; ++dt) {
-        if (lane == 0) seg[dt] = (uint32_t)cnt;
-        const int u1 = lane, u2 = dt - 2 - lane;
-        bool valid = false;
-        int e = 0;
-        if (dt >= 2 && u1 < IE_U && u2 >= 0 && u2 < IE_U) {
+    // the whole window at once (lane = u1, every u2): one memory round trip for its loads
+    if (lane < IE_U) {
+        const int u1 = lane;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int u2 = 0; u2 < IE_U; ++u2) {
+            bool valid = false;
+            int e = 0;
             if (kind == 0) {
                 const int d = p + 1 + u1, dp = q - 1 - u2;
                 if (u1 <= imin(w, MAXLOOP) - 2 && u2 <= imin(w - u1 - 6, MAXLOOP - 2) && T.pt[(dp - d) * rs + d] > 0) {
@@ -573,11 +577,21 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
                     e = T.ie[((size_t)(u1 * IE_U + u2) * (n + 1) + (dp - d)) * rs + d];
                 }
             }
+            es[u1][u2] = (int16_t)e;
+            bits |= (valid ? 1u : 0u) << u2;
         }
+        vb[u1] = bits;
+    }
+    __syncthreads();
+    int cnt = 0;
+    for (int dt = 0; dt < IL_SEG; ++dt) {
+        if (lane == 0) seg[dt] = (uint32_t)cnt;
+        const int u1 = lane, u2 = dt - 2 - lane;
+        const bool valid = dt >= 2 && u1 < IE_U && u2 >= 0 && u2 < IE_U && ((vb[u1] >> u2) & 1u);
         const unsigned long long mask = __ballot(valid);
         if (valid)
             ent[cnt + __popcll(mask & ((1ull << lane) - 1))] =
-                make_uint2(((uint32_t)dt << 21) | ((uint32_t)u1 << 16) | (uint32_t)(uint16_t)e, (uint32_t)(2 * u1 * dt));
+                make_uint2(((uint32_t)dt << 21) | ((uint32_t)u1 << 16) | (uint32_t)(uint16_t)es[u1][u2], (uint32_t)(2 * u1 * dt));
         cnt += __popcll(mask);
     }
     // null tail: dt 63 addresses T.dummy (32767), energy 32767 -> 65534, never below a clamped result
@@ -592,9 +606,10 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
 //   PR (role 1): for own a in [0, t-6], q < m:        pair (k, k+t-a), k = q+a+3, chunks over i <= q+1
 //   PM (role 2): for h in [2, m-1], j in [1, n]:      pair (j, k = j+h+2), chunks over the own a in [alo, ahi]
 // ("own": the rank's a-blocks, ccj_engine.h shard_a; every a when unsharded)
-// in this enumeration order (measured no slower than heaviest-list-first).  One workgroup per
-// (level t, shard r) walks its "rows" (one closing pair each) 256 at a time; pass 0 counts the
-// items, pass 1 writes them at offs[t*G+r] + an exclusive scan of the row counts.
+// in this enumeration order (measured no slower than heaviest-list-first).  KI_SPLIT workgroups per
+// (level t, shard r) each walk one run of its "rows" (one closing pair each) 256 at a time; pass 0
+// counts the items of each run, pass 1 writes them at offs[(t*G+r)*KI_SPLIT+s] + an exclusive scan
+// of the row counts.
 // ------------------------------------------------------------------------------------------
 // the row enumeration (ItemRows, item_row) is shared with the host's count pass: ccj_items.h
 struct DevPT {
@@ -607,21 +622,23 @@ __global__ __launch_bounds__(256) void k_items(DevTables T, int G, int rank, int
                                                int pass) {
     __shared__ int wsum[4];
     __shared__ long long tot;
-    const int b = blockIdx.x, t = b / G, r = b - t * G;
+    // workgroup = (level t, shard r, split s): rows [lo, hi) of the level (ccj_items.h ki_split_rows)
+    const int bs = blockIdx.x, b = bs / KI_SPLIT, sp = bs - b * KI_SPLIT, t = b / G, r = b - t * G;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const bool mine = simulate || r == rank;
     if (!mine || t < 4 || t >= T.nlev) {
-        if (pass == 0 && tid == 0) counts[b] = 0;
+        if (pass == 0 && tid == 0) counts[bs] = 0;
         return;  // whole workgroup
     }
     const ItemRows R = item_rows(T.n, t, G, r);
     const DevPT pt{&T};
-    const int nrows = R.nPL + R.nPR + R.nPM;
-    long long base = pass ? offs[b] : 0;
-    for (int c0 = 0; c0 < nrows; c0 += 256) {
+    int lo, hi;
+    ki_split_rows(R.nPL + R.nPR + R.nPM, sp, lo, hi);
+    long long base = pass ? offs[bs] : 0;
+    for (int c0 = lo; c0 < hi; c0 += 256) {
         const int x = c0 + tid;
         uint32_t it0 = 0;
-        const int cnt = x < nrows ? item_row(pt, T.n, t, R, x, G, r, it0, IL_CW) : 0;
+        const int cnt = x < hi ? item_row(pt, T.n, t, R, x, G, r, it0, IL_CW) : 0;
         // exclusive scan of cnt over the workgroup: wave scan, then the wave totals
         int inc = cnt;
 #pragma unroll
@@ -643,13 +660,13 @@ __global__ __launch_bounds__(256) void k_items(DevTables T, int G, int rank, int
     }
     if (pass == 0 && tid == 0) {
         tot = base;
-        counts[b] = tot;
+        counts[bs] = tot;
     }
 }
 
 extern "C" int ccjk_items(const DevTables *T, int G, int rank, int simulate, long long *counts, const long long *offs,
                           uint32_t *items, int pass, void *stream) {
-    const int blocks = T->n * G;
+    const int blocks = T->n * G * KI_SPLIT;
     if (blocks <= 0) return 0;
     hipLaunchKernelGGL(k_items, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *T, G, rank, simulate, counts,
                        offs, items, pass);

@@ -1,10 +1,10 @@
 """The interior-loop work decompositions checked against the reference (-m gpu): the default
-k_iltile tiles (16 keys x 64 cells, sequence-independent) and the k_iloop work items
-(CCJ_ILOOP_TILES=0; ccj_items.h, 128-cell items), the items enumerated three ways, each unsharded
-and band-sharded.
+k_iloop work items (ccj_items.h, 128-cell items), enumerated three ways, and the k_iltile tiles
+(CCJ_ILOOP_TILES=1: 16 keys x 64 cells, sequence-independent), each unsharded and
+band-sharded.
 
-In items mode ccj_reset sizes the k_iloop launches from per-(level, shard) item counts made on the
-GPU by k_items; the host holds the same enumeration twice (count_level_items, the fast row walk, and
+In items mode ccj_reset sizes the k_iloop launches from per-(level, shard, split) item counts made
+on the GPU by k_items; the host holds the same enumeration twice (count_level_items, the fast row walk, and
 the generic item_row).  With CCJ_CHECK_ITEMS=1 every reset recomputes both on the host and fails
 with CCJ_E_STATE if either disagrees with the GPU's count; CCJ_HOST_COUNT=1 sizes the launches from
 the host count alone.  The switches are read once per process, so each mode runs in a child

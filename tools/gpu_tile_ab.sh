@@ -1,4 +1,4 @@
-# k_iltile (default) vs the k_iloop work items (CCJ_ILOOP_TILES=0): parity of the tile path on the
+# k_iltile (CCJ_ILOOP_TILES=1) vs the default k_iloop work items: parity of the tile path on the
 # reference goldens (n=100/150, unsharded and band-sharded), then alternating fill timings at n=200.
 mkdir -p gpurun_out
 echo "== tiles parity" && { timeout -k 10 400 python -u -m pytest tests/test_gpu_items.py -x -q --timeout 380 --timeout-method thread -k tiles > gpurun_out/tile_parity.log 2>&1; rc=$?; tail -3 gpurun_out/tile_parity.log; [ $rc -eq 0 ]; } && \
