@@ -156,6 +156,7 @@ struct ccj_ctx {
     ccj_group *lgroup = nullptr;          // in-process exchange between contexts (tests), else RCCL
     long long *d_icount = nullptr, *d_ioff = nullptr;  // k_items: items per (t, r), first item
     long long *h_ioff = nullptr;          // pinned staging of it_off
+    long long *h_icount = nullptr;        // pinned landing of the k_items counts (so the copy is asynchronous)
     void *h_stage = nullptr;              // pinned staging of the sequence tables
     hipEvent_t ev_stage = nullptr;        // the uploads from the staging (and h_ioff) are done
     std::vector<long long> it_off;        // first item of (level t, shard r) at t*world + r
@@ -1548,27 +1549,36 @@ static int seq_setup(ccj_ctx *c) {
     c->hpt_h.assign(plane, 0);
     for (int w = 0; w < n; ++w)
         for (int p = 1; p + w <= n; ++p) {
-            const int q = p + w;
             const size_t x = (size_t)w * c->rs + p;
-            const int tc = c->pair[c->S[p]][c->S[q]];
+            const int tc = c->pair[c->S[p]][c->S[p + w]];
             pt[x] = (int8_t)tc;
             c->hpt_h[x] = tc;
-            // HairpinE, s_energy_matrix.cc:275-282
-            hp[x] = (tc == 0) ? INF
-                              : E_Hairpin_host(&c->prm, c->lx.data(), w - 1, tc, c->S1[p + 1], c->S1[q - 1],
-                                               c->seq.c_str() + p - 1);
-            // get_e_stP, pseudo_loop.cc:828-834 (saturated, see k_precompute_ie)
-            if (q - p >= 2 && p + 1 != q - 1) {
-                const int t2 = c->pair[c->S[p + 1]][c->S[q - 1]];
-                const int e = E_IntLoop(&c->prm, c->lx.data(), 0, 0, tc, c->rtype[t2], c->S1[p + 1], c->S1[q - 1],
-                                        c->S1[p], c->S1[q]);
-                const long v = lrint(c->e_stP * e);
-                if (v < -32768) return set_err(cp, CCJ_E_PARAMS, "e_stP below int16 range");
-                if (tc > 0 && t2 > 0 && v >= INTERN_INF) return set_err(cp, CCJ_E_PARAMS, "e_stP of a canonical stack >= 32767");
-                est[x] = (int16_t)(v >= INTERN_INF ? INTERN_INF : v);
-            }
         }
-    lap("tables");
+    // the energy tables, built on the host while the GPU counts the work items (below)
+    const char *tab_err = nullptr;
+    auto energy_tables = [&]() {
+        for (int w = 0; w < n; ++w)
+            for (int p = 1; p + w <= n; ++p) {
+                const int q = p + w;
+                const size_t x = (size_t)w * c->rs + p;
+                const int tc = pt[x];
+                // HairpinE, s_energy_matrix.cc:275-282
+                hp[x] = (tc == 0) ? INF
+                                  : E_Hairpin_host(&c->prm, c->lx.data(), w - 1, tc, c->S1[p + 1], c->S1[q - 1],
+                                                   c->seq.c_str() + p - 1);
+                // get_e_stP, pseudo_loop.cc:828-834 (saturated, see k_precompute_ie)
+                if (q - p >= 2 && p + 1 != q - 1) {
+                    const int t2 = c->pair[c->S[p + 1]][c->S[q - 1]];
+                    const int e = E_IntLoop(&c->prm, c->lx.data(), 0, 0, tc, c->rtype[t2], c->S1[p + 1], c->S1[q - 1],
+                                            c->S1[p], c->S1[q]);
+                    const long v = lrint(c->e_stP * e);
+                    if (v < -32768) { tab_err = "e_stP below int16 range"; return; }
+                    if (tc > 0 && t2 > 0 && v >= INTERN_INF) { tab_err = "e_stP of a canonical stack >= 32767"; return; }
+                    est[x] = (int16_t)(v >= INTERN_INF ? INTERN_INF : v);
+                }
+            }
+    };
+    lap("pair types");
     // the sequence tables go up asynchronously on st from pinned staging (a reset never blocks on
     // work another context has running on the GPU); the fill's launches follow on st
     // pairability bits (k_iltile): row w, bit p = pair (p, p+w) can pair
@@ -1617,9 +1627,17 @@ static int seq_setup(ccj_ctx *c) {
         static const bool host_count = getenv("CCJ_HOST_COUNT") && atoi(getenv("CCJ_HOST_COUNT")) != 0;
         if (!host_count) {
             HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, nullptr, nullptr, 0, c->st));
-            HIPCHK(cp, hipMemcpyAsync(cnt2.data(), c->d_icount, cnt2.size() * sizeof(long long), hipMemcpyDeviceToHost, c->st));
+            if (!c->h_icount) HIPCHK(cp, hipHostMalloc(&c->h_icount, cnt2.size() * sizeof(long long), hipHostMallocDefault));
+            HIPCHK(cp, hipMemcpyAsync(c->h_icount, c->d_icount, cnt2.size() * sizeof(long long), hipMemcpyDeviceToHost, c->st));
+            energy_tables();
+            lap("tables");
             HIPCHK(cp, hipStreamSynchronize(c->st));
+            memcpy(cnt2.data(), c->h_icount, cnt2.size() * sizeof(long long));
+        } else {
+            energy_tables();
+            lap("tables");
         }
+        if (tab_err) return set_err(cp, CCJ_E_PARAMS, "%s", tab_err);
         std::atomic<int> next{0};
         static const bool check = getenv("CCJ_CHECK_ITEMS") && atoi(getenv("CCJ_CHECK_ITEMS")) != 0;
         std::atomic<bool> bad{false};
@@ -1682,6 +1700,10 @@ static int seq_setup(ccj_ctx *c) {
         }
         HIPCHK(cp, hipMemcpyAsync(c->d_ioff, c->h_ioff, nsp * sizeof(long long), hipMemcpyHostToDevice, c->st));
         HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, c->d_ioff, c->d_items, 1, c->st));
+    }
+    if (c->il_tiles) {
+        energy_tables();
+        if (tab_err) return set_err(cp, CCJ_E_PARAMS, "%s", tab_err);
     }
     HIPCHK(cp, up(c->d_hp, hp.data(), plane * sizeof(int)));
     HIPCHK(cp, up(c->d_est, est.data(), plane * sizeof(int16_t)));
@@ -2922,6 +2944,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_recv);
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->h_ioff) hipHostFree(c->h_ioff);
+    if (c->h_icount) hipHostFree(c->h_icount);
     if (c->ev_stage) hipEventDestroy(c->ev_stage);
     if (c->hr_W) hipHostFree(c->hr_W);
     if (c->hr_fp) hipHostFree(c->hr_fp);
