@@ -552,6 +552,8 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
     const int p = blockIdx.x + 1, w = blockIdx.y, kind = blockIdx.z;
     const int q = p + w;
     if (q > n) return;
+    // k_iloop reads only the lists of pairs that can pair (its items exist only for those)
+    if (T.pt[(size_t)w * rs + p] <= 0) return;
     const int lane = threadIdx.x;
     const size_t pidx = (size_t)w * rs + p;
     uint32_t *seg = (kind ? T.ilmseg : T.ilseg) + pidx * IL_SEG;
