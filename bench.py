@@ -458,7 +458,7 @@ def main(argv=None):
     structure, energy = acc["last"].structure, acc["last"].energy
     wf = ctxs[0]
     # after the timed region: one fold with marker events around every launch (per-kernel-family
-    # times for the interior loops (k_iloop, or k_iltile with CCJ_ILOOP_TILES=1) / k_diag2d; the
+    # times for the interior loops (k_iloop) / k_diag2d; the
     # markers slow that fold down, so it is not part of `value`)
     wf.set_timing(2)
     wf.ccj()
@@ -484,7 +484,7 @@ def main(argv=None):
     # (tools/gpu_profile.sh -> tools/make_profiles.py -> profiles/traffic.json); null when no
     # profile of this configuration is committed (it is not measured inside this run)
     traffic = traffic_src = None
-    il_kernel = "k_iltile" if os.environ.get("CCJ_ILOOP_TILES", "0") not in ("", "0") else "k_iloop"
+    il_kernel = "k_iloop"
     il_traffic = None
     tj, tname = find_traffic(a.n, a.seed, a.params) if world == 1 or not shard else (None, None)
     if tj:

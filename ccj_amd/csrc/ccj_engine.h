@@ -111,24 +111,31 @@ __host__ __device__ __forceinline__ int shard_ceil(int x, int G, int r) {
     return (q / G) * SHARD_GRP + off;
 }
 
-// k_iltile: a tile is TL_NK consecutive keys x 64 cells, one cell per lane.  The PM
-// tiles are skewed: key kk (J = K0+kk) of tile x holds a = x0 + 64x + lane + kk, so that every key
-// of the tile reads the same 64-element source segment per row.  pm_tile_span: x0 = the smallest
-// a - kk over the tile's keys (J+g <= n, [alo, ahi] non-empty), xn = the number of 64-wide chunks
-// up to the largest a - kk.  Host (build_tiles) and kernel share it.
-constexpr int TL_NK = 16;
-__host__ __device__ inline void pm_tile_span(int n, int t, int g, int K0, int &x0, int &xn) {
-    int lo = 1 << 20, hi = -(1 << 20);
-    for (int kk = 0; kk < TL_NK; ++kk) {
-        const int J = K0 + kk, k = J + g;
-        if (J < 1 || k > n) continue;
-        const int alo = (t - (n - k)) > 2 ? t - (n - k) : 2, ahi = (t - 2) < (J - 1) ? t - 2 : J - 1;
-        if (alo > ahi) continue;
-        lo = (alo - kk) < lo ? alo - kk : lo;
-        hi = (ahi - kk) > hi ? ahi - kk : hi;
-    }
-    x0 = lo;
-    xn = hi >= lo ? (hi - lo) / 64 + 1 : 0;
+// The level-t exchange slice of a band-sharded fill, in int16 elements: the body
+// [matrix x][own index o][cell c] of nmax blocks per matrix (nmax = the largest rank's block count at
+// t, so every rank's slice has the same size and ONE all-gather moves a level), padded to 8 bytes,
+// then the P tail (XCH_PTAIL: (value, first split) uint64 per interval start 0..n) and the span tail
+// (XCH_DTAIL: XCH_DT_N int32 planes of n+1 entries).  k_pack / k_unpack / k_?tail_* and the host's
+// buffer sizing use these, and ccj_exchange_layout / ccj_exchange_index export them (tests).
+constexpr int XCH_DT_N = 10;  // span tail planes: V, Vt, P, WBP, WB, WPP, WP, WMv, WMp, WM
+__host__ __device__ __forceinline__ long long xch_body(int nmax, int M) { return ((long long)22 * nmax * M + 3) & ~3LL; }
+__host__ __device__ __forceinline__ long long xch_ptail(int n) { return 4LL * (n + 1); }
+__host__ __device__ __forceinline__ long long xch_dtail(int n) { return 2LL * XCH_DT_N * (n + 1); }
+__host__ __device__ __forceinline__ long long xch_slice(int n, int nmax, int M) { return xch_body(nmax, M) + xch_ptail(n) + xch_dtail(n); }
+// body position of matrix x, own block o, cell c
+__host__ __device__ __forceinline__ long long xch_pos(int x, int o, int c, int nmax, int M) {
+    return ((long long)x * nmax + o) * M + c;
+}
+// where block a's cells arrive: its owner's slice, at the owner's own index of a
+__host__ __device__ __forceinline__ void xch_src(int a, int G, int &owner, int &o) {
+    owner = shard_owner(a, G);
+    o = shard_count(a - 1, G, owner);
+}
+// the largest rank's block count at level t
+__host__ __device__ __forceinline__ int xch_nmax(int t, int G) {
+    int nm = 0;
+    for (int r = 0; r < G; ++r) nm = shard_count(t, G, r) > nm ? shard_count(t, G, r) : nm;
+    return nm;
 }
 
 struct LvlX {        // per-level bases of the interior-loop copies
@@ -179,10 +186,6 @@ struct DevTables {
     uint2 *il, *ilm;               // il: pair (p,p+w) closes the loop (PL, PR); ilm: pair encloses (PM)
     int16_t *dummy;                // n+64 values 32767: target of the null entries
     const uint32_t *items;         // k_iloop work items (role << 30 | f1 << 20 | f2 << 10 | chunk)
-    const uint32_t *tiles;         // k_iltile tiles (role << 30 | block << 20 | first key << 10 | cell chunk)
-    const unsigned long long *pb;  // pairability bits: [w][pbw words], bit p of row w = pt(p, p+w) > 0
-    int pbw;                       // 64-bit words per row (positions 0 .. n+1, plus one zero word)
-    int *ied;                      // k_iltile energies [type][w][p][dt-3][32] (k_ie_tiles)
     int mat5;                      // 1: the 5 record-only matrices are stored in d4 too (band-sharded exchange)
     uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
     int *err;                      // device error word
@@ -230,8 +233,6 @@ int ccjk_init2d(const ccj::DevTables *T, void *stream);
 int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
 int ccjk_build_il(const ccj::DevTables *T, void *stream);
 int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, int G, int rank, void *stream);
-int ccjk_ie_tiles(const ccj::DevTables *T, void *stream);
-int ccjk_iltile(const ccj::DevTables *T, int t, long long first_tile, int ntiles, int G, int rank, void *stream);
 int ccjk_diag2d(const ccj::DevTables *T, int sigma, int G, int rank, void *stream);
 int ccjk_dtail_pack(const ccj::DevTables *T, int sigma, int G, int rank, int16_t *tail, void *stream);
 int ccjk_dtail_unpack(const ccj::DevTables *T, int sigma, const int16_t *recv, size_t slice, size_t off, int G, int rank,

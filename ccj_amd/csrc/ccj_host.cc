@@ -144,12 +144,6 @@ struct ccj_ctx {
     uint2 *d_il = nullptr, *d_ilm = nullptr;
     int16_t *d_dummy = nullptr;
     uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
-    uint32_t *d_tiles = nullptr;          // k_iltile tiles, all levels back to back (sequence-independent)
-    unsigned long long *d_pb = nullptr;   // pairability bits [w][pbw] (k_iltile)
-    int *d_ied = nullptr;                 // k_iltile energies [type][w][p][dt-3][32] (k_ie_tiles)
-    int pbw = 0;
-    std::vector<long long> tl_off;        // first tile of (level t, shard r) at t*world + r
-    bool il_tiles = false;                // CCJ_ILOOP_TILES=1: interior loops as LDS tiles (k_iltile) instead of k_iloop work items
     size_t items_cap = 0;
     int16_t *d_send = nullptr, *d_recv = nullptr;  // band-sharded exchange: own slice, world slices
     std::vector<int> xnmax;               // per level: the largest rank's block count (slice = 22 x nmax x M)
@@ -1421,11 +1415,6 @@ extern "C" uint64_t ccj_num_cells(int n) {
 
 static thread_local std::string g_create_err;
 
-// int16 elements of the exchange slice's P tail: one 64-bit (value, first split) word per interval
-// start i = 0..n
-#define PTAIL_ELEMS(n) (4 * ((size_t)(n) + 1))
-// span tail (k_dtail_pack): 10 int32 planes of n+1 entries, the 2-D values of the span the level carries
-#define DTAIL_ELEMS(n) (2 * 10 * ((size_t)(n) + 1))
 
 // The exchange of one level through the in-process group: every member pulls each member's
 // packed slice into its own receive buffer (same device), between two barriers, so no slice is
@@ -1462,61 +1451,6 @@ static int local_allgather(ccj_ctx *c, size_t slice) {
     HIPCHK(c, e2);
     if (!g->barrier()) return set_err(c, CCJ_E_STATE, "local exchange: a group member failed");
     return CCJ_OK;
-}
-
-// k_iltile's tiles (ccj_kernels.hip), per level t and shard r in that order: one 32-bit word per
-// tile, role << 30 | block << 20 | first key << 10 | cell chunk (TL_NK keys x 64 cells):
-//   PL: own a in [6, t], keys i from 1 by 16 (i <= m), chunks of h over [0, m-i] (skewed: key kk
-//       of chunk x holds h = 64x + lane - kk)
-//   PR: own a in [0, t-6], keys q from 0 by 16 (q <= m-1), chunks of i over [1, q+1]
-//   PM: h in [2, m-1], keys j from 1 by 16 (j+h+2 <= n), skewed chunks of a over the keys' [alo, ahi]
-//       (every rank walks every a; each stores only its own)
-// Within a (level, shard) the tiles run longest first.  They depend only on n and the sharding, so
-// they are built once per context.
-static void build_tiles(int n, int nlev, int G, int rank, bool simulate, std::vector<uint32_t> &tiles,
-                        std::vector<long long> &off) {
-    constexpr int NK = TL_NK, NC = 64;
-    tiles.clear();
-    off.assign((size_t)n * G + 1, 0);
-    auto push = [&](int role, int blk, int K0, int xc) {
-        tiles.push_back(((uint32_t)role << 30) | ((uint32_t)blk << 20) | ((uint32_t)K0 << 10) | (uint32_t)xc);
-    };
-    for (int t = 0; t < n; ++t)
-        for (int r = 0; r < G; ++r) {
-            off[(size_t)t * G + r] = (long long)tiles.size();
-            if (!(simulate || r == rank) || t < 4 || t >= nlev) continue;
-            const int m = n - t - 2;
-            for (int a = 6; a <= t; ++a) {
-                if (shard_owner(a, G) != r) continue;
-                for (int K0 = 1; K0 <= m; K0 += NK)
-                    for (int xc = 0; xc * NC <= m - K0; ++xc) push(0, a, K0, xc);
-            }
-            for (int a = 0; a <= t - 6; ++a) {
-                if (shard_owner(a, G) != r) continue;
-                for (int K0 = 0; K0 <= m - 1; K0 += NK) {
-                    const int imax = std::min(K0 + NK - 1, m - 1) + 1;
-                    for (int xc = 0; 1 + xc * NC <= imax; ++xc) push(1, a, K0, xc);
-                }
-            }
-            for (int h = 2; h <= m - 1; ++h) {
-                const int g = h + 2;
-                for (int K0 = 1; K0 + g <= n; K0 += NK) {
-                    int x0, xn;  // skewed chunks (ccj_engine.h pm_tile_span)
-                    pm_tile_span(n, t, g, K0, x0, xn);
-                    for (int xc = 0; xc < xn; ++xc) push(2, h, K0, xc);
-                }
-            }
-            // longest first (the number of source-level distances a tile walks), so the short
-            // tiles fill in behind the long ones
-            auto ndt = [&](uint32_t w) {
-                const int role = (int)(w >> 30), blk = (int)((w >> 20) & 1023u);
-                const int hi = role == 0 ? blk - 4 : role == 1 ? t - blk - 4 : t - 2;
-                return std::max(0, std::min(58, hi) - 2);
-            };
-            std::stable_sort(tiles.begin() + off[(size_t)t * G + r], tiles.end(),
-                             [&](uint32_t x, uint32_t y) { return ndt(x) > ndt(y); });
-        }
-    off[(size_t)n * G] = (long long)tiles.size();
 }
 
 // Everything that depends on the sequence itself (not only on n): the encoding, the pair-type,
@@ -1581,13 +1515,7 @@ static int seq_setup(ccj_ctx *c) {
     lap("pair types");
     // the sequence tables go up asynchronously on st from pinned staging (a reset never blocks on
     // work another context has running on the GPU); the fill's launches follow on st
-    // pairability bits (k_iltile): row w, bit p = pair (p, p+w) can pair
-    std::vector<unsigned long long> pb((size_t)(n + 1) * c->pbw + 2, 0ull);
-    for (int w = 0; w < n; ++w)
-        for (int p = 1; p + w <= n; ++p)
-            if (pt[(size_t)w * c->rs + p] > 0) pb[(size_t)w * c->pbw + (p >> 6)] |= 1ull << (p & 63);
-    const size_t pb_bytes = pb.size() * sizeof(unsigned long long);
-    const size_t stage_bytes = plane * (1 + sizeof(int) + sizeof(int16_t)) + 2 * (size_t)(n + 2) * sizeof(short) + pb_bytes;
+    const size_t stage_bytes = plane * (1 + sizeof(int) + sizeof(int16_t)) + 2 * (size_t)(n + 2) * sizeof(short);
     if (!c->h_stage) {
         HIPCHK(cp, hipHostMalloc(&c->h_stage, stage_bytes, hipHostMallocDefault));
         HIPCHK(cp, hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
@@ -1602,16 +1530,14 @@ static int seq_setup(ccj_ctx *c) {
         return e;
     };
     HIPCHK(cp, up(c->d_pt, pt.data(), plane));
-    HIPCHK(cp, up(c->d_pb, pb.data(), pb_bytes));
     // ---- k_iloop work items (one per wave), counted per (level, shard), then written by k_items
     // on the GPU at the prefix offsets.  By default the count pass runs on the GPU too (k_items
     // pass 0 on st) and the host WAITS for it (hipStreamSynchronize): the offsets are needed on
     // the host to size the k_iloop launches, so ccj_reset blocks until the context's stream has
     // run it.  CCJ_HOST_COUNT=1 counts on host threads instead (the same enumeration, ccj_items.h;
-    // (only for the k_iloop path: the k_iltile tiles do not depend on the sequence)
     // slower, ~1.3 ms at n=200, but no device round trip).
     if (n > 1023) return set_err(cp, CCJ_E_ARG, "sequence longer than 1023 (k_iloop item encoding)");
-    if (!c->il_tiles) {
+    {
         const int G = c->world;
         const int nb = n * G;
         const int rs = c->rs;
@@ -1701,10 +1627,6 @@ static int seq_setup(ccj_ctx *c) {
         HIPCHK(cp, hipMemcpyAsync(c->d_ioff, c->h_ioff, nsp * sizeof(long long), hipMemcpyHostToDevice, c->st));
         HIPCHK(cp, (hipError_t)ccjk_items(&c->T, G, c->rank, c->simulate, c->d_icount, c->d_ioff, c->d_items, 1, c->st));
     }
-    if (c->il_tiles) {
-        energy_tables();
-        if (tab_err) return set_err(cp, CCJ_E_PARAMS, "%s", tab_err);
-    }
     HIPCHK(cp, up(c->d_hp, hp.data(), plane * sizeof(int)));
     HIPCHK(cp, up(c->d_est, est.data(), plane * sizeof(int16_t)));
     HIPCHK(cp, up(c->d_S, c->S.data(), (n + 2) * sizeof(short)));
@@ -1736,8 +1658,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         // (fill -0.25 ms at n=200 in 3/3 alternating runs); band-sharded fills with an exchange
         // partition each span instead, and the level-t exchange carries span t
         c->join_diag = !(c->world > 1 && !c->simulate);
-        const char *ii = getenv("CCJ_ILOOP_TILES");
-        c->il_tiles = ii && atoi(ii) != 0;
         const char *g = getenv("CCJ_SHARE_SPLITS");
         c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
     }
@@ -1886,12 +1806,10 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
             return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for split-sharing records failed",
                            SHARE_SLOTS * SHARE_NACC * accC * 16e-9);
     }
-    HIPCHK(cp, hipMalloc(&c->d_ie, (ie_elems + 64) * sizeof(int16_t)));  // + k_iltile's 16-byte tail reads
+    HIPCHK(cp, hipMalloc(&c->d_ie, ie_elems * sizeof(int16_t)));
     HIPCHK(cp, hipMalloc(&c->d_est, plane * sizeof(int16_t)));
     HIPCHK(cp, hipMalloc(&c->d_hp, plane * sizeof(int)));
     HIPCHK(cp, hipMalloc(&c->d_pt, plane));
-    c->pbw = (n + 2 + 63) / 64 + 1;
-    HIPCHK(cp, hipMalloc(&c->d_pb, ((size_t)(n + 1) * c->pbw + 2) * sizeof(unsigned long long)));
     HIPCHK(cp, hipMalloc(&c->d_pair, 64));
     HIPCHK(cp, hipMalloc(&c->d_rtype, 8));
     HIPCHK(cp, hipMalloc(&c->d_lx, c->lx.size() * sizeof(int)));
@@ -1914,8 +1832,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         const size_t pad = 256;
         c->nx = ox;
         c->npm = op;
-        // pad elements on both sides: k_iltile's row loads start up to ~50 elements before a
-        // copy's first row and end up to 63 past its last (those lanes' values are never used)
+        // pad elements on both sides (slack for clamped partner offsets; never read as values)
         if (hipMalloc(&c->d4x_alloc, ((size_t)ox + 2 * pad) * sizeof(int16_t)) != hipSuccess ||
             hipMalloc(&c->pmx_alloc, ((size_t)op + 2 * pad) * sizeof(int16_t)) != hipSuccess)
             return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for interior-loop copies failed", (ox + op) * 2e-9);
@@ -1923,19 +1840,10 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         c->pmx = c->pmx_alloc + pad;
         HIPCHK(cp, hipMalloc(&c->d_ldx, ldx.size() * sizeof(LvlX)));
         HIPCHK(cp, hipMemcpy(c->d_ldx, ldx.data(), ldx.size() * sizeof(LvlX), hipMemcpyHostToDevice));
-        if (c->il_tiles) {
-            const size_t eb = 2 * (size_t)(n + 1) * c->rs * 56 * 32;  // ccj_kernels.hip TL_KEYW per key
-            if (hipMalloc(&c->d_ied, eb * sizeof(int)) != hipSuccess)
-                return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for the interior-loop energy rows failed", eb * 4e-9);
-            std::vector<uint32_t> tiles;
-            build_tiles(n, c->nlev, c->world, c->rank, c->simulate, tiles, c->tl_off);
-            HIPCHK(cp, hipMalloc(&c->d_tiles, std::max<size_t>(tiles.size(), 1) * sizeof(uint32_t)));
-            HIPCHK(cp, hipMemcpy(c->d_tiles, tiles.data(), tiles.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        }
         std::vector<int16_t> dummy((size_t)n + 64, (int16_t)INTERN_INF);
         HIPCHK(cp, hipMalloc(&c->d_dummy, dummy.size() * sizeof(int16_t)));
         HIPCHK(cp, hipMemcpy(c->d_dummy, dummy.data(), dummy.size() * sizeof(int16_t), hipMemcpyHostToDevice));
-        if (!c->il_tiles) {  // the k_iloop work items' candidate lists (k_build_il)
+        {  // the k_iloop work items' candidate lists (k_build_il)
             const size_t pairs = (size_t)(n + 1) * c->rs;
             const size_t ents = pairs * IL_CAP;
             HIPCHK(cp, hipMalloc(&c->d_il, ents * sizeof(uint2)));
@@ -2032,12 +1940,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.ilm = c->d_ilm;
     T.dummy = c->d_dummy;
     T.items = c->d_items;
-    T.tiles = c->d_tiles;
-    T.pb = c->d_pb;
     // the exchange packs all 22 matrices from d4; CCJ_MAT5=1 stores them in every fill (A/B timing)
     T.mat5 = ((c->world > 1 && !c->simulate) || (getenv("CCJ_MAT5") && atoi(getenv("CCJ_MAT5")) != 0)) ? 1 : 0;
-    T.ied = c->d_ied;
-    T.pbw = c->pbw;
     T.ilseg = c->d_ilseg;
     T.ilmseg = c->d_ilmseg;
     T.err = c->d_err;
@@ -2058,11 +1962,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
             c->xnmax.assign(n, 0);
             size_t slice = 0;
             for (int t = 0; t < c->nlev; ++t) {
-                int nm = 0;
-                for (int r = 0; r < G; ++r) nm = std::max(nm, shard_count(t, G, r));
+                const int nm = xch_nmax(t, G);
                 c->xnmax[t] = nm;
-                slice = std::max(slice, (((size_t)NMAT4 * nm * c->lv_host[t].M + 3) & ~(size_t)3) + PTAIL_ELEMS(n) +
-                                            DTAIL_ELEMS(n));
+                slice = std::max(slice, (size_t)xch_slice(n, nm, c->lv_host[t].M));
             }
             if (hipMalloc(&c->d_send, std::max<size_t>(slice, 1) * sizeof(int16_t)) != hipSuccess ||
                 hipMalloc(&c->d_recv, std::max<size_t>(slice * G, 1) * sizeof(int16_t)) != hipSuccess)
@@ -2140,8 +2042,7 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     HIPCHK(c, hipEventRecord(c->ev_start, st));
     HIPCHK(c, (hipError_t)ccjk_init2d(&c->T, st));
     HIPCHK(c, (hipError_t)ccjk_precompute_ie(&c->T, st));
-    if (!c->il_tiles) HIPCHK(c, (hipError_t)ccjk_build_il(&c->T, st));
-    else HIPCHK(c, (hipError_t)ccjk_ie_tiles(&c->T, st));
+    HIPCHK(c, (hipError_t)ccjk_build_il(&c->T, st));
     HIPCHK(c, hipEventRecord(c->ev_pre, st));
     // Four streams:
     //   st_d : k_diag2d(s)  needs P(s) (p_done) and spans < s (stream order)
@@ -2191,12 +2092,8 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
             for (int r = 0; r < G; ++r) {  // every rank's launches in simulation, else this rank's
                 if (!c->simulate && r != c->rank) continue;
                 const size_t tr = (size_t)s * G + r;
-                if (c->il_tiles)
-                    HIPCHK(c, (hipError_t)ccjk_iltile(&c->T, s, c->tl_off[tr], (int)(c->tl_off[tr + 1] - c->tl_off[tr]), G, r,
-                                                      c->st_il));
-                else
-                    HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[tr], (int)(c->it_off[tr + 1] - c->it_off[tr]), G, r,
-                                                     c->st_il));
+                HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[tr], (int)(c->it_off[tr + 1] - c->it_off[tr]), G, r,
+                                                 c->st_il));
             }
             HIPCHK(c, trec(3, c->st_il));
             if (joined) {
@@ -2224,9 +2121,9 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                 // pushed after level s-1), min-combined on arrival: P rides the level exchange, no
                 // extra collective.
                 const int nmax = c->xnmax[s];
-                const size_t slice4 = ((size_t)NMAT4 * nmax * c->lv_host[s].M + 3) & ~(size_t)3;
-                const size_t dt_off = slice4 + PTAIL_ELEMS(n);
-                const size_t slice = dt_off + DTAIL_ELEMS(n);
+                const size_t slice4 = (size_t)xch_body(nmax, c->lv_host[s].M);
+                const size_t dt_off = slice4 + (size_t)xch_ptail(n);
+                const size_t slice = (size_t)xch_slice(n, nmax, c->lv_host[s].M);
                 // span s (this rank's intervals) rides the same slice
                 HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s], 0));
                 HIPCHK(c, (hipError_t)ccjk_dtail_pack(&c->T, s, G, c->rank, c->d_send + dt_off, st));
@@ -2845,6 +2742,49 @@ extern "C" int ccj_level_layout(int n, int t, int world, long long *C, int *M) {
     return CCJ_OK;
 }
 
+// The exchange geometry k_pack / k_unpack use (ccj_engine.h xch_*), for tests and integrators.
+extern "C" int ccj_exchange_layout(int n, int t, int world, long long *out4) {
+    if (!out4 || world < 1 || t < 0 || n < 4 || t > n - 3) return CCJ_E_ARG;
+    const int m = n - t - 2, M = m * (m + 1) / 2, nmax = xch_nmax(t, world);
+    out4[0] = nmax;
+    out4[1] = xch_body(nmax, M);                   // P tail offset
+    out4[2] = xch_body(nmax, M) + xch_ptail(n);    // span tail offset
+    out4[3] = xch_slice(n, nmax, M);               // slice elements
+    return CCJ_OK;
+}
+
+// which == 0 (pack, rank `rank`): out[k] for every body element k of the rank's slice = the level
+//   element (x * C + a * M + c) k_pack copies there, -1 for padding;
+// which == 1 (unpack at rank `rank`): out[e] for every level element e = x * C + a * M + c = the
+//   position in the gathered buffer (owner * slice + body position) k_unpack reads it from, -1 for
+//   the rank's own cells.
+// Returns the number of entries (cap: the room in out), or -CCJ_E_ARG.
+extern "C" long long ccj_exchange_index(int n, int t, int world, int rank, int which, long long *out, long long cap) {
+    if (world < 1 || rank < 0 || rank >= world || t < 0 || n < 4 || t > n - 3 || (which != 0 && which != 1))
+        return -CCJ_E_ARG;
+    const int m = n - t - 2, M = m * (m + 1) / 2, nmax = xch_nmax(t, world);
+    const long long C = (long long)(t + 1) * M, slice = xch_slice(n, nmax, M);
+    const long long cnt = which == 0 ? (long long)NMAT4 * nmax * M : (long long)NMAT4 * C;
+    if (cap < cnt || !out) return cnt;
+    if (which == 0) {
+        for (long long k = 0; k < cnt; ++k) out[k] = -1;
+        const int own = shard_count(t, world, rank);
+        for (int x = 0; x < NMAT4; ++x)
+            for (int o = 0; o < own; ++o)
+                for (int c = 0; c < M; ++c)
+                    out[xch_pos(x, o, c, nmax, M)] = x * C + (long long)shard_a(o, world, rank) * M + c;
+    } else {
+        for (int x = 0; x < NMAT4; ++x)
+            for (int a = 0; a <= t; ++a) {
+                int ro, o;
+                xch_src(a, world, ro, o);
+                for (int c = 0; c < M; ++c)
+                    out[x * C + (long long)a * M + c] = ro == rank ? -1 : ro * slice + xch_pos(x, o, c, nmax, M);
+            }
+    }
+    return cnt;
+}
+
 extern "C" int ccj_comm_unique_id(char *id_out) {
     if (!id_out) return CCJ_E_ARG;
     ncclUniqueId id;
@@ -2892,13 +2832,21 @@ extern "C" const char *ccj_last_error(const ccj_ctx *c) { return c ? c->err.c_st
 
 extern "C" void ccj_destroy(ccj_ctx *c) {
     if (!c) return;
+    bool leak_send = false;
     if (c->lgroup) {  // leave the in-process group: no member may copy from this context's buffers
         ccj_group *g = c->lgroup;
         std::unique_lock<std::mutex> lk(g->mu);
-        if (g->members[c->rank] == c) g->members[c->rank] = nullptr;
-        g->broken = true;  // the exchange cannot complete without this rank
-        g->cv.notify_all();
-        g->cv.wait(lk, [&] { return g->busy == 0; });  // peers still copying from d_send
+        if (g->members[c->rank] == c) {  // registered (a failed ccj_comm_init_local never was)
+            g->members[c->rank] = nullptr;
+            g->broken = true;  // the exchange cannot complete without this rank
+            g->cv.notify_all();
+        }
+        // peers still copying from d_send; bounded like the group's barriers (a peer stuck in a
+        // GPU call must not hang this destroy): on timeout d_send is leaked instead of freed
+        if (!g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return g->busy == 0; })) {
+            fprintf(stderr, "ccj_destroy: a group member is still copying after 120 s; leaking its source buffer\n");
+            leak_send = true;
+        }
         c->lgroup = nullptr;
     }
     hipSetDevice(c->device);
@@ -2937,10 +2885,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_ilm);
     hipFree(c->d_dummy);
     hipFree(c->d_items);
-    hipFree(c->d_tiles);
-    hipFree(c->d_pb);
-    hipFree(c->d_ied);
-    hipFree(c->d_send);
+    if (!leak_send) hipFree(c->d_send);
     hipFree(c->d_recv);
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->h_ioff) hipHostFree(c->h_ioff);

@@ -1070,419 +1070,6 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
 }
 
 // ------------------------------------------------------------------------------------------
-// Interior loops as tiles (k_iltile).  The same minima as k_iloop (get_PLiloop /
-// get_PRiloop / get_PMiloop, pseudo_loop.cc:682-773, source-level distances dt = 3..58; dt = 2 is
-// k_level4d's), organised so that a partner value is fetched once per tile and dt instead of once
-// per closing pair that reads it.  A tile is TL_NK consecutive keys of one role and block times 64
-// cells, one cell per lane:
-//   PL: block a, keys K = i (pair (i, i+a)),           cell h = X0 + lane - kk   (skewed)
-//   PR: block a, keys K = q (pair (k, l), k = q+a+3),  cell i = X0 + lane
-//   PM: row h,   keys K = j (pair (j, j+h+2)),         cell a = X0 + lane + kk   (skewed)
-// For one dt the candidate (key kk, window position j) reads source row r = kk + j of that dt's
-// copy (PL: column i+1+u1, PR: row q+1+u1, PM: row d = j-1-u1; PM numbers j from u1 = u1max
-// down), and with the skew every key reads the SAME 64 elements of a row (PL: h' = X0+lane+dt-1-
-// u1min-r, PR: i-1, PM: a-1-u1 = X0+lane-1-u1max+r).  So a wave stages, per dt, the <= TL_ROWS
-// rows its keys read into LDS with 16-byte loads (only rows whose pair can pair: the reference's
-// can_pair(d, dp) is a property of the row), together with the keys' energies e(kk, dt, j)
-// (T.ied: int32, TL_BIG where the candidate does not exist: the inner pair cannot pair or j is past
-// the window), and then walks acc[kk] = min_j row[kk+j][lane] + e(kk, dt, j): one LDS read, an add
-// and a min per candidate and 64 cells, with no per-candidate bookkeeping.  Rows not staged hold
-// stale int16 values, and their energies are TL_BIG, so they never win.  The TL_W waves of a tile
-// take dt = 3+w, 3+w+TL_W, ... (each stages and walks its own dts, the next dt's loads in flight
-// during the walk) and meet in LDS at the end.  PM's per-cell window (d > i, dp < l, i.e. u1 <=
-// a-2, u2 <= b-2) is a lane mask over rows.  Min is order-independent: bit-identical minima.
-// ------------------------------------------------------------------------------------------
-#ifndef CCJ_TLW
-#define CCJ_TLW 4
-#endif
-constexpr int TL_W = CCJ_TLW;                           // waves per tile
-constexpr int TL_ROWS = TL_NK + IE_U - 1;               // 44 source rows per dt at most
-constexpr int TL_DT0 = 3, TL_DT1 = 2 * (IE_U - 1) + 2;  // dt = 3 .. 58
-constexpr int TL_DTN = TL_DT1 - TL_DT0 + 1;             // 56
-constexpr int TL_EJ = 32;                               // energies per (key, dt); j = 0..28 used
-constexpr int TL_KEYW = TL_DTN * TL_EJ;                 // int32 per key in T.ied
-constexpr int TL_BIG = 1 << 20;
-constexpr int TL_OFF_E = TL_ROWS * 128;                 // per wave: rows [44][64] int16, then
-constexpr int TL_OFF_A = TL_OFF_E + TL_NK * 128;        //   energies [16][32] int32, acc [16][64] int16
-constexpr int TL_WB = TL_OFF_A + TL_NK * 128;           // 9728 bytes per wave
-constexpr int TL_LDS = TL_W * TL_WB;
-constexpr int TL_NLR = (TL_ROWS * 8 + 63) / 64;          // 6 row loads per dt (8 x 16 B per row)
-constexpr int TL_NLE = TL_NK * 8 / 64;                   // 2 energy loads per dt (8 x 16 B per key)
-constexpr int TL_PAD = 128;                              // slack (elements) in front of the copies
-
-// bits r in [lo, hi] (lo, hi in [0, 63]; empty when lo > hi)
-__device__ __forceinline__ unsigned long long bit_range(int lo, int hi) {
-    if (lo > hi) return 0ull;
-    const unsigned long long up = hi >= 63 ? ~0ull : ((2ull << hi) - 1ull);
-    return up & ~((1ull << lo) - 1ull);
-}
-// pairability bits (T.pb: per span w a bit row over positions p, bit p = pair (p, p+w) can pair):
-// bit r of the result = pair (p0+r, p0+r+w) can pair; 0 outside the table.  Scalar loads.
-__device__ __forceinline__ unsigned long long pbits(const DevTables &T, int w, int p0) {
-    if (w < 0 || w > T.n || p0 > T.n + 1 || p0 <= -64) return 0ull;
-    typedef const __attribute__((address_space(4))) unsigned long long cu64;
-    cu64 *row = (cu64 *)(unsigned long long)(T.pb + (size_t)w * T.pbw);
-    if (p0 < 0) return row[0] << (-p0);
-    const int wi = p0 >> 6, sh = p0 & 63;
-    unsigned long long x = row[wi] >> sh;
-    if (sh) x |= row[wi + 1] << (64 - sh);
-    return x;
-}
-
-typedef unsigned tl_u32x4 __attribute__((ext_vector_type(4)));
-typedef int tl_i32x4 __attribute__((ext_vector_type(4)));
-
-// One dt of a wave's walk (scalar): the rows to stage and where they come from.
-struct TlDt {
-    unsigned long long mask;  // rows r staged (pair can pair, inside the copy, read by a live key)
-    int nrows, cnt, u1max;
-    long long rbase;          // element index of (row 0, lane 0) minus the row's own offset (below)
-    long long ebase;          // element index in T.ied of key 0's energies for this dt
-    int Rlo, mp, tp1;         // row-offset parameters
-};
-
-// pairability bits as above, per lane (vector loads)
-__device__ __forceinline__ unsigned long long pbits_v(const DevTables &T, int w, int p0) {
-    if (w < 0 || w > T.n || p0 > T.n + 1 || p0 <= -64) return 0ull;
-    const unsigned long long *row = T.pb + (size_t)w * T.pbw;
-    if (p0 < 0) return row[0] << (-p0);
-    const int wi = p0 >> 6, sh = p0 & 63;
-    unsigned long long x = row[wi] >> sh;
-    if (sh) x |= row[wi + 1] << (64 - sh);
-    return x;
-}
-
-// The dts of a wave, one per lane: lane z describes dt = TL_DT0 + wv + TL_W*z.  Computed once per
-// tile with vector loads (one memory round trip for all of them, instead of scalar loads in front
-// of every dt's row loads); tl_dt_pick reads the z-th one out with readlanes.
-template <int role>
-__device__ __forceinline__ TlDt tl_dt_setup(const DevTables &T, int t, int dt, int a, int b, int g, int K0, int X0,
-                                            unsigned keymask) {
-    TlDt d;
-    const int n = T.n, rs = T.rs, m = n - t - 2, tp = t - dt;
-    const int u1min = imax(0, dt - 2 - (IE_U - 1)), u1max = imin(IE_U - 1, dt - 2), cnt = u1max - u1min + 1;
-    d.nrows = TL_NK + cnt - 1;
-    d.cnt = cnt;
-    d.u1max = u1max;
-    d.mp = m + dt;
-    d.tp1 = tp + 1;
-    // rows read by a live key: keymask spread over cnt consecutive bits
-    unsigned long long used = keymask;
-    for (int len = 1; len < cnt;) {
-        const int st = imin(len, cnt - len);
-        used |= used << st;
-        len += st;
-    }
-    const long long lbx = T.ldx[tp].lbx;
-    int w, p0, rlo, rhi;
-    if (role == 0) {
-        const int Mp = T.ld[tp].M;
-        d.Rlo = K0 + 1 + u1min;  // column c = Rlo + r
-        w = a - dt; p0 = d.Rlo; rlo = 1 - d.Rlo; rhi = d.mp - d.Rlo;
-        d.rbase = lbx + (long long)(a - dt) * Mp + (X0 + dt - 1 - u1min) - TL_PAD;
-        d.ebase = (((long long)0 * (n + 1) + a) * rs + K0) * TL_KEYW;
-    } else if (role == 1) {
-        const int Mp = T.ld[tp].M, Cp = T.ld[tp].C;
-        d.Rlo = K0 + 1 + u1min;  // PRx row q' = Rlo + r
-        w = b - dt; p0 = d.Rlo + a + 3; rlo = -d.Rlo; rhi = d.mp - 1 - d.Rlo;
-        d.rbase = lbx + Cp + (long long)a * Mp + (X0 - 1);
-        d.ebase = (((long long)0 * (n + 1) + b) * rs + K0 + a + 3) * TL_KEYW;
-    } else {
-        const long long pmb = T.ldx[tp].pmb;
-        d.Rlo = K0 - 1 - u1max;  // PMx row d = Rlo + r (at h' = h + dt)
-        w = g + dt; p0 = d.Rlo; rlo = 1 - d.Rlo; rhi = n - g - dt - d.Rlo;
-        d.rbase = pmb + (long long)(g - 2 + dt) * n * (tp + 1) + (X0 - 1 - u1max) - TL_PAD;
-        d.ebase = (((long long)1 * (n + 1) + g) * rs + K0) * TL_KEYW;
-    }
-    d.ebase += (long long)(dt - TL_DT0) * TL_EJ;
-    d.mask = used & pbits_v(T, w, p0) & bit_range(imax(rlo, 0), imin(rhi, d.nrows - 1));
-    return d;
-}
-
-__device__ __forceinline__ TlDt tl_dt_pick(const TlDt &v, int z) {
-    TlDt d;
-    d.mask = rdl64(v.mask, z);
-    d.rbase = (long long)rdl64((unsigned long long)v.rbase, z);
-    d.ebase = (long long)rdl64((unsigned long long)v.ebase, z);
-    d.nrows = __builtin_amdgcn_readlane(v.nrows, z);
-    d.cnt = __builtin_amdgcn_readlane(v.cnt, z);
-    d.u1max = __builtin_amdgcn_readlane(v.u1max, z);
-    d.Rlo = __builtin_amdgcn_readlane(v.Rlo, z);
-    d.mp = __builtin_amdgcn_readlane(v.mp, z);
-    d.tp1 = __builtin_amdgcn_readlane(v.tp1, z);
-    return d;
-}
-
-// element offset of row r (lane 0, chunk 0) relative to d.rbase (>= 0 for every staged row)
-template <int role>
-__device__ __forceinline__ int tl_row_off(const TlDt &d, int r) {
-    if (role == 0) {
-        const int c1 = d.Rlo + r - 1;  // column c - 1
-        return c1 * d.mp - ((c1 * (c1 - 1)) >> 1) - r + TL_PAD;
-    } else if (role == 1) {
-        const int q = d.Rlo + r;
-        return (q * (q + 1)) >> 1;
-    } else {
-        return (d.Rlo + r - 1) * d.tp1 + r + TL_PAD;
-    }
-}
-
-// issue the 16-byte loads of one dt: rows (TL_NLR loads, 8 lanes per row) and energies (TL_NLE
-// loads, 8 lanes per key); lanes of rows / keys not staged load nothing.  (Buffer loads with
-// out-of-range offsets for those lanes, so that every load is issued and two dts can be in flight
-// with exact waits, measured slower in the fill: 42.1 vs 39.1 ms, the same 111 us per launch.)
-template <int role>
-__device__ __forceinline__ void tl_issue_e(const DevTables &T, const TlDt &d, unsigned keymask, int lane, uint4 *E);
-// so[s]: the LDS byte offset the lane's chunk goes to (staged row r -> slot popcount(mask below r),
-// the compacted order the energies of T.ied follow), -1 when the row is not staged
-template <int role>
-__device__ __forceinline__ void tl_issue(const DevTables &T, const TlDt &d, unsigned keymask, int lane, uint4 *R, uint4 *E,
-                                         int *so) {
-    tl_issue_e<role>(T, d, keymask, lane, E);
-    const char *cb = (const char *)((role == 2 ? T.pmx : T.d4x) + d.rbase);
-#pragma unroll
-    for (int s = 0; s < TL_NLR; ++s) {
-        const int idx = s * 64 + lane, r = idx >> 3, ch = idx & 7;
-        const bool on = r < d.nrows && ((d.mask >> r) & 1ull);
-        so[s] = on ? __popcll(d.mask & ((1ull << r) - 1ull)) * 128 + ch * 16 : -1;
-        if (on) {
-            const unsigned off = 2u * (unsigned)(tl_row_off<role>(d, r) + 8 * ch);
-            const tl_u32x4 v = *(const __attribute__((address_space(1))) tl_u32x4 *)(cb + off);
-            R[s] = make_uint4(v.x, v.y, v.z, v.w);
-        }
-    }
-}
-
-template <int role>
-__device__ __forceinline__ void tl_issue_e(const DevTables &T, const TlDt &d, unsigned keymask, int lane, uint4 *E) {
-    const char *eb = (const char *)(T.ied + d.ebase);
-#pragma unroll
-    for (int s = 0; s < TL_NLE; ++s) {
-        const int idx = s * 64 + lane, kk = idx >> 3, ch = idx & 7;
-        if ((keymask >> kk) & 1u) {
-            const unsigned off = (unsigned)(kk * TL_KEYW * 4 + ch * 16);
-            const tl_u32x4 v = *(const __attribute__((address_space(1))) tl_u32x4 *)(eb + off);
-            E[s] = make_uint4(v.x, v.y, v.z, v.w);
-        }
-    }
-}
-
-// the walk of key kk over one dt: acc = min over the key's candidates of staged row + energy.  The
-// key's candidate rows kk..kk+cnt-1 that can pair are the consecutive LDS slots P .. P+nk-1
-// (compacted staging), and T.ied holds its energies in the same compacted order (TL_BIG past nk),
-// so the walk is 4 slots per step with affine addresses.  (Two keys per step, or 8 slots per step,
-// measured slower: DESIGN.md §4.)
-template <bool PMMASK>
-__device__ __forceinline__ int tl_walk_key(const char *wl, int kk, int P, int nk, int acc, int lane, int SPlo, unsigned SPn) {
-#pragma unroll
-    for (int gp = 0; gp < TL_EJ / 4; ++gp) {
-        if (4 * gp >= nk) break;
-        const tl_i32x4 e = *(const tl_i32x4 *)(wl + TL_OFF_E + kk * 128 + 16 * gp);
-        const char *rb = wl + (P + 4 * gp) * 128 + lane * 2;
-        int x[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = (int)*(const int16_t *)(rb + u * 128);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            int c = x[u] + e[u];
-            if (PMMASK) c = ((unsigned)(P + 4 * gp + u - SPlo) < SPn) ? c : TL_BIG;
-            acc = imin(acc, c);
-        }
-    }
-    return acc;
-}
-
-// every live key of one dt (accumulators in LDS, clamped like a store: the clamp commutes with
-// min).  mask: the staged rows; a key's slots start at popcount(mask below kk).
-template <bool PMMASK>
-__device__ __forceinline__ void tl_walk(char *wl, unsigned km, int lane, unsigned long long mask, int cnt, int SPlo,
-                                        unsigned SPn) {
-    const unsigned long long win = (1ull << cnt) - 1ull;
-#pragma unroll 1
-    while (km) {
-        const int kk = __builtin_ctz(km);
-        km &= km - 1u;
-        const int nk = __popcll(mask & (win << kk));
-        if (nk == 0) continue;
-        int16_t *ap = (int16_t *)(wl + TL_OFF_A + kk * 128 + lane * 2);
-        *ap = (int16_t)clamp_store(tl_walk_key<PMMASK>(wl, kk, __popcll(mask & ((1ull << kk) - 1ull)), nk, (int)*ap, lane, SPlo, SPn));
-    }
-}
-
-template <int role>
-__device__ __forceinline__ void iltile_body(const DevTables &T, int t, uint32_t tw, int G_SH, int rank, char *smem) {
-    const int n = T.n, m = n - t - 2;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int blk = (int)((tw >> 20) & 1023u), K0 = (int)((tw >> 10) & 1023u), xc = (int)(tw & 1023u);
-    int a = 0, b = 0, g = 0, X0, dtmax;
-    if (role == 0) {
-        a = blk; b = t - a; X0 = xc * 64; dtmax = imin(TL_DT1, a - 4);
-    } else if (role == 1) {
-        a = blk; b = t - a; X0 = 1 + xc * 64; dtmax = imin(TL_DT1, b - 4);
-    } else {
-        g = blk + 2;
-        int x0, xn;
-        pm_tile_span(n, t, g, K0, x0, xn);
-        X0 = x0 + xc * 64; dtmax = imin(TL_DT1, t - 2);
-    }
-    // ---- keys (lanes 0..15, the same in every wave): the pair can pair and owns a cell in this tile
-    unsigned keymask;
-    {
-        const int kk = lane, K = K0 + kk;
-        bool ok = false;
-        if (kk < TL_NK) {
-            if (role == 0) ok = K >= 1 && K <= m;
-            else if (role == 1) ok = K <= m - 1 && X0 <= K + 1;
-            else {
-                const int k = K + g;
-                if (K >= 1 && k <= n) {
-                    const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, K - 1);
-                    ok = alo <= ahi && X0 + kk <= ahi && X0 + kk + 63 >= alo;
-                }
-            }
-        }
-        const unsigned long long kp = role == 0 ? pbits(T, a, K0) : role == 1 ? pbits(T, b, K0 + a + 3) : pbits(T, g, K0);
-        keymask = (unsigned)(__ballot(ok) & kp) & ((1u << TL_NK) - 1u);
-        keymask = (unsigned)__builtin_amdgcn_readfirstlane((int)keymask);
-    }
-    if (keymask == 0) return;  // the whole workgroup (uniform)
-    char *wl = smem + wv * TL_WB;
-    // accumulators: 32767 (the clamp of "no candidate")
-    {
-        uint4 *ap = (uint4 *)(wl + TL_OFF_A) + lane * 2;
-        const unsigned inf2 = ((unsigned)INTERN_INF << 16) | (unsigned)INTERN_INF;
-        ap[0] = make_uint4(inf2, inf2, inf2, inf2);
-        ap[1] = make_uint4(inf2, inf2, inf2, inf2);
-    }
-    const int nz = dtmax >= TL_DT0 + wv ? (dtmax - TL_DT0 - wv) / TL_W + 1 : 0;  // this wave's dts
-    if (nz > 0) {
-        const TlDt dv = tl_dt_setup<role>(T, t, imin(TL_DT0 + wv + TL_W * lane, dtmax), a, b, g, K0, X0, keymask);
-        uint4 R[TL_NLR], E[TL_NLE];
-        int so[TL_NLR];
-#pragma unroll
-        for (int s = 0; s < TL_NLR; ++s) R[s] = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-        for (int s = 0; s < TL_NLE; ++s) E[s] = make_uint4(0u, 0u, 0u, 0u);
-        tl_issue<role>(T, tl_dt_pick(dv, 0), keymask, lane, R, E, so);
-#pragma unroll 1
-        for (int z = 0; z < nz; ++z) {
-            // the pending dt's rows and energies into LDS (every slot: rows not staged keep stale
-            // values), the next dt's loads into the freed registers, then the walk
-#pragma unroll
-            for (int s = 0; s < TL_NLR; ++s)
-                if (so[s] >= 0) *(uint4 *)(wl + so[s]) = R[s];
-#pragma unroll
-            for (int s = 0; s < TL_NLE; ++s) *(uint4 *)(wl + TL_OFF_E + (s * 64 + lane) * 16) = E[s];
-            const TlDt d = tl_dt_pick(dv, z);
-            const int dt = TL_DT0 + wv + TL_W * z;
-            if (z + 1 < nz) tl_issue<role>(T, tl_dt_pick(dv, z + 1), keymask, lane, R, E, so);
-            // PM's window as a row mask per lane: row r is a candidate of cell a = X0+lane+kk iff
-            // u1 = kk+u1max-r in [a-t+dt, a-2]  <=>  r in [BL, BL + t-dt-2], BL = u1max+2-X0-lane; in
-            // slots: [SPlo, SPlo + SPn)
-            const bool pmmask = role == 2 && !(d.u1max + 2 - X0 <= 0 && d.u1max + 2 - X0 - 63 + (t - dt - 2) >= d.nrows - 1);
-            if (pmmask) {
-                auto below = [&](int x) {  // staged rows below row x (branch-free)
-                    const unsigned xc = (unsigned)imin(imax(x, 0), 64);
-                    const unsigned long long lm = ((1ull << (xc & 63u)) - 1ull) | ((xc >> 6) ? ~0ull : 0ull);
-                    return __popcll(d.mask & lm);
-                };
-                const int BL = d.u1max + 2 - X0 - lane, BH = BL + (t - dt - 2) + 1;
-                const int SPlo = below(BL);
-                tl_walk<true>(wl, keymask, lane, d.mask, d.cnt, SPlo, (unsigned)(below(BH) - SPlo));
-            } else {
-                tl_walk<false>(wl, keymask, lane, d.mask, d.cnt, 0, 0u);
-            }
-        }
-    }
-    __syncthreads();
-    // ---- results: wave wv finishes keys kk = wv, wv+TL_W, ... (min over the waves' accumulators)
-    const LvlDev Lt = T.ld[t];
-    for (int kk = wv; kk < TL_NK; kk += TL_W) {
-        if (!((keymask >> kk) & 1u)) continue;
-        int v = INTERN_INF;
-#pragma unroll
-        for (int w2 = 0; w2 < TL_W; ++w2) v = imin(v, (int)*(const int16_t *)(smem + w2 * TL_WB + TL_OFF_A + kk * 128 + lane * 2));
-        const int K = K0 + kk;
-        if (role == 0) {
-            const int h = X0 + lane - kk;
-            if (h >= 0 && h <= m - K)
-                T.d4[Lt.lb + (long long)PL * Lt.C + (long long)a * Lt.M + h * m - ((h * (h - 1)) >> 1) + K - 1] = (int16_t)v;
-        } else if (role == 1) {
-            const int i = X0 + lane, h = K + 1 - i;
-            if (i <= K + 1) T.d4[Lt.lb + (long long)PR * Lt.C + (long long)a * Lt.M + h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)v;
-        } else {
-            const int k = K + g, h = g - 2, aa = X0 + lane + kk;
-            const int alo = imax(2, t - (n - k)), ahi = imin(t - 2, K - 1);
-            if (aa >= alo && aa <= ahi && shard_owner(aa, G_SH) == rank)
-                T.d4[Lt.lb + (long long)PM * Lt.C + (long long)aa * Lt.M + h * m - ((h * (h - 1)) >> 1) + K - aa - 1] = (int16_t)v;
-        }
-    }
-}
-
-__global__ __launch_bounds__(64 * TL_W) void k_iltile(DevTables T, int t, long long first, int G_SH, int rank) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    // tiles in the host's order (longest first, build_tiles), dealt round-robin over the XCDs
-    const uint32_t tw = ld_const(T.tiles + first + blockIdx.x);
-    const int role = (int)(tw >> 30);
-    if (role == 0) iltile_body<0>(T, t, tw, G_SH, rank, smem);
-    else if (role == 1) iltile_body<1>(T, t, tw, G_SH, rank, smem);
-    else iltile_body<2>(T, t, tw, G_SH, rank, smem);
-}
-
-// Per-(key, dt) energy rows for k_iltile (from T.ie, once per fill): T.ied[type][w][p][dt-3][.], int32,
-// for the keys whose pair (p, p+w) can pair, the candidates that exist in window order (the same
-// order as k_iltile's compacted row slots), then TL_BIG.  Window position j:
-//   type 0, the pair closes the loop (PL, PR): j-th window position u1 = u1min + j;
-//   type 1, the pair is the loop's inner pair (PM): u1 = u1max - j, outer pair (p-1-u1, p+w+1+u2);
-// e = lrint(e_intP * E_IntLoop) (pseudo_loop.cc:836-840), TL_BIG where the reference skips the
-// candidate (the other pair cannot pair: T.ie holds 32767) or j is past the window.
-__global__ __launch_bounds__(256) void k_ie_tiles(DevTables T) {
-    __shared__ int buf[TL_NK][8 * TL_EJ + 1];
-    const int n = T.n, rs = T.rs;
-    const int p0 = (int)blockIdx.x * TL_NK, w = (int)blockIdx.y, type = (int)blockIdx.z;
-    for (int dc = 0; dc < TL_DTN / 8; ++dc) {
-        for (int idx = threadIdx.x; idx < TL_NK * 8 * TL_EJ; idx += 256) {
-            const int kk = idx & (TL_NK - 1), e = idx >> 4;
-            const int dt = TL_DT0 + dc * 8 + (e >> 5), j = e & (TL_EJ - 1);
-            const int p = p0 + kk;
-            const int u1min = imax(0, dt - 2 - (IE_U - 1)), u1max = imin(IE_U - 1, dt - 2), cnt = u1max - u1min + 1;
-            int v = TL_BIG;
-            if (j < cnt && p >= 1 && p + w <= n) {
-                int u1, ws, ps;
-                if (type == 0) { u1 = u1min + j; ws = w; ps = p; }
-                else { u1 = u1max - j; ws = w + dt; ps = p - 1 - u1; }
-                const int u2 = dt - 2 - u1;
-                if (ps >= 1 && ps + ws <= n) {
-                    const int x = T.ie[((size_t)(u1 * IE_U + u2) * (n + 1) + ws) * rs + ps];
-                    v = x >= INTERN_INF ? TL_BIG : x;
-                }
-            }
-            buf[kk][e] = v;
-        }
-        __syncthreads();
-        // each (key, dt) row in compacted order: the candidates that exist, in window order, then TL_BIG
-        if (threadIdx.x < TL_NK * 8) {
-            int *row = &buf[threadIdx.x >> 3][(threadIdx.x & 7) * TL_EJ];
-            int q = 0;
-            for (int j = 0; j < TL_EJ; ++j) {
-                const int v = row[j];
-                if (v != TL_BIG) row[q++] = v;
-            }
-            for (; q < TL_EJ; ++q) row[q] = TL_BIG;
-        }
-        __syncthreads();
-        for (int idx = threadIdx.x; idx < TL_NK * 8 * TL_EJ; idx += 256) {
-            const int kk = idx >> 8, e = idx & 255;
-            const int p = p0 + kk;
-            if (p >= 1 && p + w <= n && T.pt[(size_t)w * rs + p] > 0)
-                T.ied[(((size_t)type * (n + 1) + w) * rs + p) * TL_KEYW + dc * 8 * TL_EJ + e] = buf[kk][e];
-        }
-        __syncthreads();
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // AoS loop records (ccj_engine.h RecType): pack / unpack int16 pairs
 __device__ __forceinline__ unsigned pk16(int lo, int hi) { return (unsigned)(uint16_t)lo | ((unsigned)(uint16_t)hi << 16); }
 __device__ __forceinline__ int lo16(unsigned w) { return (int)(int16_t)(w & 0xffffu); }
@@ -2303,7 +1890,7 @@ extern "C" int ccjk_diag2d(const DevTables *T, int sigma, int G, int rank, void 
 // The 2-D values of span sigma that k_diag2d writes, for the band-sharded exchange: DT_N int32 planes
 // of n+1 entries (V, Vt, P, WBP, WB, WPP, WP, WMv, WMp, WM) in the tail of the level-sigma slice.
 // Pack: this rank's intervals.  Unpack: every other rank's intervals (owner (i-1) % G), plus WBW.
-constexpr int DT_N = 10;
+constexpr int DT_N = XCH_DT_N;
 __global__ __launch_bounds__(256) void k_dtail_pack(DevTables T, int sigma, int G, int rank, int *tail) {
     const int i = 1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
     const int n = T.n;
@@ -2390,30 +1977,13 @@ extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int n
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_ie_tiles(const DevTables *T, void *stream) {
-    const int n = T->n;
-    if (n < 1) return 0;
-    hipLaunchKernelGGL(k_ie_tiles, dim3((unsigned)((T->rs + TL_NK - 1) / TL_NK), (unsigned)(n + 1), 2u), dim3(256), 0,
-                       (hipStream_t)stream, *T);
-    return (int)hipGetLastError();
-}
-
-extern "C" int ccjk_iltile(const DevTables *T, int t, long long first_tile, int ntiles, int G, int rank, void *stream) {
-#ifdef CCJ_ABLATE_ILOOP
-    return 0;
-#endif
-    if (ntiles <= 0) return 0;
-    hipLaunchKernelGGL(k_iltile, dim3((unsigned)ntiles), dim3(64 * TL_W), TL_LDS, (hipStream_t)stream, *T, t, first_tile, G, rank);
-    return (int)hipGetLastError();
-}
-
 // ------------------------------------------------------------------------------------------
 // Band-sharded exchange of level t.  k_pack: rank r's own cells, all 22 matrices,
 // into one contiguous slice [x][own index][M] of nmax blocks per matrix (nmax = the largest rank's
 // block count at t), so the exchange is ONE all-gather of equal slices.  k_unpack: every cell of the
 // other ranks' blocks from the gathered slices (rank r's at recv + r * rstride) back into the level layout, plus its loop records and
-// interior-loop copies (what k_level4d writes for its own cells).  recv == nullptr: the cells are
-// already in the level layout and only their records and copies are rebuilt.
+// interior-loop copies (what k_level4d writes for its own cells).  The slices carry all 22 matrices,
+// the record-only five included (exchange fills keep T.mat5 = 1), so the records are rebuilt from them.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_pack(DevTables T, int t, int G, int r, int nmax, int16_t *send) {
     const int n = T.n, m = n - t - 2, Mt = (m * (m + 1)) >> 1;
@@ -2424,7 +1994,7 @@ __global__ __launch_bounds__(256) void k_pack(DevTables T, int t, int G, int r, 
     const LvlDev Lt = T.ld[t];
     const int16_t *src = T.d4 + Lt.lb + (long long)shard_a(o, G, r) * Mt + c;
 #pragma unroll 2
-    for (int x = 0; x < NMAT4; ++x) send[((long long)x * nmax + o) * Mt + c] = src[(long long)x * Lt.C];
+    for (int x = 0; x < NMAT4; ++x) send[xch_pos(x, o, c, nmax, Mt)] = src[(long long)x * Lt.C];
 }
 
 __global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r, int nmax, const int16_t *recv, size_t rstride) {
@@ -2432,7 +2002,8 @@ __global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r
     const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const int a = (int)(gc / Mt);
     if (a > t) return;
-    const int ro = shard_owner(a, G);
+    int ro, o;
+    xch_src(a, G, ro, o);
     if (ro == r) return;  // own cell: k_level4d wrote it with its records and copies
     const int c = (int)(gc - (long long)a * Mt);
     const float tm = 2.0f * m + 1.0f;
@@ -2448,17 +2019,11 @@ __global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r
     int16_t *dst = T.d4 + Lt.lb + (long long)a * Mt + c;
     const long long C = Lt.C;
     int v[NMAT4];
-    if (recv) {
-        const int o = shard_count(a - 1, G, ro);  // a's own index on its rank
-        const int16_t *sl = recv + (size_t)ro * rstride + (long long)o * Mt + c;
+    const int16_t *sl = recv + (size_t)ro * rstride;
 #pragma unroll
-        for (int x = 0; x < NMAT4; ++x) {
-            v[x] = sl[(long long)x * nmax * Mt];
-            dst[x * C] = (int16_t)v[x];
-        }
-    } else {
-#pragma unroll
-        for (int x = 0; x < NMAT4; ++x) v[x] = dst[x * C];
+    for (int x = 0; x < NMAT4; ++x) {
+        v[x] = sl[xch_pos(x, o, c, nmax, Mt)];
+        dst[x * C] = (int16_t)v[x];
     }
     write_records(T, Lt.lr, Lt.C, (unsigned)(a * Mt + c), v[PLmloop00], v[PMmloop00], v[POmloop00], v[PfromL], v[PfromO],
                   v[PLmloop10], v[PfromMprime], v[PK], v[PRmloop00], v[PfromR], imin(v[PL], v[PR]), v[PMmloop10],
@@ -2522,6 +2087,9 @@ extern "C" int ccjk_unpack(const DevTables *T, int t, int G, int r, int nmax, co
                            void *stream) {
     const int m = T->n - t - 2;
     if (m <= 0) return 0;
+    // the records of the other ranks' cells are rebuilt from the slices, which must carry all 22
+    // matrices: without T.mat5 the five record-only matrices are not in d4 (k_pack would ship stale ones)
+    if (!recv || !T->mat5) return (int)hipErrorInvalidValue;
     const long long cells = (long long)(t + 1) * (m * (m + 1) / 2);
     hipLaunchKernelGGL(k_unpack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, G, r, nmax, recv,
                        rstride);

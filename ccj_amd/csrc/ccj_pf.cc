@@ -216,6 +216,30 @@ struct ccj_pf_ctx {
     int ptype(int i, int j) const { return pair[S[i]][S[j]]; }
 };
 
+// The allocations of ccj_pf_create for a sequence of length n, in bytes: device (every hipMalloc
+// of create_impl; the work items, sequence-dependent, are bounded by one 64-lane chunk per PL/PR/PM
+// row) and host (the two get_e_intP window tables, built before they are uploaded).
+extern "C" void ccj_pf_footprint(int n, unsigned long long *device_bytes, unsigned long long *host_bytes) {
+    if (n < 1) n = 1;
+    const unsigned long long rs = (unsigned long long)n + 2, plane = (unsigned long long)(n + 1) * rs;
+    const unsigned long long ie = 2ull * PF_IEW * PF_IEW * plane * sizeof(double);  // ieO + ieI
+    unsigned long long d4 = 0, cx = 0, pmx = 0, maxC = 1, rows = 0;
+    for (int t = 0; t <= n - 3; ++t) {
+        const unsigned long long m = (unsigned long long)(n - t - 2), C = (unsigned long long)(t + 1) * (m * (m + 1) / 2);
+        d4 += (unsigned long long)PF_NMAT4 * C;
+        cx += 2 * C;
+        pmx += m * (unsigned long long)n * (t + 1);
+        maxC = std::max(maxC, C);
+        rows += (unsigned long long)(t + 1) * m * 3 + m * (unsigned long long)n;  // item bound (rows x chunks)
+    }
+    unsigned long long dev = ie + (d4 + cx + pmx) * sizeof(int) + 2ull * 3 * maxC * sizeof(double);
+    dev += (unsigned long long)CCJ_PF_NMAT2 * plane * sizeof(double) + 2 * plane * sizeof(long long);  // 2-D, Pacc, Pabs
+    dev += 3 * plane * sizeof(double) + plane + 2ull * plane * PF_IEW * sizeof(uint32_t);             // hp, est, cp; pt; mO, mI
+    dev += rows * sizeof(uint32_t) + sizeof(PfExp) + (1u << 20);                                      // items; small tables
+    if (device_bytes) *device_bytes = dev;
+    if (host_bytes) *host_bytes = ie;
+}
+
 namespace {
 
 int pf_err(ccj_pf_ctx *c, int code, const char *what, hipError_t e = hipSuccess) {
@@ -437,21 +461,30 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     c->rs = n + 2;
     const int rs = c->rs;
     {
-        // Size check before any table is built: the two get_e_intP window tables (host, then
-        // device) and the int32 4-D store (21 x C(n+1,4) cells).  Past what the host or the GPU can
-        // hold, fail with CCJ_E_OOM up front instead of after seconds of table building.
-        const double plane_b = (double)(n + 1) * rs, cells = (double)(n + 1) * n * (n - 1) * (n - 2) / 24.0;
-        const double ie_b = 2.0 * PF_IEW * PF_IEW * plane_b * sizeof(double);
-        const double dev_b = ie_b + 21.0 * cells * sizeof(int) * 1.5;  // + copies, slack
-        const double host_b = ie_b;
+        // Size check before any table is built (ccj_pf_footprint: the allocations below, summed).
+        // Past what the host or the GPU can hold, fail with CCJ_E_OOM up front instead of after
+        // seconds of table building.  CCJ_PF_DEVMEM_LIMIT (bytes) stands in for the device's free
+        // memory (tests pin the accept/reject boundary with it).
+        unsigned long long dev_b = 0, host_b = 0;
+        ccj_pf_footprint(n, &dev_b, &host_b);
         size_t dfree = 0, dtotal = 0;
         char msg[200];
-        if (hipSetDevice(device) == hipSuccess && hipMemGetInfo(&dfree, &dtotal) == hipSuccess && dev_b > (double)dfree) {
+        const char *lim = getenv("CCJ_PF_DEVMEM_LIMIT");
+        if (lim && *lim) dfree = (size_t)strtoull(lim, nullptr, 10);
+        else if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&dfree, &dtotal) != hipSuccess) dfree = SIZE_MAX;
+        if ((double)dev_b > (double)dfree) {
             snprintf(msg, sizeof msg, "n=%d needs ~%.1f GB of device memory, %.1f GB free", n, dev_b / 1e9, dfree / 1e9);
             return pf_err(c, CCJ_E_OOM, msg);
         }
-        const long pages = sysconf(_SC_AVPHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
-        if (pages > 0 && psz > 0 && host_b > (double)pages * (double)psz) {
+        // MemAvailable counts reclaimable page cache (sysconf(_SC_AVPHYS_PAGES) does not)
+        unsigned long long avail_kb = 0;
+        if (FILE *f = fopen("/proc/meminfo", "r")) {
+            char line[256];
+            while (fgets(line, sizeof line, f))
+                if (sscanf(line, "MemAvailable: %llu kB", &avail_kb) == 1) break;
+            fclose(f);
+        }
+        if (avail_kb > 0 && (double)host_b > (double)avail_kb * 1024.0) {
             snprintf(msg, sizeof msg, "n=%d needs ~%.1f GB of host memory for the interior-loop tables", n, host_b / 1e9);
             return pf_err(c, CCJ_E_OOM, msg);
         }

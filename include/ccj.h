@@ -173,6 +173,15 @@ int  ccj_comm_init(ccj_ctx *ctx, const char *id);
 int  ccj_shard_blocks(int n, int t, int world, int rank, int *a_out, int cap);
 /* Per-matrix element count C_t of level t and the a-block size M_t (the same for every world). */
 int  ccj_level_layout(int n, int t, int world, long long *C, int *M);
+/* The level-t exchange slice (host helper, no GPU; the geometry k_pack / k_unpack use),
+ * in int16 elements: out4 = {nmax (the largest rank's block count), P-tail offset, span-tail offset,
+ * slice size}.  The body is [matrix][own block][cell] of nmax blocks per matrix. */
+int  ccj_exchange_layout(int n, int t, int world, long long *out4);
+/* which = 0: for each body element of rank's slice, the level element (x*C + a*M + c) packed there
+ * (-1: padding); which = 1: for each level element, its position in the gathered buffer
+ * (owner * slice + body position) as rank unpacks it (-1: rank's own cell).  Returns the entry
+ * count; fills out only when cap >= that count.  < 0: bad arguments. */
+long long ccj_exchange_index(int n, int t, int world, int rank, int which, long long *out, long long cap);
 /* In-process exchange group (tests, and several ranks sharing one device): shard_world contexts,
  * each driven by its own host thread, join one group instead of an RCCL communicator. */
 typedef struct ccj_group ccj_group;

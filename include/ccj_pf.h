@@ -77,6 +77,9 @@ typedef struct ccj_pf_raw {
  * type 0 rows taken as INF, which every shipped set has).  device = HIP ordinal. */
 int ccj_pf_create(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_pf_ctx **out);
 void ccj_pf_destroy(ccj_pf_ctx *ctx);
+/* The device and host bytes ccj_pf_create allocates for a sequence of length n (its up-front size
+ * check compares them with the device's free memory and the host's MemAvailable). */
+void ccj_pf_footprint(int n, unsigned long long *device_bytes, unsigned long long *host_bytes);
 
 /* ccj_pf(): the whole fill on the GPU, then W on the host.  *energy = to_Energy(W[n], n)
  * (part_func.cc:148-150,173). */

@@ -22,7 +22,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from tests.oracle_lib import HASH_NAMES, blob, oracle_lib  # noqa: E402
 
-CASES = [("t04_400_seed6", 6, 400, "Turner04"), ("t04_400_seed7", 7, 400, "Turner04")]
+# Config 5 is seeds 6..13 (bench.py --n 400 --seed 6 --gpus 8: rank r folds seed 6 + r).
+CASES = [("t04_400_seed%d" % s, s, 400, "Turner04") for s in range(6, 14)]
 
 
 def seq(seed, n):

@@ -107,3 +107,20 @@ def test_cli_validation_paths(capsys):
     out = io.StringIO()
     assert run([], stdin=io.StringIO("\n"), stdout=out, stderr=err) == 1
     assert out.getvalue() == "sequence is missing\n"
+
+
+def test_pf_footprint_counts_the_large_allocations():
+    """ccj_pf_footprint (the basis of ccj_pf_create's up-front size check): at least
+    the int32 4-D store, its copies and the two double window tables; host = the window tables."""
+    import ctypes
+    L = ctypes.CDLL(LIB)
+    L.ccj_pf_footprint.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]
+    L.ccj_pf_footprint.restype = None
+    for n in (10, 100, 200):
+        dev, host = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        L.ccj_pf_footprint(n, ctypes.byref(dev), ctypes.byref(host))
+        cells = sum((t + 1) * (n - t - 2) * (n - t - 1) // 2 for t in range(n - 2))
+        ie = 2 * 29 * 29 * (n + 1) * (n + 2) * 8
+        assert host.value == ie
+        assert dev.value >= ie + (21 + 2) * cells * 4
+        assert dev.value <= 1.3 * (ie + (21 + 2) * cells * 4) + (64 << 20)

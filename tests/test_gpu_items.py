@@ -1,7 +1,5 @@
-"""The interior-loop work decompositions checked against the reference (-m gpu): the default
-k_iloop work items (ccj_items.h, 128-cell items), enumerated three ways, and the k_iltile tiles
-(CCJ_ILOOP_TILES=1: 16 keys x 64 cells, sequence-independent), each unsharded and
-band-sharded.
+"""The interior-loop work decomposition checked against the reference (-m gpu): the k_iloop work
+items (ccj_items.h, 128-cell items), counted two ways, each unsharded and band-sharded.
 
 In items mode ccj_reset sizes the k_iloop launches from per-(level, shard, split) item counts made
 on the GPU by k_items; the host holds the same enumeration twice (count_level_items, the fast row walk, and
@@ -43,10 +41,9 @@ print(json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("mode", [{"CCJ_ILOOP_TILES": "0", "CCJ_CHECK_ITEMS": "1"},
-                                  {"CCJ_ILOOP_TILES": "0", "CCJ_HOST_COUNT": "1", "CCJ_CHECK_ITEMS": "1"},
-                                  {"CCJ_ILOOP_TILES": "1"}],
-                         ids=["items-gpu-count-checked", "items-host-count", "tiles"])
+@pytest.mark.parametrize("mode", [{"CCJ_CHECK_ITEMS": "1"},
+                                  {"CCJ_HOST_COUNT": "1", "CCJ_CHECK_ITEMS": "1"}],
+                         ids=["items-gpu-count-checked", "items-host-count"])
 def test_item_counts_agree_and_fold_matches_reference(mode):
     env = dict(os.environ, **mode)
     cases = [{k: c[k] for k in ("tag", "seq", "dangles", "params", "noGU")} for c in CASES]

@@ -88,6 +88,31 @@ def test_pf_past_295_checks_exactness():
 
 
 @pytest.mark.gpu
+def test_pf_size_check_boundary(monkeypatch):
+    """ccj_pf_create's up-front size check: with the device's free memory set to exactly the bytes
+    ccj_pf_footprint reports (CCJ_PF_DEVMEM_LIMIT, a test hook) the context is created; one byte
+    less fails with CCJ_E_OOM (2) before any table is built."""
+    import ctypes
+    import ccj_amd
+    L = ccj_amd.lib()
+    L.ccj_pf_footprint.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]
+    L.ccj_pf_footprint.restype = None
+    seq = "GGGAAACCCAGCUUCGGCUGGGAAACCC"
+    dev, host = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+    L.ccj_pf_footprint(len(seq), ctypes.byref(dev), ctypes.byref(host))
+    monkeypatch.setenv("CCJ_PF_DEVMEM_LIMIT", str(dev.value - 1))
+    with pytest.raises(ccj_amd.CCJError) as ei:
+        ccj_amd.W_final_pf(seq)
+    assert ei.value.code == 2, ei.value
+    monkeypatch.setenv("CCJ_PF_DEVMEM_LIMIT", str(dev.value))
+    pf = ccj_amd.W_final_pf(seq)
+    try:
+        pf.ccj_pf()
+    finally:
+        pf.close()
+
+
+@pytest.mark.gpu
 def test_pf_range_exit(monkeypatch):
     """The exactness guard itself: with the bound lowered from 2^53 to 2^10 (CCJ_PF_RANGE_LOG2, a
     test hook), a sequence whose P sums carry large terms fails with CCJ_E_PF_RANGE (10) naming the

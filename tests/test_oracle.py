@@ -66,12 +66,25 @@ def test_level_parallel_oracle_matches_reference_n100():
         o.close()
 
 
+def test_level_parallel_oracle_matches_reference_n200():
+    """n=200 (the headline bench sequence, t04_200) in the default CPU suite: the level-parallel
+    restatement the config-5 fixtures (hashes_n400.json) rest on, against the reference's 31 hashes."""
+    case = [c for c in golden("hashes_large.json") if c["tag"] == "t04_200"][0]
+    o = OracleFold(case["seq"], blob(case["params"]), 2, 0, threads=int(os.environ.get("CCJ_ORACLE_THREADS", "0")))
+    try:
+        got = o.hashes()
+        assert got == case["hashes"]
+        assert o.W(200) == case["mfe"]
+    finally:
+        o.close()
+
+
 SLOW = os.environ.get("CCJ_SLOW_TESTS") == "1"
 
 
 @pytest.mark.skipif(not SLOW, reason="minutes per case on 8 cores: run with CCJ_SLOW_TESTS=1 "
                     "(log of the last run: profiles/r4_oracle_par_large.log)")
-@pytest.mark.parametrize("tag", ["t04_150", "t04_200", "dp09_200", "t04_220", "dp09_230"])
+@pytest.mark.parametrize("tag", ["t04_150", "dp09_200", "t04_220", "dp09_230"])
 def test_level_parallel_oracle_matches_reference_large(tag):
     """The level-parallel restatement against the reference's 31 matrix hashes at the BASELINE
     sizes and past the stock abort (n=220 / 230: the reference's own sources built with -DNDEBUG,

@@ -7,10 +7,13 @@
   the C oracle, which is the checker here) into one slice [matrix][own block][cell] of nmax blocks
   (nmax = the largest rank's block count), the slices are all-gathered as ONE collective per level
   (the RCCL path does the same on the GPU), and unpacking the other ranks' slices must rebuild the
-  level exactly as one process writes it.
+  level exactly as one process writes it.  Pack, unpack and the slice layout go through the shipped
+  index maps (ccj_exchange_index / ccj_exchange_layout: the ccj_engine.h xch_* functions k_pack and
+  k_unpack use), not a model of them.
 * 2-D spans: interval i of every span belongs to rank (i-1) % world (k_diag2d); the exchange of
-  level t also carries span t (k_dtail_pack / k_dtail_unpack: V, Vt, P, WBP, WPP, WM, WMv, WMp ... of
-  the rank's own intervals), and unpacking must give every rank the whole span.
+  level t also carries span t (k_dtail_pack / k_dtail_unpack: the 10 int32 planes V, Vt, P, WBP, WB,
+  WPP, WP, WMv, WMp, WM of the rank's own intervals, in the kernels' order), and unpacking must give
+  every rank the whole span.
 * P terms: each rank pushes only its share of the terms of P(i, i+sigma) (k_ppush outer index
   jo / d-j-1 taken r, r+G, ...), as (value + 2^31) << 32 | first-split key words; the tail of the
   exchange of level sigma-2 carries them and the minimum over the ranks must be the reference's P
@@ -81,23 +84,48 @@ def _level(n, t, fold, blocks):
     return buf, C, M
 
 
-def _pack(level, C, M, blocks, nmax):
-    """k_pack: slice [x][own index][M] of nmax blocks per matrix."""
-    sl = np.zeros(NMAT4 * nmax * M, dtype=np.int16)
-    for o, a in enumerate(blocks):
-        for x in range(NMAT4):
-            sl[(x * nmax + o) * M:(x * nmax + o + 1) * M] = level[x * C + a * M: x * C + (a + 1) * M]
-    return sl
+def _xlib():
+    import ctypes
+    from tests.oracle_lib import ROOT
+    L = ctypes.CDLL(os.path.join(ROOT, "ccj_amd", "lib", "libccj_hip.so"))
+    L.ccj_exchange_layout.argtypes = [ctypes.c_int] * 3 + [ctypes.POINTER(ctypes.c_longlong)]
+    L.ccj_exchange_index.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_longlong), ctypes.c_longlong]
+    L.ccj_exchange_index.restype = ctypes.c_longlong
+    return L
 
 
-def _unpack(level, C, M, slices, world, rank, t, nmax, shard_blocks, n):
-    """k_unpack: the other ranks' blocks from their slices."""
-    for r in range(world):
-        if r == rank:
-            continue
-        for o, a in enumerate(shard_blocks(n, t, world, r)):
-            for x in range(NMAT4):
-                level[x * C + a * M: x * C + (a + 1) * M] = slices[r][(x * nmax + o) * M:(x * nmax + o + 1) * M]
+def xch_layout(n, t, world):
+    """{nmax, P-tail offset, span-tail offset, slice} in int16 elements (ccj_exchange_layout: the
+    geometry k_pack / k_unpack / the host's slices use, ccj_engine.h xch_*)."""
+    import ctypes
+    out = (ctypes.c_longlong * 4)()
+    assert _xlib().ccj_exchange_layout(n, t, world, out) == 0
+    return list(out)
+
+
+def xch_index(n, t, world, rank, which):
+    """ccj_exchange_index: which 0 = the level element each body element of rank's slice packs
+    (-1 padding); 1 = each level element's position in the gathered buffer (-1 own cell)."""
+    import ctypes
+    L = _xlib()
+    cnt = L.ccj_exchange_index(n, t, world, rank, which, None, 0)
+    assert cnt >= 0
+    out = np.zeros(cnt, dtype=np.int64)
+    assert L.ccj_exchange_index(n, t, world, rank, which, out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), cnt) == cnt
+    return out
+
+
+def _pack(level, n, t, world, rank):
+    """k_pack through the shipped index map: the body of rank's slice."""
+    idx = xch_index(n, t, world, rank, 0)
+    return np.where(idx >= 0, level[np.maximum(idx, 0)], 0).astype(np.int16)
+
+
+def _unpack(level, gathered, n, t, world, rank):
+    """k_unpack through the shipped index map: every other rank's cell from the gathered slices."""
+    idx = xch_index(n, t, world, rank, 1)
+    other = idx >= 0
+    level[other] = gathered[idx[other]]
 
 
 def _gloo_rank(rank, world, port, n, seq, q):
@@ -142,44 +170,60 @@ def _p_partials(fold, n, sigma, world, rank):
     return out
 
 
+CP_PENALTY, PUP_PENALTY = 12, 6  # h_globals.hh:11,25 (the defaults every oracle fold here uses)
+
+
+def _span_values(fold, i, l):
+    """The XCH_DT_N = 10 planes of k_dtail_pack, in its order: V, Vt, P, WBP, WB, WPP, WP, WMv, WMp,
+    WM (oracle get2 ids: P 0, WBP 1, WPP 2, V 3, Vt 4, WM 5, WMv 6, WMp 7); WB / WP are k_diag2d's
+    derived min(cp * len, WBP) / min(PUP * len, WPP)."""
+    g = [fold.get2(x, i, l) for x in range(8)]
+    ln = l - i + 1
+    return [g[3], g[4], g[0], g[1], min(CP_PENALTY * ln, g[1]), g[2], min(PUP_PENALTY * ln, g[2]), g[6], g[7], g[5]]
+
+
 def _span_tail(fold, n, sigma, world, rank):
-    """k_dtail_pack: the 2-D values (oracle get2 ids 0..7) of this rank's intervals of span sigma."""
-    tail = np.zeros((8, n + 1), dtype=np.int32)
+    """k_dtail_pack: the 10 planes of this rank's intervals of span sigma."""
+    tail = np.zeros((10, n + 1), dtype=np.int32)
     for i in range(1, n - sigma + 1):
         if (i - 1) % world == rank:
-            tail[:, i] = [fold.get2(x, i, i + sigma) for x in range(8)]
+            tail[:, i] = _span_values(fold, i, i + sigma)
     return tail
 
 
 def _gloo_body(rank, world, n, seq, torch, dist):
-    from ccj_amd import shard_blocks
     fold = OracleFold(seq, blob("Turner04"), 2, 0)
     ok = True
     for t in range(n - 2):
+        from ccj_amd import shard_blocks
         mine = shard_blocks(n, t, world, rank)
-        nmax = max(len(shard_blocks(n, t, world, r)) for r in range(world))
+        nmax, p_off, d_off, slice_n = xch_layout(n, t, world)
         level, C, M = _level(n, t, fold, mine)
         sig = t + 2  # the P span whose partials ride this exchange (pushed after level t-1)
-        tail = _p_partials(fold, n, sig, world, rank) if 1 <= t and sig <= n - 1 else np.zeros(n + 1, np.uint64)
-        body = _pack(level, C, M, mine, nmax).view(np.uint8)
-        span = _span_tail(fold, n, t, world, rank)
-        own = torch.from_numpy(np.concatenate([body, np.zeros((-len(body)) % 8, np.uint8), tail.view(np.uint8),
-                                               span.reshape(-1).view(np.uint8)]))
-        parts = [torch.empty_like(own) for _ in range(world)]
-        dist.all_gather(parts, own)  # ONE collective per level: cells + P tail + span t
-        nb = len(body) + (-len(body)) % 8
-        slices = [p[:len(body)].numpy().view(np.int16) for p in parts]
-        _unpack(level, C, M, slices, world, rank, t, nmax, shard_blocks, n)
+        ptail = _p_partials(fold, n, sig, world, rank) if 1 <= t and sig <= n - 1 else np.zeros(n + 1, np.uint64)
+        # this rank's slice, laid out as the host lays out d_send: body, P tail, span tail
+        own = np.zeros(slice_n, dtype=np.int16)
+        body = _pack(level, n, t, world, rank)
+        own[:len(body)] = body
+        own[p_off:d_off] = ptail.view(np.int16)
+        own[d_off:] = _span_tail(fold, n, t, world, rank).reshape(-1).view(np.int16)
+        # gloo has no int16 all-gather: the slices travel as bytes (RCCL: ncclInt8 likewise)
+        parts = [torch.empty(2 * slice_n, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, torch.from_numpy(own.view(np.uint8)))  # ONE collective per level: cells + P tail + span t
+        parts = [p.numpy().view(np.int16) for p in parts]
+        gathered = np.concatenate(parts)
+        _unpack(level, gathered, n, t, world, rank)
         full, _, _ = _level(n, t, fold, range(t + 1))
         ok &= bool(np.array_equal(level, full))
-        # k_dtail_unpack: each interval from its owner's slice; the whole span on every rank
-        st = nb + 8 * (n + 1)
-        spans = [p[st:].numpy().view(np.int32).reshape(8, n + 1) for p in parts]
+        # k_dtail_unpack: each interval from its owner's slice (the whole span on every rank), and
+        # WBW rebuilt from the WBP / WP planes
         for i in range(1, n - t + 1):
-            got = spans[(i - 1) % world][:, i]
-            ok &= all(int(got[x]) == fold.get2(x, i, i + t) for x in range(8))
+            sl = gathered[((i - 1) % world) * slice_n + d_off:((i - 1) % world + 1) * slice_n].view(np.int32)
+            got = [int(sl[x * (n + 1) + i]) for x in range(10)]
+            ok &= got == _span_values(fold, i, i + t)
+            ok &= (got[3], got[6]) == (_span_values(fold, i, i + t)[3], _span_values(fold, i, i + t)[6])
         if 1 <= t and sig <= n - 1:
-            comb = np.minimum.reduce([p[nb:].numpy().view(np.uint64) for p in parts])
+            comb = np.minimum.reduce([p[p_off:d_off].view(np.uint64) for p in parts])
             for i in range(1, n - sig + 1):
                 ref = fold.get2(0, i, i + sig)  # reference P (INF+1 when no term)
                 got = int(comb[i])
@@ -221,3 +265,35 @@ def test_p_term_partition_covers_every_term_once(world):
         for do in range(jo + 1, sigma):
             for ko in range(do + 1, sigma):
                 assert 0 <= p_term_rank(jo, do, ko, sigma, world) < world
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_exchange_index_maps_rebuild_every_level(world):
+    """The shipped pack / unpack maps (ccj_exchange_index) at every level of n=40: each rank's slice
+    holds exactly its own cells, and unpacking the gathered slices gives every rank every other
+    rank's cell, so own + unpacked = the whole level (values: the element indices themselves)."""
+    from ccj_amd import shard_blocks
+    n = 40
+    for t in range(n - 2):
+        nmax, p_off, d_off, slice_n = xch_layout(n, t, world)
+        C = (t + 1) * (n - t - 2) * (n - t - 1) // 2
+        full = np.arange(NMAT4 * C, dtype=np.int64)
+        slices = []
+        for r in range(world):
+            idx = xch_index(n, t, world, r, 0)
+            assert len(idx) <= p_off and len(idx) == NMAT4 * nmax * ((n - t - 2) * (n - t - 1) // 2)
+            own = idx[idx >= 0]
+            assert len(np.unique(own)) == len(own)
+            M = (n - t - 2) * (n - t - 1) // 2
+            assert sorted(set((own % C) // M)) == shard_blocks(n, t, world, r)
+            sl = np.full(slice_n, -1, dtype=np.int64)
+            sl[:len(idx)] = np.where(idx >= 0, full[np.maximum(idx, 0)], -1)
+            slices.append(sl)
+        gathered = np.concatenate(slices)
+        for r in range(world):
+            u = xch_index(n, t, world, r, 1)
+            M = (n - t - 2) * (n - t - 1) // 2
+            mine = np.isin((np.arange(NMAT4 * C) % C) // M, shard_blocks(n, t, world, r))
+            assert np.array_equal(u < 0, mine)
+            got = np.where(u >= 0, gathered[np.maximum(u, 0)], full)
+            assert np.array_equal(got, full)
