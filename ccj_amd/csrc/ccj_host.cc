@@ -167,7 +167,7 @@ struct ccj_ctx {
     bool join_diag = true;               // k_diag2d(t-1) after k_iloop(t) on st_il (one cross-stream wait per level)
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<hipEvent_t> pp_done; // band-sharded: this rank's P-term push of span sigma done (before the exchange)
-    std::vector<double> lev_ms_v, diag_ms_v, il_ms_v;
+    std::vector<double> lev_ms_v, diag_ms_v, il_ms_v, xch_ms_v;
     std::vector<hipEvent_t> il_done, dg_done;  // k_iloop(t) / k_diag2d(sigma) finished
     std::vector<hipEvent_t> lev_done;
     std::vector<hipEvent_t> tev;  // timing events: 2 per k_level4d, k_iloop and k_diag2d launch
@@ -2114,6 +2114,7 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                 HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, G, r, st));
             }
             if (G > 1 && !c->simulate) {
+                HIPCHK(c, trec(6, st));  // timing mode 2: the exchange's share of the level span
                 // band-sharded exchange: this rank's cells of the level, all 22
                 // matrices, packed into one slice; ONE all-gather of equal slices; the other ranks'
                 // cells unpacked with their loop records and interior-loop copies
@@ -2233,6 +2234,7 @@ static int fill_finish(ccj_ctx *c) {
     c->lev_ms_v.assign(n, 0.0);
     c->diag_ms_v.assign(n, 0.0);
     c->il_ms_v.assign(n, 0.0);
+    c->xch_ms_v.assign(n, 0.0);
     if (c->level_timing == 1) {
         // level s = from the end of level s-1 (ev_pre for s = 0) to its lev_done on st: the waits for
         // k_iloop(s) / k_diag2d(s-1), the plain launch and the leaders
@@ -2255,6 +2257,10 @@ static int fill_finish(ccj_ctx *c) {
             HIPCHK(c, hipEventElapsedTime(&ms, ev[4], ev[5]));
             lsum += ms;
             c->lev_ms_v[s] = ms;
+            if (c->world > 1 && !c->simulate) {  // waits for span s / P tail, packs, all-gather, unpacks
+                HIPCHK(c, hipEventElapsedTime(&ms, ev[6], ev[5]));
+                c->xch_ms_v[s] = ms;
+            }
         }
     }
     c->level_ms = lsum;
@@ -2715,6 +2721,12 @@ extern "C" int ccj_level_times(const ccj_ctx *c, double *level_ms, double *diag_
 extern "C" int ccj_iloop_times(const ccj_ctx *c, double *iloop_ms, int cap) {
     if (!c || !iloop_ms) return CCJ_E_ARG;
     for (int t = 0; t < cap && t < (int)c->il_ms_v.size(); ++t) iloop_ms[t] = c->il_ms_v[t];
+    return CCJ_OK;
+}
+
+extern "C" int ccj_exchange_times(const ccj_ctx *c, double *xch_ms, int cap) {
+    if (!c || !xch_ms) return CCJ_E_ARG;
+    for (int t = 0; t < cap && t < (int)c->xch_ms_v.size(); ++t) xch_ms[t] = c->xch_ms_v[t];
     return CCJ_OK;
 }
 

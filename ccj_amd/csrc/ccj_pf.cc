@@ -760,8 +760,13 @@ int fill_impl(ccj_pf_ctx *c) {
     // run beside level t-1, off the level chain.  Every event is recorded before a wait on it is
     // enqueued (host order below).
     const int nl = n - 2;  // levels 0 .. n-3
+    // P(s): pushed by level (k_pf_ppush(s-3) completes it, after every earlier push on this stream),
+    // or pulled per span (k_pf_pterm, CCJ_PF_PULL=1)
+    const bool pull = getenv("CCJ_PF_PULL") && atoi(getenv("CCJ_PF_PULL")) != 0;
     auto span = [&](int s) -> hipError_t {
-        hipError_t e = launch(2, c->st_d, [&] { return ccjk_pf_pterm(&c->D, s, c->st_d); });
+        hipError_t e = launch(2, c->st_d, [&] {
+            return pull ? ccjk_pf_pterm(&c->D, s, c->st_d) : s >= 3 ? ccjk_pf_ppush(&c->D, s - 3, c->st_d) : 0;
+        });
         if (e == hipSuccess) e = launch(3, c->st_d, [&] { return ccjk_pf_diag(&c->D, s, c->st_d); });
         return e != hipSuccess ? e : hipEventRecord(c->ev_dg[s], c->st_d);
     };

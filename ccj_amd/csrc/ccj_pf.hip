@@ -155,6 +155,168 @@ __global__ __launch_bounds__(256) void k_pf_pterm(PfDev D, int s) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// The same P terms pushed by level (the MFE engine's k_ppush scheme): k_pf_ppush(T),
+// after level T, sums every term whose higher operand level is T (part A: t1 = T >= t2; part B:
+// t2 = T > t1; t1 + t2 = s - 3 for P(i, i+s)).  That completes P(T+3) and adds partial sums to the
+// longer spans.  The level-T operand of a term is the same cell for PF_PP_S consecutive spans, so a
+// wave loads it once for PF_PP_S partners (1 + 1/PF_PP_S loads per term instead of 2), and it is
+// the level just written.  The sums are exact int64 (as in k_pf_pterm), so any order is the same.
+//   part A wave: (jo, 64 consecutive i, PF_PP_S consecutive t2), loop h1 = d-j-1:
+//       A = level T, block jo, row h1, position i;  B = level t2, block h1, row T-jo, position i+jo+1
+//   part B wave: (a2 = d-j-1, 64 consecutive l, PF_PP_S consecutive t1), loop h2 = k-d-1:
+//       B = level T, block a2, row h2, position l-h2-T-2;  A = level t1, block t1-h2, row a2, position l-T-3-t1
+// ---------------------------------------------------------------------------------------------
+constexpr int PF_PP_S = 8;
+
+__device__ __forceinline__ const int *pf_pk_row(const PfDev &D, int t, int a, int h) {
+    const PfLvlS L = ldc_lvl(D.ld + t);
+    const int m = D.n - t - 2;
+    return D.d4 + L.lb + PF_PK * L.C + (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) - 1;  // + position (1-based)
+}
+__device__ __forceinline__ const int *pf_uni(const int *p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    return (const int *)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ int pf_at(const int *row, int pos) {
+    typedef const __attribute__((address_space(1))) char gchar;
+    typedef const __attribute__((address_space(1))) int gint;
+    return *(gint *)((gchar *)row + (unsigned)(pos << 2));  // global_load saddr + voffset
+}
+
+__global__ __launch_bounds__(256) void k_pf_ppush(PfDev D, int lev, int ngrp, int npairs, int hs_len, int blocksA) {
+    const int n = D.n, rs = D.rs;
+    const int lane = threadIdx.x & 63;
+    const int partB = (int)blockIdx.x >= blocksA;
+    const int item = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - (partB ? blocksA : 0)) * 4 + (int)(threadIdx.x >> 6));
+    // item = (pair * nout + outer) * ngrp + g (k_ppush's enumeration, unsharded): g, 64 intervals,
+    // fastest, so a workgroup's 4 waves read adjacent segments of the same rows
+    const int nout = lev + 1;
+    const int g = item % ngrp;
+    int pr = item / ngrp;
+    const int outer = pr % nout;
+    pr /= nout;
+    if (pr >= npairs) return;  // whole wave
+    const int nmax = imin(lev, n - 4 - lev) + 1;
+    int c = 0;
+    for (;; ++c) {
+        const int cnt = (imin((c + 1) * PF_PP_S, nmax) + hs_len - 1) / hs_len;
+        if (pr < cnt) break;
+        pr -= cnt;
+    }
+    const int hs = pr;
+    const int nother = (partB ? imin(lev - 1, n - 4 - lev) : imin(lev, n - 4 - lev)) + 1;
+    const int o0 = c * PF_PP_S;
+    if (o0 >= nother) return;
+    const int ns = imin(PF_PP_S, nother - o0);
+    const int h_lo = hs * hs_len;
+    const int hmax = imin(o0 + ns - 1, h_lo + hs_len - 1);
+    if (h_lo > hmax) return;
+    long long acc[PF_PP_S];
+    unsigned long long aab[PF_PP_S];
+#pragma unroll
+    for (int s = 0; s < PF_PP_S; ++s) acc[s] = 0, aab[s] = 0;
+    const int mT = n - lev - 2;
+    auto add = [&](int s, int x, bool live) {
+        const long long v = live ? (long long)x : 0;
+        acc[s] += v;
+        aab[s] += (unsigned long long)(v < 0 ? -v : v);
+    };
+    if (!partB) {
+        const int jo = outer, b1 = lev - jo;
+        const int i = 1 + g * 64 + lane;
+        if (1 + g * 64 > n - (lev + 3 + o0)) return;  // no lane has an interval of the shortest span
+        const int *rowA0 = pf_pk_row(D, lev, jo, 0);  // row h: + h*mT - h(h-1)/2
+        const int *rowB[PF_PP_S];
+        int Ms[PF_PP_S], offB[PF_PP_S];
+#pragma unroll
+        for (int s = 0; s < PF_PP_S; ++s) {
+            const int t2 = imin(o0 + s, o0 + ns - 1);
+            rowB[s] = pf_pk_row(D, t2, 0, b1);  // block h1 added per step
+            Ms[s] = ldc_lvl(D.ld + t2).M;
+            offB[s] = imin(i, n - (lev + 3 + t2)) + jo + 1;
+        }
+        // two steps per iteration, all 2 * (PF_PP_S + 1) loads in flight together (the second step of
+        // an odd tail re-reads the first and is masked)
+        for (int h1 = h_lo; h1 <= hmax; h1 += 2) {
+            int va[2], vb[2][PF_PP_S], hh[2];
+            hh[0] = h1;
+            hh[1] = imin(h1 + 1, hmax);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int h = hh[u];
+                va[u] = pf_at(pf_uni(rowA0 + h * mT - ((h * (h - 1)) >> 1)), imin(i, mT - h));
+#pragma unroll
+                for (int s = 0; s < PF_PP_S; ++s) {
+                    const int t2 = imin(o0 + s, o0 + ns - 1), hc = imin(h, t2);
+                    vb[u][s] = pf_at(pf_uni(rowB[s] + (long long)hc * Ms[s]), offB[s]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const bool live = u == 0 || h1 + 1 <= hmax;
+#pragma unroll
+                for (int s = 0; s < PF_PP_S; ++s) add(s, imul_wrap(va[u], vb[u][s]), live && s < ns && hh[u] <= o0 + s);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < PF_PP_S; ++s) {
+            const int sg = lev + 3 + o0 + s;
+            if (s < ns && i + sg <= n) {
+                if (acc[s]) atomicAdd((unsigned long long *)&D.Pacc[sg * rs + i], (unsigned long long)acc[s]);
+                if (aab[s]) atomicAdd(&D.Pabs[sg * rs + i], aab[s]);
+            }
+        }
+    } else {
+        const int a2 = outer;
+        const int l = lev + 4 + o0 + g * 64 + lane;
+        if (lev + 4 + o0 + g * 64 > n) return;
+        const int lc = imin(l, n);
+        const int *rowB0 = pf_pk_row(D, lev, a2, 0);
+        const int *rowA[PF_PP_S];
+        int Ms[PF_PP_S], offA[PF_PP_S];
+#pragma unroll
+        for (int s = 0; s < PF_PP_S; ++s) {
+            const int t1 = imin(o0 + s, o0 + ns - 1);
+            rowA[s] = pf_pk_row(D, t1, t1, a2);  // block t1-h2: minus h2*M per step
+            Ms[s] = ldc_lvl(D.ld + t1).M;
+            offA[s] = imax(1, lc - (lev + 3 + t1));
+        }
+        for (int h2 = hmax; h2 >= h_lo; h2 -= 2) {
+            int vb[2], va[2][PF_PP_S], hh[2];
+            hh[0] = h2;
+            hh[1] = imax(h2 - 1, h_lo);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int h = hh[u];
+                vb[u] = pf_at(pf_uni(rowB0 + h * mT - ((h * (h - 1)) >> 1)), imax(1, imin(lc - h - lev - 2, mT - h)));
+#pragma unroll
+                for (int s = 0; s < PF_PP_S; ++s) {
+                    const int t1 = imin(o0 + s, o0 + ns - 1), hc = imin(h, t1);
+                    va[u][s] = pf_at(pf_uni(rowA[s] - (long long)hc * Ms[s]), offA[s]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const bool live = u == 0 || h2 - 1 >= h_lo;
+#pragma unroll
+                for (int s = 0; s < PF_PP_S; ++s) add(s, imul_wrap(va[u][s], vb[u]), live && s < ns && hh[u] <= o0 + s);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < PF_PP_S; ++s) {
+            const int sg = lev + 3 + o0 + s;
+            const int i = l - sg;
+            if (s < ns && l <= n && i >= 1) {
+                if (acc[s]) atomicAdd((unsigned long long *)&D.Pacc[sg * rs + i], (unsigned long long)acc[s]);
+                if (aab[s]) atomicAdd(&D.Pabs[sg * rs + i], aab[s]);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // The 2-D values of span s, one wave per interval (i, j = i+s).  Every sum keeps the reference's
 // term order and association: the lanes evaluate up to 64 terms at once (the products, each as
 // written), then the sum adds them one after another in the reference's order (lane u's term
@@ -833,6 +995,26 @@ extern "C" int ccjk_pf_pterm(const PfDev *D, int s, void *stream) {
     if (s < 3 || ni <= 0) return 0;
     hipLaunchKernelGGL(k_pf_pterm, dim3((unsigned)((ni + 63) / 64), (unsigned)(s - 2), (unsigned)((s - 2 + PT_DD - 1) / PT_DD)),
                        dim3(256), 0, (hipStream_t)stream, *D, s);
+    return (int)hipGetLastError();
+}
+
+// P terms whose operands' highest level is lev (k_pf_ppush); completes P(lev+3).  The grid as
+// ccjk_ppush's (MFE) for one rank.
+extern "C" int ccjk_pf_ppush(const PfDev *D, int lev, void *stream) {
+#ifdef CCJ_ABLATE_PF_PTERM
+    return 0;  // timing only: this PF kernel skipped (wrong results)
+#endif
+    const int n = D->n;
+    const int nmax = imin(lev, n - 4 - lev) + 1;
+    if (nmax <= 0) return 0;
+    const int ngrp = (n - lev - 3 + 63) / 64;
+    constexpr int hs_len = 32;
+    const int nch = (nmax + PF_PP_S - 1) / PF_PP_S;
+    int npairs = 0;
+    for (int c = 0; c < nch; ++c) npairs += (imin((c + 1) * PF_PP_S, nmax) + hs_len - 1) / hs_len;
+    const int blocksA = (npairs * ngrp * (lev + 1) + 3) / 4;
+    hipLaunchKernelGGL(k_pf_ppush, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *D, lev, ngrp, npairs,
+                       hs_len, blocksA);
     return (int)hipGetLastError();
 }
 

@@ -69,6 +69,7 @@ struct PfDev {
 
 extern "C" {
 int ccjk_pf_pterm(const ccj::PfDev *D, int s, void *stream);
+int ccjk_pf_ppush(const ccj::PfDev *D, int lev, void *stream);
 int ccjk_pf_diag(const ccj::PfDev *D, int s, void *stream);
 int ccjk_pf_level(const ccj::PfDev *D, const ccj::PfLvl *Lh, int t, void *stream);
 int ccjk_pf_iloop(const ccj::PfDev *D, int t, long long first, int nitems, void *stream);

@@ -155,6 +155,10 @@ int  ccj_host_timing(const ccj_ctx *ctx, double *out3);
 /* Per-level kernel times of the last fill (ms): level_ms[t] (k_level4d, level t), diag_ms[s]
  * (k_diag2d, span s); ccj_iloop_times: iloop_ms[t] (k_iloop, level t). */
 int  ccj_level_times(const ccj_ctx *ctx, double *level_ms, double *diag_ms, int cap);
+/* Band-sharded contexts in timing mode 2: per level, the exchange's part of the level span (from
+ * the end of the level's launches to the end of its unpack: waits for the span and P tails, packs,
+ * the all-gather, unpacks); 0 elsewhere. */
+int  ccj_exchange_times(const ccj_ctx *ctx, double *xch_ms, int cap);
 int  ccj_iloop_times(const ccj_ctx *ctx, double *iloop_ms, int cap);
 /* What the next fills time (HIP events): 0 = the fill only; 1 (default) = + per-level durations
  * (level_ms, from events the fill records anyway); 2 = + k_diag2d / k_iloop times and level spans

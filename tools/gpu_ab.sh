@@ -17,8 +17,8 @@ for rep in $(seq 1 "${REPS:-3}"); do
     else
       env $envp timeout -k 10 300 python bench.py --steps 8 --warmup 2 --no-cpu-baseline $args > gpurun_out/ab/out.json 2> gpurun_out/ab/err.txt || { echo "FAIL $v"; tail -5 gpurun_out/ab/err.txt; exit 1; }
       python3 -c "
-import json,sys; d=json.load(open('gpurun_out/ab/out.json')); b=d['breakdown_ms']
-print('%-34s step %.2f fill %.2f level %s setup %s mfe %s' % (sys.argv[1], d['ms_per_step'], b.get('fill_device', b.get('fill', 0)), b.get('level4d_levels', '-'), d.get('setup_ms', '-'), d.get('mfe', d.get('energy'))))" "$v" | tee -a gpurun_out/ab/ab.txt
+import json,sys; d=json.load(open('gpurun_out/ab/out.json')); b=d.get('breakdown_ms', {})
+print('%-34s step %.2f fill %.2f level %s setup %s mfe %s' % (sys.argv[1], d['ms_per_step'], b.get('fill_device', d.get('fill_ms', 0)), b.get('level4d_levels', '-'), d.get('setup_ms', '-'), d.get('mfe', d.get('energy'))))" "$v" | tee -a gpurun_out/ab/ab.txt
     fi
   done
 done
