@@ -384,7 +384,7 @@ __device__ __forceinline__ const int16_t *uni(const int16_t *p) {
 // minimum.  Steps that are not terms of a span (h > its t) add PP_OFF and never win.
 constexpr int PP_OFF = 1 << 30;
 
-template <int PP_S>
+template <int PP_S, int PP_U>
 __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, int npairs, int hs_len, int blocksA, int G,
                                                int rank, int nout) {
     const int n = T.n, rs = T.rs;
@@ -441,14 +441,14 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
             Ms[s] = LD[t2].M;
             offB[s] = imin(i, n - (lev + 3 + t2)) + jo + 1;
         }
-        // two steps per iteration, all 2 * (PP_S + 1) loads in flight together (the second step of
-        // an odd tail re-reads the first and is masked)
-        for (int h1 = h_lo; h1 <= hmax; h1 += 2) {
-            int va[2], vb[2][PP_S], hh[2];
-            hh[0] = h1;
-            hh[1] = imin(h1 + 1, hmax);
+        // PP_U steps per iteration, all PP_U * (PP_S + 1) loads in flight together (the steps of a
+        // short tail re-read the last one and are masked)
+        for (int h1 = h_lo; h1 <= hmax; h1 += PP_U) {
+            int va[PP_U], vb[PP_U][PP_S], hh[PP_U];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < PP_U; ++u) hh[u] = imin(h1 + u, hmax);
+#pragma unroll
+            for (int u = 0; u < PP_U; ++u) {
                 const int h = hh[u];
                 va[u] = pk_at(T, uni(rowA0 + h * mT - ((h * (h - 1)) >> 1)), lev, jo, h, imin(i, mT - h));
                 // every load unconditional (steps with h1 > t2 read a clamped valid cell and are
@@ -460,8 +460,8 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const bool live = u == 0 || h1 + 1 <= hmax;
+            for (int u = 0; u < PP_U; ++u) {
+                const bool live = h1 + u <= hmax;
 #pragma unroll
                 for (int s = 0; s < PP_S; ++s) {
                     const int code = (live && s < ns && hh[u] <= o0 + s) ? hh[u] : PP_OFF;
@@ -493,12 +493,12 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
             Ms[s] = LD[t1].M;
             offA[s] = imax(1, lc - (lev + 3 + t1));
         }
-        for (int h2 = hmax; h2 >= h_lo; h2 -= 2) {  // two steps per iteration, as in part A
-            int vb[2], va[2][PP_S], hh[2];
-            hh[0] = h2;
-            hh[1] = imax(h2 - 1, h_lo);
+        for (int h2 = hmax; h2 >= h_lo; h2 -= PP_U) {  // PP_U steps per iteration, as in part A
+            int vb[PP_U], va[PP_U][PP_S], hh[PP_U];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < PP_U; ++u) hh[u] = imax(h2 - u, h_lo);
+#pragma unroll
+            for (int u = 0; u < PP_U; ++u) {
                 const int h = hh[u];
                 vb[u] = pk_at(T, uni(rowB0 + h * mT - ((h * (h - 1)) >> 1)), lev, a2, h, imax(1, imin(lc - h - lev - 2, mT - h)));
 #pragma unroll
@@ -508,8 +508,8 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const bool live = u == 0 || h2 - 1 >= h_lo;
+            for (int u = 0; u < PP_U; ++u) {
+                const bool live = h2 - u >= h_lo;
 #pragma unroll
                 for (int s = 0; s < PP_S; ++s) {
                     const int code = (live && s < ns && hh[u] <= o0 + s) ? 1023 - hh[u] : PP_OFF;
@@ -731,11 +731,14 @@ __device__ __forceinline__ int2 il_scan(const DevTables &T, const uint2 *__restr
     cnt = __builtin_amdgcn_readfirstlane(cnt);
     if (cnt <= 0) return make_int2(b1, b2);
     ent = uni_ptr(ent);
+    // a batch of NB entries (8 or 16 bytes x NB) as ONE scalar load: s_load_dwordx16 / x8 (as NB
+    // separate dwordx2 loads the compiler computed a 64-bit address per entry)
+    typedef unsigned ent_vec __attribute__((ext_vector_type(2 * NB)));
     auto fetch = [&](int e0, uint2 *E) {
-        const uint2 *ep = ent + e0;
+        const ent_vec v = *(const __attribute__((address_space(4))) ent_vec *)(unsigned long long)(ent + e0);
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
-            E[u] = ld_const(ep + u);
+            E[u] = make_uint2(v[2 * u], v[2 * u + 1]);
             // PM stops at dt <= t-2, before the list's null tail: past cnt, substitute a null entry
             if (PMWIN && e0 + u >= cnt) E[u] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0u);
         }
@@ -765,14 +768,18 @@ __device__ __forceinline__ int2 il_scan(const DevTables &T, const uint2 *__restr
                 }
             }
 #endif
-            // global address space: a plain pointer rebuilt from an integer would become a flat load
+            // global address space, cast BEFORE the lane offset is added: a wave-uniform base plus a
+            // 32-bit lane offset is then one global_load saddr + voffset (added in the flat space and
+            // cast after, it cost a 64-bit VALU add per candidate)
+            typedef const __attribute__((address_space(1))) char gchar;
+            typedef const __attribute__((address_space(1))) int16_t gshort;
 #ifdef CCJ_ABLATE_ILHOT
             // timing only: every partner read hits the same cache-resident line (wrong results)
-            v[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)T.dummy + lofs2 + (((uintptr_t)p) & 0));
-            if (PAIR) w[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)T.dummy + lofs2 + 2);
+            v[u] = *(gshort *)((gchar *)T.dummy + lofs2 + (((uintptr_t)p) & 0));
+            if (PAIR) w[u] = *(gshort *)((gchar *)T.dummy + lofs2 + 2);
 #else
-            v[u] = *(const __attribute__((address_space(1))) int16_t *)(p + lofs2);
-            if (PAIR) w[u] = *(const __attribute__((address_space(1))) int16_t *)(p + lofs2b);
+            v[u] = *(gshort *)((gchar *)p + lofs2);
+            if (PAIR) w[u] = *(gshort *)((gchar *)p + lofs2b);
 #endif
         }
     };
@@ -1955,8 +1962,15 @@ extern "C" int ccjk_ppush(const DevTables *T, int lev, int G, int rank, void *st
     const int nout = rank <= lev ? (lev - rank) / G + 1 : 0;  // this rank's outer indices r, r+G, ... <= lev
     if (nout <= 0) return 0;
     const int blocksA = (npairs * ngrp * nout + 3) / 4;
-    hipLaunchKernelGGL(k_ppush<S>, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp, npairs,
-                       hs_len, blocksA, G, rank, nout);
+    // split steps in flight per wave: 4 (98 VGPRs) measured 42.1 us per launch standalone vs 53.8 with
+    // 2 (62 VGPRs), the same bytes fetched (profiles/r5_ab.txt); CCJ_PP_STEPS=2 for the A/B
+    static const int steps = getenv("CCJ_PP_STEPS") ? atoi(getenv("CCJ_PP_STEPS")) : 4;
+    if (steps >= 4)
+        hipLaunchKernelGGL((k_ppush<S, 4>), dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp,
+                           npairs, hs_len, blocksA, G, rank, nout);
+    else
+        hipLaunchKernelGGL((k_ppush<S, 2>), dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *T, lev, ngrp,
+                           npairs, hs_len, blocksA, G, rank, nout);
     return (int)hipGetLastError();
 }
 
