@@ -136,6 +136,22 @@ def host_cores():
     return max(1, min(n, cap))
 
 
+def ref_allcores_n200():
+    """The committed all-cores reference measurement at n=200 (profiles/r*_ref_allcores_n200.json,
+    written from tools/ref_allcores.py's output), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_ref_allcores_n200.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return {"value": d["value"], "unit": d["unit"], "cores": d["cores"], "wall_s": d["wall_s"],
+            "per_process_seconds": d["per_process_seconds"], "kind": "reference",
+            "source": "profiles/" + os.path.basename(files[-1]),
+            "sample": f"{d['cores']} concurrent reference folds of n=200 random RNAs (seeds "
+                      f"{d['seeds'][0]}..{d['seeds'][1]}, Turner04) on the GPU box's host"}
+
+
 def _ref_fold_cmd(drv, blob, seq):
     return [drv, "fold", "--blob", blob, "--time", seq]
 
@@ -239,7 +255,7 @@ def pf_bench(a, rank, world, dist, barrier, dev=0):
         return
     cells = num_cells(a.n)
     nl = {"k_pf_iloop": max(a.n - 2, 1), "k_pf_level": max(a.n - 2, 1), "k_pf_pterm": max(a.n - 3, 1),
-          "k_pf_diag": a.n}
+          "k_pf_ppush": max(a.n - 3, 1), "k_pf_diag": a.n}
 
     # HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this workload
     # (tools/gpu_pf_prof.sh -> tools/make_profiles.py --pf), when committed
@@ -577,6 +593,12 @@ def main(argv=None):
     out["reference_cpu_n200_s"] = REF_N200_S
     out["reference_n200_cells_per_s"] = num_cells(200) / REF_N200_S
     out["speedup_vs_reference_n200"] = REF_N200_S / sec_per_step if a.n == 200 else None
+    # the reference at the headline size on ALL host cores of a GPU box (16 concurrent n=200 folds,
+    # tools/ref_allcores.py; 12-15 min of CPU time, so measured once and committed, not per run)
+    ra = ref_allcores_n200()
+    if ra and a.n == 200:
+        out["reference_n200_allcores"] = ra
+        out["speedup_vs_reference_n200_allcores"] = value / ra["value"]
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -641,7 +641,9 @@ class W_final_pf:
         self._check(lib().ccj_pf_timing(self._h, ctypes.byref(t)))
         return t.value
 
-    PF_KERNELS = ("k_pf_iloop", "k_pf_level", "k_pf_pterm", "k_pf_diag")
+    # family 2, the P terms: k_pf_ppush (pushed by level, the default) or k_pf_pterm (CCJ_PF_PULL=1)
+    PF_KERNELS = ("k_pf_iloop", "k_pf_level",
+                  "k_pf_pterm" if os.environ.get("CCJ_PF_PULL", "0") not in ("", "0") else "k_pf_ppush", "k_pf_diag")
 
     def set_timing(self, on: bool = True):
         """Event pairs around every launch of the following fills (ccj_pf_set_timing)."""

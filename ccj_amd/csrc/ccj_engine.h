@@ -192,6 +192,8 @@ struct DevTables {
     // split-point sharing (above): levels [g_lo, g_hi) share; partial-record ring of SHARE_R
     // slots x SHARE_NACC x accC
     int split_target;              // k_level4d: narrow levels split loops so ~this many waves run (0: never)
+    long long xpad;                // 32767 sentinel elements in front of every level's PLx/PRx and PMx (k_iloop's null target)
+    long long xspan;               // bytes k_iloop may address from a wave's buffer base (debug check)
     int g_lo, g_hi;
     // k_level4d_lead walks only the long-scan a-blocks of a sharing level, longest scan first:
     // rank r's list lord[lord_off[t*G+r] .. lord_off[t*G+r+1]) (device), lord_off_h = the same

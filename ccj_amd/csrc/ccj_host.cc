@@ -139,7 +139,7 @@ struct ccj_ctx {
     std::vector<int> lord_off;
     int2 *d_wbw = nullptr;                   // (WBP, WP) pairs [w][p]
     long long nrec = 0;
-    long long nx = 0, npm = 0;
+    long long nx = 0, npm = 0, xpad = 0, xspan = 0;
     LvlX *d_ldx = nullptr;
     uint2 *d_il = nullptr, *d_ilm = nullptr;
     int16_t *d_dummy = nullptr;
@@ -1821,21 +1821,34 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipMalloc(&c->d_lb, c->lv_off.size() * sizeof(long long)));
     HIPCHK(cp, hipMalloc(&c->d_ld, c->lv_off.size() * sizeof(LvlDev)));
     {
-        // interior-loop copies (ccj_engine.h): PLx+PRx mirror the level sizes, PMx is padded per (h, j)
+        // interior-loop copies (ccj_engine.h): PLx+PRx mirror the level sizes, PMx is padded per (h, j).
+        // In front of every level: xpad sentinel elements of 32767, the null target of k_iloop's
+        // waves (a wave addresses its source levels as 32-bit offsets from the pad of the lowest)
+        const long long xpad = n + 256;
         std::vector<LvlX> ldx(c->lv_off.size(), LvlX{0, 0});
-        long long ox = 0, op = 0;
+        long long ox = 0, op = 0, span = 0;
         for (int t = 0; t < c->nlev; ++t) {
+            ox += xpad;
+            op += xpad;
             ldx[t] = LvlX{ox, op};
             ox += 2LL * c->lv_host[t].C;
             op += (long long)c->lv_host[t].m * n * (t + 1);
+            const int tlo = std::max(0, t - (2 * MAXLOOP - 2));  // a wave of level t + 3 .. t + 58 reads down to tlo
+            span = std::max({span, 2 * (ox - (ldx[tlo].lbx - xpad)), 2 * (op - (ldx[tlo].pmb - xpad))});
         }
+        if (span >= (1LL << 32) - 4096)
+            return set_err(cp, CCJ_E_ARG, "n=%d: the interior-loop copies of 56 levels exceed 4 GB (k_iloop offsets)", n);
         const size_t pad = 256;
         c->nx = ox;
         c->npm = op;
-        // pad elements on both sides (slack for clamped partner offsets; never read as values)
+        c->xpad = xpad;
+        c->xspan = span;
+        // pad elements on both sides; everything starts as 32767 (the pads stay so: no level writes them)
         if (hipMalloc(&c->d4x_alloc, ((size_t)ox + 2 * pad) * sizeof(int16_t)) != hipSuccess ||
             hipMalloc(&c->pmx_alloc, ((size_t)op + 2 * pad) * sizeof(int16_t)) != hipSuccess)
             return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for interior-loop copies failed", (ox + op) * 2e-9);
+        HIPCHK(cp, hipMemsetD16((hipDeviceptr_t)c->d4x_alloc, (unsigned short)INTERN_INF, (size_t)ox + 2 * pad));
+        HIPCHK(cp, hipMemsetD16((hipDeviceptr_t)c->pmx_alloc, (unsigned short)INTERN_INF, (size_t)op + 2 * pad));
         c->d4x = c->d4x_alloc + pad;
         c->pmx = c->pmx_alloc + pad;
         HIPCHK(cp, hipMalloc(&c->d_ldx, ldx.size() * sizeof(LvlX)));
@@ -1935,6 +1948,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.pmx = c->pmx;
     T.nx = c->nx;
     T.npm = c->npm;
+    T.xpad = c->xpad;
+    T.xspan = c->xspan;
     T.ldx = c->d_ldx;
     T.il = c->d_il;
     T.ilm = c->d_ilm;

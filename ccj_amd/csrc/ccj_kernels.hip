@@ -596,7 +596,7 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
                 make_uint2(((uint32_t)dt << 21) | ((uint32_t)u1 << 16) | (uint32_t)(uint16_t)es[u1][u2], (uint32_t)(2 * u1 * dt));
         cnt += __popcll(mask);
     }
-    // null tail: dt 63 addresses T.dummy (32767), energy 32767 -> 65534, never below a clamped result
+    // null tail: dt 63 addresses the sentinel pad (32767), energy 32767 -> 65534, never below a clamped result
     if (lane < IL_B) ent[cnt + lane] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0u);
 }
 
@@ -692,7 +692,7 @@ extern "C" int ccjk_items(const DevTables *T, int G, int rank, int simulate, lon
 // offset: A (64-bit, per source level) and B (per u1) are per-wave tables held one value per lane
 // and fetched with readlane, so an entry costs a few scalar ops and one load on a uniform base.
 // IL_B entries are loaded together (one s_load burst), then IL_B partner values, then reduced.
-// Null tail entries (dt 63) hit T.dummy, so the last batch needs no masking (PL/PR: cnt is the
+// Null tail entries (dt 63) hit the sentinel pad, so the last batch needs no masking (PL/PR: cnt is the
 // whole list; PM stops early and substitutes null entries).
 // Loads at wave-uniform addresses of data no kernel of the fill writes (candidate lists, segment
 // tables): through the constant address space, so they are scalar (SMEM) loads.  As plain global
@@ -724,7 +724,7 @@ __device__ __forceinline__ int il_e(uint32_t x) { return (int)(int16_t)(x & 0xff
 // entries per batch keep the loads in flight (and the registers) at 2*IL_B.
 template <bool CROSS, bool PMWIN, bool PAIR>
 __device__ __forceinline__ int2 il_scan(const DevTables &T, const uint2 *__restrict__ ent, int cnt,
-                                        unsigned long long Atab, int Btab, unsigned lofs2, int as, int bs,
+                                        __amdgpu_buffer_rsrc_t src, int Atab, int Btab, unsigned lofs2, int as, int bs,
                                         unsigned lofs2b, int asb, int bsb) {
     constexpr int NB = PAIR ? IL_B / 2 : IL_B;
     int b1 = INF, b2 = INF;
@@ -747,17 +747,17 @@ __device__ __forceinline__ int2 il_scan(const DevTables &T, const uint2 *__restr
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
             const int dt = il_dt(E[u].x), u1 = il_u1(E[u].x);
-            unsigned off = (unsigned)__builtin_amdgcn_readlane(Btab, u1);
+            // the partner's byte offset from the wave's buffer base: A[dt] + B[u1] (+ 2 u1 dt), all
+            // 32-bit and wave-uniform, so it is the load's soffset and the lane's offset its voffset
+            // (a 64-bit address per candidate cost a 64-bit VALU add and a third readlane)
+            unsigned off = (unsigned)__builtin_amdgcn_readlane(Btab, u1) + (unsigned)__builtin_amdgcn_readlane(Atab, dt);
             if (CROSS) off += E[u].y;
-            const char *p = (const char *)(rdl64(Atab, dt) + off);
 #ifdef CCJ_DEBUG_BOUNDS
-            {   // the partner must lie inside its copy (or be the null target)
+            {   // the partner must lie inside its copy (the null target is the pad in front of a level)
                 bool bad = false;
                 for (int c = 0; c < (PAIR ? 2 : 1); ++c) {
-                    const int16_t *q = (const int16_t *)(p + (c ? lofs2b : lofs2));
-                    const bool in = (q >= T.d4x && q < T.d4x + T.nx) || (q >= T.pmx && q < T.pmx + T.npm) ||
-                                    (q >= T.dummy && q < T.dummy + T.n + 64);
-                    bad = bad || !in;
+                    const unsigned o = off + (c ? lofs2b : lofs2);
+                    bad = bad || o >= (unsigned)T.xspan;
                 }
                 if (bad || (dt != 63 && (dt < 2 || dt > 2 * MAXLOOP - 2))) {
                     if (atomicOr(T.err, 64) == 0)
@@ -768,19 +768,12 @@ __device__ __forceinline__ int2 il_scan(const DevTables &T, const uint2 *__restr
                 }
             }
 #endif
-            // global address space, cast BEFORE the lane offset is added: a wave-uniform base plus a
-            // 32-bit lane offset is then one global_load saddr + voffset (added in the flat space and
-            // cast after, it cost a 64-bit VALU add per candidate)
-            typedef const __attribute__((address_space(1))) char gchar;
-            typedef const __attribute__((address_space(1))) int16_t gshort;
 #ifdef CCJ_ABLATE_ILHOT
             // timing only: every partner read hits the same cache-resident line (wrong results)
-            v[u] = *(gshort *)((gchar *)T.dummy + lofs2 + (((uintptr_t)p) & 0));
-            if (PAIR) w[u] = *(gshort *)((gchar *)T.dummy + lofs2 + 2);
-#else
-            v[u] = *(gshort *)((gchar *)p + lofs2);
-            if (PAIR) w[u] = *(gshort *)((gchar *)p + lofs2b);
+            off &= 0u;
 #endif
+            v[u] = (int)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(src, (int)lofs2, (int)off, 0);
+            if (PAIR) w[u] = (int)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(src, (int)lofs2b, (int)off, 0);
         }
     };
     auto reduce = [&](const uint2 *E, const int *v, const int *w) {
@@ -844,11 +837,10 @@ __device__ __forceinline__ int bperm(int v, int l) { return __builtin_amdgcn_ds_
 #endif
 constexpr int ILG_B = CCJ_ILG_B;  // entries per lane per batch in the grouped walk (registers: 8 waves/SIMD)
 template <bool CROSS, bool PMWIN>
-__device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__restrict__ ent, int cnt, unsigned long long Atab, int Btab,
-                                         unsigned lofs2, int as, int bs, int G, int W, int g, int rl) {
+__device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__restrict__ ent, int cnt, __amdgpu_buffer_rsrc_t src,
+                                         int Atab, int Btab, unsigned lofs2, int as, int bs, int G, int W, int g, int rl) {
     int b1 = INF;
     if (cnt <= 0) return b1;
-    const int alo = (int)(unsigned)Atab, ahi = (int)(unsigned)(Atab >> 32);
     // only the packed word is loaded (the cross term 2*u1*dt is recomputed): half the registers
     const uint32_t nul = (63u << 21) | (uint32_t)INTERN_INF;
     auto fetch = [&](int e0, uint32_t *E) {
@@ -863,26 +855,20 @@ __device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__rest
 #pragma unroll
         for (int u = 0; u < ILG_B; ++u) {
             const int dt = il_dt(E[u]), u1 = il_u1(E[u]);
-            unsigned off = (unsigned)bperm(Btab, u1);
+            // per-lane entries: the offset from the wave's buffer base is per lane (voffset)
+            unsigned off = (unsigned)bperm(Btab, u1) + (unsigned)bperm(Atab, dt) + lofs2;
             if (CROSS) off += (unsigned)(2 * u1 * dt);
-            const unsigned long long A = ((unsigned long long)(unsigned)bperm(ahi, dt) << 32) | (unsigned)bperm(alo, dt);
 #ifdef CCJ_DEBUG_BOUNDS
-            {
-                const int16_t *q = (const int16_t *)((const char *)(A + off) + lofs2);
-                const bool in = (q >= T.d4x && q < T.d4x + T.nx) || (q >= T.pmx && q < T.pmx + T.npm) ||
-                                (q >= T.dummy && q < T.dummy + T.n + 64);
-                if (!in || (dt != 63 && (dt < 2 || dt > 2 * MAXLOOP - 2))) {
-                    if (atomicOr(T.err, 64) == 0) printf("k_iloop (grouped, G %d) OOB: dt %d u1 %d\n", G, dt, u1);
-                    v[u] = 0;
-                    continue;
-                }
+            if (off >= (unsigned)T.xspan || (dt != 63 && (dt < 2 || dt > 2 * MAXLOOP - 2))) {
+                if (atomicOr(T.err, 64) == 0) printf("k_iloop (grouped, G %d) OOB: dt %d u1 %d\n", G, dt, u1);
+                v[u] = 0;
+                continue;
             }
 #endif
 #ifdef CCJ_ABLATE_ILHOT
-            v[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)T.dummy + lofs2 + ((A + off) & 0));
-#else
-            v[u] = *(const __attribute__((address_space(1))) int16_t *)((const char *)(A + off) + lofs2);
+            off = lofs2;  // timing only: every partner read on the lane's own line of the pad
 #endif
+            v[u] = (int)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(src, (int)off, 0, 0);
         }
     };
     auto reduce = [&](const uint32_t *E, const int *v) {
@@ -940,6 +926,18 @@ __device__ __forceinline__ ILGroups il_groups(int nact, int lane) {
     return {64 / W, W, lane / W, lane & (W - 1)};
 }
 
+// The partner buffer of one k_iloop wave: every copy row its candidates read lies in the source
+// levels t-58 .. t-3, at most a few GB past the sentinel pad (T.xpad elements of 32767) in front of
+// the lowest one, so the wave addresses them as 32-bit byte offsets from that pad (buffer loads:
+// soffset = the candidate's uniform offset, voffset = the lane's).  A null list entry (dt 63, the
+// lane-63 A entry) lands in the pad: 32767, never below a clamped result.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t il_src(const int16_t *base) {
+    const unsigned long long v = (unsigned long long)base;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((unsigned long long)hi << 32) | lo), (short)0, -1, 0x00020000);
+}
+
 // one wave per work item: a closing pair that can pair and up to IL_CW (two 64-lane chunks) of
 // its cells (ccj_items.h, built by k_items in enumeration order)
 constexpr int IL_WPB = 4;  // waves (consecutive items) per k_iloop workgroup (1, 2, 8, 16 measured +3.6 ... +9 ms)
@@ -955,6 +953,10 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
     const int tl = t - lane;  // A-table lane L describes source level t-L (dt = L)
     const bool lvl_ok = lane >= 2 && lane <= 2 * MAXLOOP - 2 && tl >= 0;
     const long long BIAS = (long long)(n + 64) * (n + 64);  // keeps B >= 0
+    // the wave's buffer base: the sentinel pad in front of the lowest source level's copies
+    const int tlo = imax(0, t - (2 * MAXLOOP - 2));
+    const long long xb = T.ldx[tlo].lbx - T.xpad, pb = T.ldx[tlo].pmb - T.xpad;  // elements
+    const __amdgpu_buffer_rsrc_t src = il_src(role == 2 ? T.pmx + pb : T.d4x + xb);
     if (role == 0) {
         // PL: wave = (a, i, h-chunk), lanes h; closing pair (i, j)
         const int a = f1, i = f2, len = m - i + 1, h0 = zc * IL_CW;
@@ -970,18 +972,18 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         //   = [lbx + (a-dt)M + i*m + i*dt + dt-1] + [u1*m - x(x-1)/2 - u1] + u1*dt
         const int x = i + lane;
         const int Btab = (int)(2 * ((long long)lane * m - ((long long)x * (x - 1) >> 1) - lane + BIAS));
-        unsigned long long Atab = 0;
+        int Atab = 0;
         if (lvl_ok && a >= lane)
-            Atab = (unsigned long long)T.d4x +
-                   2 * (T.ldx[tl].lbx + (long long)(a - lane) * T.ld[tl].M + (long long)i * m + (long long)i * lane + lane - 1 - BIAS);
+            Atab = (int)(unsigned)(2 * (T.ldx[tl].lbx - xb + (long long)(a - lane) * T.ld[tl].M + (long long)i * m +
+                                        (long long)i * lane + lane - 1 - BIAS));
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
-        if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
+        if (lane == 63) Atab = -B0;
         const int e0 = (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
         const uint2 *le = T.il + pidx * IL_CAP + e0;
         const int lc = (int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0;
-        const int2 bm = G > 1  ? make_int2(il_scan_g<true, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl), INF)
-                        : pair ? il_scan<true, false, true>(T, le, lc, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
-                               : il_scan<true, false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
+        const int2 bm = G > 1  ? make_int2(il_scan_g<true, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl), INF)
+                        : pair ? il_scan<true, false, true>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
+                               : il_scan<true, false, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
         if ((act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) || (actb && hb >= m)) {
             atomicOr(T.err, 128);
@@ -1009,16 +1011,16 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         // PRx(t-dt, a, h+1+u1, i) = lbx + C + a*M + qq(qq+1)/2 + i-1, qq = q+1+u1
         const int qq = q + 1 + lane;
         const int Btab = qq * (qq + 1);  // bytes
-        unsigned long long Atab = 0;
-        if (lvl_ok) Atab = (unsigned long long)T.d4x + 2 * (T.ldx[tl].lbx + T.ld[tl].C + (long long)a * T.ld[tl].M);
+        int Atab = 0;
+        if (lvl_ok) Atab = (int)(unsigned)(2 * (T.ldx[tl].lbx - xb + T.ld[tl].C + (long long)a * T.ld[tl].M));
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
-        if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
+        if (lane == 63) Atab = -B0;
         const int e0 = (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
         const uint2 *le = T.il + pidx * IL_CAP + e0;
         const int lc = (int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0;
-        const int2 bm = G > 1  ? make_int2(il_scan_g<false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl), INF)
-                        : pair ? il_scan<false, false, true>(T, le, lc, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
-                               : il_scan<false, false, false>(T, le, lc, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
+        const int2 bm = G > 1  ? make_int2(il_scan_g<false, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl), INF)
+                        : pair ? il_scan<false, false, true>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
+                               : il_scan<false, false, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
         if ((act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) || (actb && (hb < 0 || ib > m - hb))) {
             atomicOr(T.err, 128);
@@ -1050,19 +1052,18 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         // Lanes outside the get_PMiloop window read another cell of the same level (h+dt >= 4:
         // in bounds) and are masked.
         const int Btab = (int)(2 * (-(long long)lane * (t + 2) + BIAS));
-        unsigned long long Atab = 0;
+        int Atab = 0;
         if (lvl_ok)
-            Atab = (unsigned long long)T.pmx +
-                   2 * (T.ldx[tl].pmb + ((long long)(h + lane) * n + (j - 2)) * (tl + 1) - 1 - BIAS);
+            Atab = (int)(unsigned)(2 * (T.ldx[tl].pmb - pb + ((long long)(h + lane) * n + (j - 2)) * (tl + 1) - 1 - BIAS));
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
-        if (lane == 63) Atab = (unsigned long long)T.dummy - (unsigned)B0;
+        if (lane == 63) Atab = -B0;
         // entries with dt > t-2 fit no cell of this level
         const int cnt = (int)ld_const(T.ilmseg + pidx * IL_SEG + imin(t - 1, IL_SEG - 1));
         const int e0 = (int)ld_const(T.ilmseg + pidx * IL_SEG + 3);
         const uint2 *le = T.ilm + pidx * IL_CAP + e0;
-        const int2 bm = G > 1  ? make_int2(il_scan_g<true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl), INF)
-                        : pair ? il_scan<true, true, true>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, lofs2b, ab, t - ab)
-                               : il_scan<true, true, false>(T, le, cnt - e0, Atab, Btab, lofs2, as, t - as, 0u, 0, 0);
+        const int2 bm = G > 1  ? make_int2(il_scan_g<true, true>(T, le, cnt - e0, src, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl), INF)
+                        : pair ? il_scan<true, true, true>(T, le, cnt - e0, src, Atab, Btab, lofs2, as, t - as, lofs2b, ab, t - ab)
+                               : il_scan<true, true, false>(T, le, cnt - e0, src, Atab, Btab, lofs2, as, t - as, 0u, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
         if ((act && (a < 0 || a > t || h < 0 || h >= m || (j - a) < 1 || (j - a) > m - h)) ||
             (actb && (ab < 0 || ab > t || (j - ab) < 1 || (j - ab) > m - h))) {

@@ -188,7 +188,7 @@ struct ccj_pf_ctx {
     PfLvl *d_ld = nullptr;
     hipStream_t st = nullptr;     // levels (k_pf_level), the memsets, the result copies
     hipStream_t st_il = nullptr;  // k_pf_iloop(t): after level t-2
-    hipStream_t st_d = nullptr;   // k_pf_pterm(s), k_pf_diag(s): after level s-3
+    hipStream_t st_d = nullptr;   // k_pf_ppush(s-3) (P of span s), k_pf_diag(s): after level s-3
     std::vector<hipEvent_t> ev_lev, ev_il, ev_dg;  // level t done, iloop t done, span s done
     hipEvent_t ev_start = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -202,7 +202,7 @@ struct ccj_pf_ctx {
     // per-kernel-family timing (ccj_pf_set_timing): an event pair around every launch
     bool timing = false;
     std::vector<hipEvent_t> tev;
-    std::vector<int> tfam;      // family of launch q: 0 k_pf_iloop, 1 k_pf_level, 2 k_pf_pterm, 3 k_pf_diag
+    std::vector<int> tfam;      // family of launch q: 0 k_pf_iloop, 1 k_pf_level, 2 P terms (k_pf_ppush / k_pf_pterm), 3 k_pf_diag
     double kms[4] = {0, 0, 0, 0};
     std::string msg;
     // vrna_urn() of the reference build: rand() / RAND_MAX (utils.c:262-271, no HAVE_ERAND48), on
@@ -345,7 +345,7 @@ void free_dev(ccj_pf_ctx *c) {
 //   k_pf_iloop: 4 B per active lane per window term it loads (masked), 4 B stack operand, 8 B R store
 //   k_pf_level: 4 B per 4-D operand load of the 21 recurrences (split loops, seeds, P blocks as
 //               evaluated for this sequence's pairs), 8 B per R read, 21 x 4 B stores + 4 B per copy
-//   k_pf_pterm: 2 x 4 B per PK product;  k_pf_diag: 8 B per 2-D operand of the span's sums
+//   P terms (k_pf_ppush / k_pf_pterm): 2 x 4 B per PK product, the pull form's operands;  k_pf_diag: 8 B per 2-D operand of the span's sums
 struct PfWork {
     double iloop = 0, level = 0, pterm = 0, diag = 0;
 };
