@@ -351,32 +351,29 @@ __device__ __forceinline__ unsigned long long rdl64(unsigned long long v, int l)
 // (pseudo_loop.cc:867-896) its first split, without a rescan.
 // ------------------------------------------------------------------------------------------
 
-__device__ __forceinline__ const int16_t *pk_row(const DevTables &T, int t, int a, int h) {
-    const int m = T.n - t - 2;
-    const LvlDev *__restrict__ LD = T.ld;  // read-only in the kernel: scalar loads
-    const LvlDev L = LD[t];
-    return T.d4 + L.lb + (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) - 1;  // + position (1-based)
+// k_ppush's operands as buffer loads: a wave reads PK at level lev and at the PP_S consecutive levels
+// o0 .. o0+ns-1, each set within a few hundred MB of its lowest level's start, so each is one buffer
+// (base = that level's start) and an operand is (uniform byte offset, lane byte offset) = (soffset,
+// voffset): no 64-bit address per load (as row pointers the compiler ran out of SGPRs and formed a
+// 64-bit VGPR address for most of them)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pk_src(const DevTables &T, int t) {
+    const unsigned long long v = (unsigned long long)(T.d4 + T.ld[t].lb);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((unsigned long long)hi << 32) | lo), (short)0, -1, 0x00020000);
 }
-
-// one int16 of a PK row: wave-uniform row pointer + 32-bit lane offset (saddr + voffset load)
-__device__ __forceinline__ int pk_at(const DevTables &T, const int16_t *row, int t, int a, int h, int pos) {
+// PK at (level t, block a, row h, position pos) read through the buffer of level tb <= t: soff =
+// 2 * (the row's start relative to tb's start), voff = 2 * (pos - 1)
+__device__ __forceinline__ int pk_buf(const DevTables &T, __amdgpu_buffer_rsrc_t src, int soff, int voff, int t, int a, int h,
+                                      int pos) {
 #ifdef CCJ_DEBUG_BOUNDS
     if (t < 0 || t >= T.nlev || a < 0 || a > t || h < 0 || h >= T.n - t - 2 || pos < 1 || pos > T.n - t - 2 - h) {
         atomicOr(T.err, 32);
         return 0;
     }
 #endif
-    typedef const __attribute__((address_space(1))) char gchar;
-    typedef const __attribute__((address_space(1))) int16_t gshort;
-    return (int)*(gshort *)((gchar *)row + (unsigned)(pos << 1));  // global_load saddr + voffset
-}
-
-// a wave-uniform pointer, marked so (keeps row bases in SGPRs: saddr loads, no 64-bit VALU adds)
-__device__ __forceinline__ const int16_t *uni(const int16_t *p) {
-    const unsigned long long v = (unsigned long long)p;
-    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
-    return (const int16_t *)(((unsigned long long)hi << 32) | lo);
+    (void)T; (void)t; (void)a; (void)h; (void)pos;
+    return (int)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(src, voff, soff, 0);
 }
 
 // A wave's running minimum per span is one int: (value << 10) + code, code = the step's position in
@@ -426,20 +423,23 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
     for (int s = 0; s < PP_S; ++s) bv[s] = 0x7fffffff;
     const int mT = n - lev - 2;
     const LvlDev *__restrict__ LD = T.ld;
-    const int16_t *lev0 = T.d4 + LD[lev].lb - 1;
+    const int Mlev = LD[lev].M;
+    const long long lbo = LD[o0].lb;  // the other operand's buffer: levels o0 .. o0+ns-1
+    const __amdgpu_buffer_rsrc_t srcT = pk_src(T, lev), srcO = pk_src(T, o0);
+    auto Grow = [&](int m_, int h) { return h * m_ - ((h * (h - 1)) >> 1); };
     if (!partB) {
         const int jo = outer, b1 = lev - jo;
         const int i = 1 + g * 64 + lane;
         if (1 + g * 64 > n - (lev + 3 + o0)) return;  // no lane has an interval of the shortest span
-        const int16_t *rowA0 = lev0 + (long long)jo * LD[lev].M;
-        const int16_t *rowB[PP_S];
-        int Ms[PP_S], offB[PP_S];
+        const int sA0 = 2 * (jo * Mlev);  // + 2 G(h) per step
+        // B of span s: the row's start relative to level o0 plus the lane's position (voffset, fixed
+        // per lane) and the block h1 (soffset h1 * 2M, per step)
+        int voB[PP_S], Ms2[PP_S];
 #pragma unroll
         for (int s = 0; s < PP_S; ++s) {
             const int t2 = imin(o0 + s, o0 + ns - 1);
-            rowB[s] = pk_row(T, t2, 0, b1);  // block h1 added per step
-            Ms[s] = LD[t2].M;
-            offB[s] = imin(i, n - (lev + 3 + t2)) + jo + 1;
+            Ms2[s] = __builtin_amdgcn_readfirstlane(2 * LD[t2].M);  // uniform: a per-lane soffset would be a waterfall loop
+            voB[s] = (int)(2 * (LD[t2].lb - lbo + Grow(n - t2 - 2, b1))) + 2 * (imin(i, n - (lev + 3 + t2)) + jo);
         }
         // PP_U steps per iteration, all PP_U * (PP_S + 1) loads in flight together (the steps of a
         // short tail re-read the last one and are masked)
@@ -450,13 +450,13 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
 #pragma unroll
             for (int u = 0; u < PP_U; ++u) {
                 const int h = hh[u];
-                va[u] = pk_at(T, uni(rowA0 + h * mT - ((h * (h - 1)) >> 1)), lev, jo, h, imin(i, mT - h));
+                va[u] = pk_buf(T, srcT, sA0 + 2 * Grow(mT, h), 2 * (imin(i, mT - h) - 1), lev, jo, h, imin(i, mT - h));
                 // every load unconditional (steps with h1 > t2 read a clamped valid cell and are
                 // masked)
 #pragma unroll
                 for (int s = 0; s < PP_S; ++s) {
                     const int t2 = imin(o0 + s, o0 + ns - 1), hc = imin(h, t2);
-                    vb[u][s] = pk_at(T, uni(rowB[s] + (long long)hc * Ms[s]), t2, hc, b1, offB[s]);
+                    vb[u][s] = pk_buf(T, srcO, hc * Ms2[s], voB[s], t2, hc, b1, imin(i, n - (lev + 3 + t2)) + jo + 1);
                 }
             }
 #pragma unroll
@@ -483,15 +483,15 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
         const int l = lev + 4 + o0 + g * 64 + lane;
         if (lev + 4 + o0 + g * 64 > n) return;
         const int lc = imin(l, n);
-        const int16_t *rowB0 = lev0 + (long long)a2 * LD[lev].M;
-        const int16_t *rowA[PP_S];
-        int Ms[PP_S], offA[PP_S];
+        const int sB0 = 2 * (a2 * Mlev);  // + 2 G(h) per step
+        // A of span s: row start relative to level o0 plus the lane's position (voffset), block
+        // t1-h2 (soffset (t1-h2) * 2M, per step)
+        int voA[PP_S], Ms2[PP_S];
 #pragma unroll
         for (int s = 0; s < PP_S; ++s) {
             const int t1 = imin(o0 + s, o0 + ns - 1);
-            rowA[s] = pk_row(T, t1, t1, a2);  // block t1-h2: minus h2*M per step
-            Ms[s] = LD[t1].M;
-            offA[s] = imax(1, lc - (lev + 3 + t1));
+            Ms2[s] = __builtin_amdgcn_readfirstlane(2 * LD[t1].M);
+            voA[s] = (int)(2 * (LD[t1].lb - lbo + Grow(n - t1 - 2, a2))) + 2 * (imax(1, lc - (lev + 3 + t1)) - 1);
         }
         for (int h2 = hmax; h2 >= h_lo; h2 -= PP_U) {  // PP_U steps per iteration, as in part A
             int vb[PP_U], va[PP_U][PP_S], hh[PP_U];
@@ -500,11 +500,12 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
 #pragma unroll
             for (int u = 0; u < PP_U; ++u) {
                 const int h = hh[u];
-                vb[u] = pk_at(T, uni(rowB0 + h * mT - ((h * (h - 1)) >> 1)), lev, a2, h, imax(1, imin(lc - h - lev - 2, mT - h)));
+                const int pb = imax(1, imin(lc - h - lev - 2, mT - h));
+                vb[u] = pk_buf(T, srcT, sB0 + 2 * Grow(mT, h), 2 * (pb - 1), lev, a2, h, pb);
 #pragma unroll
                 for (int s = 0; s < PP_S; ++s) {  // unconditional loads, clamped and masked as in part A
                     const int t1 = imin(o0 + s, o0 + ns - 1), hc = imin(h, t1);
-                    va[u][s] = pk_at(T, uni(rowA[s] - (long long)hc * Ms[s]), t1, t1 - hc, a2, offA[s]);
+                    va[u][s] = pk_buf(T, srcO, (t1 - hc) * Ms2[s], voA[s], t1, t1 - hc, a2, imax(1, lc - (lev + 3 + t1)));
                 }
             }
 #pragma unroll
