@@ -162,7 +162,7 @@ struct DevTables {
     const int8_t *rtype;           // 8
     const int *hp;                 // [w][p] HairpinE (s_energy_matrix.cc:275-282), INF if type 0
     const int16_t *est;            // [w][p] e_stP, saturated at 32767
-    int16_t *ie;                   // [u1][u2][w][p] e_intP, saturated at 32767
+    int16_t *ie;                   // [w][p] e_intP of the u1 = u2 = 0 interior loop (k_precompute_ie), 32767 where skipped
     int *V; int8_t *Vt; int *WM, *WMv, *WMp, *P, *WBP, *WPP, *WB, *WP;  // [w][p]
     int2 *WBW;                     // [w][p] (WBP, WP): the two 2-D operands of a k_level4d split step, one load
     unsigned long long *Pk;        // [w][p] (P + 2^31) << 32 | first (j,d,k) split of the minimum (k_pterm)

@@ -1739,7 +1739,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     for (auto &e : c->tev) HIPCHK(cp, hipEventCreate(&e));
 
     const size_t plane = (size_t)(n + 1) * c->rs;
-    const size_t ie_elems = (size_t)IE_U * IE_U * (n + 1) * c->rs;
+    const size_t ie_elems = (size_t)(n + 1) * c->rs;  // the u1 = u2 = 0 plane (k_build_il evaluates the rest)
     if (c->total4 > 0 && hipMalloc(&c->d4, (size_t)c->total4 * sizeof(int16_t)) != hipSuccess)
         return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for 4-D matrices failed", c->total4 * 2e-9);
     // AoS loop records: NREC 16-byte records per cell (ccj_engine.h)

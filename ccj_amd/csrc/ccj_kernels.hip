@@ -157,35 +157,31 @@ __global__ void k_init2d(DevTables T, int total) {
 }
 
 // ------------------------------------------------------------------------------------------
-// e_intP table: IE[u1][u2][w][p] = lrint(e_intP * E_IntLoop(...)) for outer (p, p+w) and inner
-// (p+u1+1, p+w-u2-1)  (pseudo_loop.cc:822-826, 836-840).  The reference skips a candidate unless
-// both pairs can pair (get_P?iloop's can_pair tests); such entries hold 32767, and the matrix value
-// they are added to is then the never-set 32767 of that pair, so the sum can never
-// undercut a stored value (all stores clamp at 32767).
+// e_intP of one pseudoknot interior loop: lrint(e_intP * E_IntLoop(...)) for outer (p, p+w) and
+// inner (p+u1+1, p+w-u2-1) (pseudo_loop.cc:822-826, 836-840).  The reference skips a candidate
+// unless both pairs can pair (get_P?iloop's can_pair tests): 32767 then, and the matrix value it
+// would be added to is the never-set 32767 of that pair, so the sum can never
+// undercut a stored value (all stores clamp at 32767).  k_build_il evaluates it for every list
+// entry (each candidate once per list), k_precompute_ie for u1 = u2 = 0 (k_level4d's stack-like
+// interior loop, the plane T.ie).
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int e_intP(const DevTables &T, int u1, int u2, int p, int q) {
+    const int d = p + u1 + 1, dp = q - u2 - 1;
+    if (dp - d < 1) return INTERN_INF;
+    const int t1 = T.pair[T.S[p] * 8 + T.S[q]];
+    const int t2 = T.pair[T.S[d] * 8 + T.S[dp]];
+    if (t1 <= 0 || t2 <= 0) return INTERN_INF;  // the reference only visits candidates with can_pair() on both pairs
+    const int e = E_IntLoop(T.prm, T.lx, u1, u2, t1, T.rtype[t2], T.S1[p + 1], T.S1[q - 1], T.S1[d - 1], T.S1[dp + 1]);
+    const int v = (int)rint(T.e_intP * (double)e);
+    if (v < -32768 || v >= INTERN_INF) atomicOr(T.err, 1);
+    return v;
+}
+
 __global__ void k_precompute_ie(DevTables T) {
     const int n = T.n, rs = T.rs;
-    const int w = blockIdx.y;          // outer span
-    const int uu = blockIdx.z;         // u1*29+u2
-    const int u1 = uu / IE_U, u2 = uu - u1 * IE_U;
-    for (int p = 1 + blockIdx.x * blockDim.x + threadIdx.x; p + w <= n; p += gridDim.x * blockDim.x) {
-        const int q = p + w;
-        const int d = p + u1 + 1, dp = q - u2 - 1;
-        int16_t out = INTERN_INF;
-        if (dp - d >= 1) {
-            const int t1 = T.pair[T.S[p] * 8 + T.S[q]];
-            const int t2 = T.pair[T.S[d] * 8 + T.S[dp]];
-            const int e = E_IntLoop(T.prm, T.lx, u1, u2, t1, T.rtype[t2], T.S1[p + 1], T.S1[q - 1], T.S1[d - 1],
-                                    T.S1[dp + 1]);
-            const int v = (int)rint(T.e_intP * (double)e);
-            if (t1 > 0 && t2 > 0) {
-                // the reference only visits candidates with can_pair() on both pairs
-                if (v < -32768 || v >= INTERN_INF) atomicOr(T.err, 1);
-                out = (int16_t)v;
-            }
-        }
-        T.ie[((size_t)uu * (n + 1) + w) * rs + p] = out;
-    }
+    const int w = blockIdx.y;  // outer span
+    for (int p = 1 + blockIdx.x * blockDim.x + threadIdx.x; p + w <= n; p += gridDim.x * blockDim.x)
+        T.ie[(size_t)w * rs + p] = (int16_t)e_intP(T, 0, 0, p, p + w);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -571,13 +567,13 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
                 const int d = p + 1 + u1, dp = q - 1 - u2;
                 if (u1 <= imin(w, MAXLOOP) - 2 && u2 <= imin(w - u1 - 6, MAXLOOP - 2) && T.pt[(dp - d) * rs + d] > 0) {
                     valid = true;
-                    e = T.ie[((size_t)(u1 * IE_U + u2) * (n + 1) + w) * rs + p];
+                    e = e_intP(T, u1, u2, p, q);
                 }
             } else {
                 const int d = p - 1 - u1, dp = q + 1 + u2;
                 if (d >= 1 && dp <= n && T.pt[(dp - d) * rs + d] > 0) {
                     valid = true;
-                    e = T.ie[((size_t)(u1 * IE_U + u2) * (n + 1) + (dp - d)) * rs + d];
+                    e = e_intP(T, u1, u2, d, dp);
                 }
             }
             es[u1][u2] = (int16_t)e;
@@ -1883,7 +1879,7 @@ extern "C" int ccjk_init2d(const DevTables *T, void *stream) {
 
 extern "C" int ccjk_precompute_ie(const DevTables *T, void *stream) {
     const int n = T->n;
-    dim3 grid((n + 255) / 256, n + 1, IE_U * IE_U);
+    dim3 grid((n + 255) / 256, n + 1, 1);
     hipLaunchKernelGGL(k_precompute_ie, grid, dim3(256), 0, (hipStream_t)stream, *T);
     return (int)hipGetLastError();
 }
