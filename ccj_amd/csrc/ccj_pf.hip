@@ -856,36 +856,60 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t low_bits(int u) { return u < 0 ? 0u : (2u << u) - 1u; }  // bits 0..u (u <= 30)
 
-// r + term(u) for each set bit u of mk in ascending order (the reference's u2 order), where lane
-// predicate on(u) holds; four terms per round, so that their loads are in flight together
-template <class T, class P>
-__device__ __forceinline__ double window_row(double r, uint32_t mk, T term, P on) {
+// readlane of a 64-bit value (lane l wave-uniform)
+__device__ __forceinline__ long long rdl64(long long v, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned long long)v, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)((unsigned long long)v >> 32), l);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+// r + e1[u2] * x(u2) for each set bit u2 of mk in ascending order (the reference's u2 order), where
+// lane predicate on(u2) holds; four terms per round, so that their loads are in flight together
+template <class LDX, class P>
+__device__ __forceinline__ double window_row(double r, uint32_t mk, const double *e1, LDX ldx, P on) {
     while (mk) {
-        const uint32_t m1 = mk & (mk - 1), m2 = m1 & (m1 - 1), m3 = m2 & (m2 - 1);
         const int q0 = __builtin_ctz(mk);
-        const int q1 = m1 ? __builtin_ctz(m1) : q0, q2 = m2 ? __builtin_ctz(m2) : q0, q3 = m3 ? __builtin_ctz(m3) : q0;
-        const double x0 = term(q0), x1 = term(q1), x2 = term(q2), x3 = term(q3);
-        if (on(q0)) r += x0;
-        if (m1 && on(q1)) r += x1;
-        if (m2 && on(q2)) r += x2;
-        if (m3 && on(q3)) r += x3;
-        mk = m3 & (m3 - 1);
+        mk &= mk - 1;
+        const bool v1 = mk != 0;
+        const int q1 = v1 ? __builtin_ctz(mk) : q0;
+        mk &= mk - 1;
+        const bool v2 = v1 && mk != 0;
+        const int q2 = v2 ? __builtin_ctz(mk) : q0;
+        mk &= mk - 1;
+        const bool v3 = v2 && mk != 0;
+        const int q3 = v3 ? __builtin_ctz(mk) : q0;
+        mk &= mk - 1;
+        if (!v3) mk = 0;
+        const int x0 = ldx(q0), x1 = ldx(q1), x2 = ldx(q2), x3 = ldx(q3);
+        const double w0 = e1[q0], w1 = e1[q1], w2 = e1[q2], w3 = e1[q3];
+        if (on(q0)) r += w0 * x0 * 1.0;
+        if (v1 && on(q1)) r += w1 * x1 * 1.0;
+        if (v2 && on(q2)) r += w2 * x2 * 1.0;
+        if (v3 && on(q3)) r += w3 * x3 * 1.0;
     }
     return r;
 }
 
+// The partner of candidate (u1, u2) (dt = 2+u1+u2, source level t-dt) is one int per lane at
+//   copy + X(dt) + Y(u1, dt) + lane offset,
+// where X(dt) (the level's block base, 64-bit) sits in lane dt of a per-wave table built once from
+// the level descriptors, so a candidate costs two readlanes and a few scalar adds instead of a
+// dependent scalar load of its level descriptor and 64-bit index arithmetic (the kernel was bound by
+// its scalar instruction stream: ~37 SALU per candidate).
 __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long first, int nitems) {
     const int wv = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
     if (wv >= nitems) return;
     const int lane = threadIdx.x & 63;
     const uint32_t it = (uint32_t)__builtin_amdgcn_readfirstlane((int)D.items[first + wv]);
     const int role = (int)(it >> 30), f1 = (int)((it >> 20) & 1023), f2 = (int)((it >> 10) & 1023), ch = (int)(it & 1023);
-    const PfG G{D};
     const int n = D.n, rs = D.rs, m = n - t - 2;
     const PfLvl L = D.ld[t];
     typedef const __attribute__((address_space(1))) int gint;
     const int *cx = D.cx, *pmx = D.pmx;
     constexpr int W2 = PF_IEW * PF_IEW;
+    // lane dt: level t-dt's descriptor (dt = 2 .. t; other lanes unused)
+    const bool lv = lane >= 2 && lane <= t;
+    const PfLvl Ll = D.ld[lv ? t - lane : t];
     double r = 0;
     long long dst;  // the cell in R
     bool act;
@@ -900,19 +924,19 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             r += x * D.est[a * rs + i];
         }
         // d = i+1+u1 < min(j, i+30); dp = j-1-u2 > max(d+3, j-30): u1 <= min(a,30)-2, u2 <= min(a-u1-6, 28)
+        // PLx(t-dt, a-dt, h+1+u2, d) at X(dt) + (i+u1)*m - (i+u1)(i+u1-1)/2 + u1*dt + u2 + hc with
+        // X(dt) = lbx + (a-dt)*M + 1 + i*dt; u1*dt + u2 = u1*(u1+2) + (u1+1)*u2
+        const long long X = Ll.lbx + (long long)(a - lane) * Ll.M + 1 + (long long)i * lane;
         const size_t pr = (size_t)a * rs + i;
         const double *ew = D.ieO + pr * W2;
         const uint32_t *mw = D.mO + pr * PF_IEW;
         const int u1m = imin(a, MAXLOOP) - 2;
         for (int u1 = 0; u1 <= u1m; ++u1) {
-            const int d = i + 1 + u1, u2m = imin(a - u1 - 6, PF_IEW - 1);
-            const double *e1 = ew + u1 * PF_IEW;
-            r = window_row(r, mw[u1] & low_bits(u2m), [&](int u2) {
-                const int dt = 2 + u1 + u2, ms = m + dt;
-                const PfLvl Ls = D.ld[t - dt];
-                const int x = *(gint *)(cx + Ls.lbx + (long long)(a - dt) * Ls.M + (d - 1) * ms - (((d - 1) * (d - 2)) >> 1) +
-                                        hc + 1 + u2);
-                return e1[u2] * x * 1.0;
+            const int u2m = imin(a - u1 - 6, PF_IEW - 1), d1 = i + u1;
+            const long long Y = (long long)d1 * m - (((long long)d1 * (d1 - 1)) >> 1) + u1 * (u1 + 2);
+            r = window_row(r, mw[u1] & low_bits(u2m), ew + u1 * PF_IEW, [&](int u2) {
+                const int dt = 2 + u1 + u2;
+                return *(gint *)(cx + (rdl64(X, dt) + Y + (u1 + 1) * u2) + hc);
             }, [](int) { return true; });
         }
     } else if (role == 1) {  // PR: q = i+h-1 fixed, lanes i <= q+1
@@ -925,18 +949,17 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             const int x = *(gint *)(cx + L2.lbx + L2.C + (long long)a * L2.M + (((q + 1) * (q + 2)) >> 1) + ic - 1);
             r += x * D.est[b * rs + k];
         }
+        // PRx(t-dt, a, h+1+u1, i) at X(dt) + qq(qq+1)/2 + ic, qq = q+1+u1, X(dt) = lbx + C + a*M - 1
+        const long long X = Ll.lbx + Ll.C + (long long)a * Ll.M - 1;
         const size_t pr = (size_t)b * rs + k;
         const double *ew = D.ieO + pr * W2;
         const uint32_t *mw = D.mO + pr * PF_IEW;
         const int u1m = imin(b, MAXLOOP) - 2;
         for (int u1 = 0; u1 <= u1m; ++u1) {
             const int u2m = imin(b - u1 - 6, PF_IEW - 1), qq = q + 1 + u1;
-            const int rowo = ((qq * (qq + 1)) >> 1) + ic - 1;
-            const double *e1 = ew + u1 * PF_IEW;
-            r = window_row(r, mw[u1] & low_bits(u2m), [&](int u2) {
-                const PfLvl Ls = D.ld[t - 2 - u1 - u2];
-                const int x = *(gint *)(cx + Ls.lbx + Ls.C + (long long)a * Ls.M + rowo);
-                return e1[u2] * x * 1.0;
+            const int rowo = ((qq * (qq + 1)) >> 1) + ic;
+            r = window_row(r, mw[u1] & low_bits(u2m), ew + u1 * PF_IEW, [&](int u2) {
+                return *(gint *)(cx + rdl64(X, 2 + u1 + u2) + rowo);
             }, [](int) { return true; });
         }
     } else {  // PM: pair (j, k = j+h+2), lanes a in [alo, ahi]
@@ -952,22 +975,21 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             r += x * D.est[(h + 4) * rs + (j - 1)];
         }
         // d = j-1-u1 > max(i, j-30), dp = k+1+u2 < min(l, k+30): u1 <= min(a-2, 28), u2 <= min(b-2, 28)
+        // PMx(tp, h+dt, d, min(ap, tp)) at X(dt) - u1*(tp+1) + min(ap, tp), tp = t-dt,
+        // X(dt) = pmb + ((h+dt)*n + j-2) * (tp+1)
+        const long long X = Ll.pmb + ((long long)(h + lane) * n + j - 2) * (t - lane + 1);
         const size_t pr = (size_t)(h + 2) * rs + j;
         const double *ew = D.ieI + pr * W2;
         const uint32_t *mw = D.mI + pr * PF_IEW;
         const int u1m = imin(ahi - 2, PF_IEW - 1), u2m = imin(t - alo - 2, PF_IEW - 1);
         const int u2l = b - 2;  // this lane's u2 bound
         for (int u1 = 0; u1 <= u1m; ++u1) {
-            const int d = j - 1 - u1;
             const bool on1 = u1 <= ac - 2;
             const int ap = imax(ac - 1 - u1, 0);
             const int u2e = imin(u2m, t - 4 - u1);  // a lane with u1 <= a-2 has b-2 <= t-4-u1
-            const double *e1 = ew + u1 * PF_IEW;
-            r = window_row(r, u2e >= 0 ? mw[u1] & low_bits(u2e) : 0u, [&](int u2) {
+            r = window_row(r, u2e >= 0 ? mw[u1] & low_bits(u2e) : 0u, ew + u1 * PF_IEW, [&](int u2) {
                 const int dt = 2 + u1 + u2, tp = t - dt;
-                const PfLvl Ls = D.ld[tp];
-                const int x = *(gint *)(pmx + Ls.pmb + ((long long)(h + dt) * n + d - 1) * (tp + 1) + imin(ap, tp));
-                return e1[u2] * x * 1.0;
+                return *(gint *)(pmx + (rdl64(X, dt) - (long long)u1 * (tp + 1)) + imin(ap, tp));
             }, [&](int u2) { return on1 && u2 <= u2l; });
         }
     }
