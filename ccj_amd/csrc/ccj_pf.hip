@@ -77,6 +77,22 @@ __device__ __forceinline__ PfLvlS ldc_lvl(const PfLvl *p) {
     return PfLvlS{q->lb, q->C, q->M};
 }
 
+// Buffer loads with a wave-uniform 32-bit byte offset (soffset) and a per-lane one (voffset) from a
+// uniform base: the split loops' operands without 64-bit address arithmetic per load (as 64-bit
+// indices the loop spent ~10 scalar instructions per load)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pf_rsrc(const void *p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((unsigned long long)hi << 32) | lo), (short)0, -1, 0x00020000);
+}
+__device__ __forceinline__ int bld32(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return (int)__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+__device__ __forceinline__ double bld64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+
 // Software-pipelined split loop over s = s0 .. s1: the loads of step s+1 are issued before step s
 // is reduced, into two alternating buffers (no register copies across the back-edge, which would
 // make the compiler wait for every load of the trip first).  The reduce adds each sum's terms in
@@ -575,26 +591,37 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         cLm01 += lm00 * bpj;  // :574-576
         cMm00 += X2(PF_PMmloop00, 0) * wbj;  // :632-633
     }
+    // split-loop operands as buffer loads: the 2-D tables from their starts (lane offset 8i / 8k),
+    // the 4-D values from the start of their level (lane offset 4(off + h*(dt-dh)))
+    const __amdgpu_buffer_rsrc_t rWBP = pf_rsrc(WBP), rWPP = pf_rsrc(WPP);
+    const int vi8 = 8 * i, vk8 = 8 * k, rs8 = 8 * rs, voff4 = 4 * off;
     struct SA { double bpi, wppi, bpj, wppj; int lm1, mm1, om1, fl1, fo1, lm2, l102, mm2, fl2, fm2, k2, s; };
     auto ldA = [&](int s) {
         SA v;
         v.s = s;
         const PfLvlS L1 = ldc_lvl(D.ld + t - s), L2 = ldc_lvl(D.ld + b + s);
-        v.bpi = WBP[(s - 1) * rs + i];
-        v.bpj = WBP[(a - s - 1) * rs + i + s + 1];
-        v.wppi = WPP[(s - 1) * rs + i];
-        v.wppj = WPP[(a - s - 1) * rs + i + s + 1];
-        v.lm1 = Xs(L1, PF_PLmloop00, s, s, 0, s);  // X1 = X(i+s, j, k, l)
-        v.mm1 = Xs(L1, PF_PMmloop00, s, s, 0, s);
-        v.om1 = Xs(L1, PF_POmloop00, s, s, 0, s);
-        v.fl1 = Xs(L1, PF_PfromL, s, s, 0, s);
-        v.fo1 = Xs(L1, PF_PfromO, s, s, 0, s);
-        v.lm2 = Xs(L2, PF_PLmloop00, a - s, a - s, a - s, 0);  // X2 = X(i, i+s, k, l)
-        v.l102 = Xs(L2, PF_PLmloop10, a - s, a - s, a - s, 0);
-        v.mm2 = Xs(L2, PF_PMmloop00, a - s, a - s, a - s, 0);
-        v.fl2 = Xs(L2, PF_PfromL, a - s, a - s, a - s, 0);
-        v.fm2 = Xs(L2, PF_PfromM, a - s, a - s, a - s, 0);
-        v.k2 = Xs(L2, PF_PK, a - s, a - s, a - s, 0);
+        const int oi = (s - 1) * rs8, oj = (a - s - 1) * rs8 + 8 * (s + 1);
+        v.bpi = bld64(rWBP, vi8, oi);
+        v.bpj = bld64(rWBP, vi8, oj);
+        v.wppi = bld64(rWPP, vi8, oi);
+        v.wppj = bld64(rWPP, vi8, oj);
+        // X1 = X(i+s, j, k, l) = (t-s, a-s, h, i+s): level start + 4((a-s)M + s) + lane 4(off + h s)
+        const __amdgpu_buffer_rsrc_t r1 = pf_rsrc(D.d4 + L1.lb);
+        const int C1 = 4 * (int)L1.C, s1 = 4 * ((a - s) * L1.M + s), v1 = voff4 + 4 * h * s;
+        v.lm1 = bld32(r1, v1, s1 + PF_PLmloop00 * C1);
+        v.mm1 = bld32(r1, v1, s1 + PF_PMmloop00 * C1);
+        v.om1 = bld32(r1, v1, s1 + PF_POmloop00 * C1);
+        v.fl1 = bld32(r1, v1, s1 + PF_PfromL * C1);
+        v.fo1 = bld32(r1, v1, s1 + PF_PfromO * C1);
+        // X2 = X(i, i+s, k, l) = (b+s, s, h+a-s, i): level start + 4(s M + G(a-s)) + lane 4 off
+        const __amdgpu_buffer_rsrc_t r2 = pf_rsrc(D.d4 + L2.lb);
+        const int dh = a - s, C2 = 4 * (int)L2.C, s2 = 4 * (s * L2.M + dh * (m + dh) - ((dh * (dh - 1)) >> 1));
+        v.lm2 = bld32(r2, voff4, s2 + PF_PLmloop00 * C2);
+        v.l102 = bld32(r2, voff4, s2 + PF_PLmloop10 * C2);
+        v.mm2 = bld32(r2, voff4, s2 + PF_PMmloop00 * C2);
+        v.fl2 = bld32(r2, voff4, s2 + PF_PfromL * C2);
+        v.fm2 = bld32(r2, voff4, s2 + PF_PfromM * C2);
+        v.k2 = bld32(r2, voff4, s2 + PF_PK * C2);
         return v;
     };
     auto rdA = [&](const SA &v) {
@@ -643,21 +670,28 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         SB v;
         v.s = s;
         const PfLvlS L3 = ldc_lvl(D.ld + t - s), L4 = ldc_lvl(D.ld + a + s);
-        v.bpk = WBP[(s - 1) * rs + k];
-        v.bpl = WBP[(b - s - 1) * rs + k + s + 1];
-        v.wppk = WPP[(s - 1) * rs + k];
-        v.wppl = WPP[(b - s - 1) * rs + k + s + 1];
-        v.rm3 = Xs(L3, PF_PRmloop00, s, 0, s, 0);  // X3 = X(i, j, k+s, l)
-        v.mm3 = Xs(L3, PF_PMmloop00, s, 0, s, 0);
-        v.fr3 = Xs(L3, PF_PfromR, s, 0, s, 0);
-        v.fm3 = Xs(L3, PF_PfromM, s, 0, s, 0);
-        v.k3 = Xs(L3, PF_PK, s, 0, s, 0);
-        v.rm4 = Xs(L4, PF_PRmloop00, b - s, 0, 0, 0);  // X4 = X(i, j, k, k+s)
-        v.mm4 = Xs(L4, PF_PMmloop00, b - s, 0, 0, 0);
-        v.om4 = Xs(L4, PF_POmloop00, b - s, 0, 0, 0);
-        v.o104 = Xs(L4, PF_POmloop10, b - s, 0, 0, 0);
-        v.fr4 = Xs(L4, PF_PfromR, b - s, 0, 0, 0);
-        v.fo4 = Xs(L4, PF_PfromO, b - s, 0, 0, 0);
+        const int ok = (s - 1) * rs8, ol = (b - s - 1) * rs8 + 8 * (s + 1);
+        v.bpk = bld64(rWBP, vk8, ok);
+        v.bpl = bld64(rWBP, vk8, ol);
+        v.wppk = bld64(rWPP, vk8, ok);
+        v.wppl = bld64(rWPP, vk8, ol);
+        // X3 = X(i, j, k+s, l) = (t-s, a, h+s, i): level start + 4(a M + G(s) at m+s) + lane 4 off
+        const __amdgpu_buffer_rsrc_t r3 = pf_rsrc(D.d4 + L3.lb);
+        const int C3 = 4 * (int)L3.C, s3 = 4 * (a * L3.M + s * (m + s) - ((s * (s - 1)) >> 1));
+        v.rm3 = bld32(r3, voff4, s3 + PF_PRmloop00 * C3);
+        v.mm3 = bld32(r3, voff4, s3 + PF_PMmloop00 * C3);
+        v.fr3 = bld32(r3, voff4, s3 + PF_PfromR * C3);
+        v.fm3 = bld32(r3, voff4, s3 + PF_PfromM * C3);
+        v.k3 = bld32(r3, voff4, s3 + PF_PK * C3);
+        // X4 = X(i, j, k, k+s) = (a+s, a, h, i): level start + 4 a M + lane 4(off + h (b-s))
+        const __amdgpu_buffer_rsrc_t r4 = pf_rsrc(D.d4 + L4.lb);
+        const int C4 = 4 * (int)L4.C, s4 = 4 * (a * L4.M), v4 = voff4 + 4 * h * (b - s);
+        v.rm4 = bld32(r4, v4, s4 + PF_PRmloop00 * C4);
+        v.mm4 = bld32(r4, v4, s4 + PF_PMmloop00 * C4);
+        v.om4 = bld32(r4, v4, s4 + PF_POmloop00 * C4);
+        v.o104 = bld32(r4, v4, s4 + PF_POmloop10 * C4);
+        v.fr4 = bld32(r4, v4, s4 + PF_PfromR * C4);
+        v.fo4 = bld32(r4, v4, s4 + PF_PfromO * C4);
         return v;
     };
     auto rdB = [&](const SB &v) {
