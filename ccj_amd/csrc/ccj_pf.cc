@@ -222,7 +222,7 @@ struct ccj_pf_ctx {
 extern "C" void ccj_pf_footprint(int n, unsigned long long *device_bytes, unsigned long long *host_bytes) {
     if (n < 1) n = 1;
     const unsigned long long rs = (unsigned long long)n + 2, plane = (unsigned long long)(n + 1) * rs;
-    const unsigned long long ie = 2ull * PF_IEW * PF_IEW * plane * sizeof(double);  // ieO + ieI
+    const unsigned long long ie = 2ull * (PF_IEW * PF_IEW * plane + 8) * sizeof(double);  // ieO + ieI (+ tail pad)
     unsigned long long d4 = 0, cx = 0, pmx = 0, maxC = 1, rows = 0;
     for (int t = 0; t <= n - 3; ++t) {
         const unsigned long long m = (unsigned long long)(n - t - 2), C = (unsigned long long)(t + 1) * (m * (m + 1) / 2);
@@ -660,8 +660,23 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     PFCHK(c, up((void **)&c->d_rtype, rt8, 8));
     PFCHK(c, up((void **)&c->d_hp, c->hp.data(), plane * sizeof(double)));
     PFCHK(c, up((void **)&c->d_est, est.data(), plane * sizeof(double)));
-    PFCHK(c, up((void **)&c->d_ieO, ie.data(), ie_n * sizeof(double)));
-    PFCHK(c, up((void **)&c->d_ieI, ieI.data(), ie_n * sizeof(double)));
+    // k_pf_iloop reads the weights of a window row only at the row's mask bits, in ascending order:
+    // store them compacted (k-th set bit -> slot k), so that a round's weights are one scalar load;
+    // 8 zero doubles of tail padding cover the last row's 8-wide reads
+    auto compact = [&](std::vector<double> &v, const std::vector<uint32_t> &mk) {
+        for (size_t r = 0; r < mk.size(); ++r) {
+            double *row = v.data() + r * PF_IEW;
+            int k = 0;
+            for (int u2 = 0; u2 < PF_IEW; ++u2)
+                if (mk[r] >> u2 & 1u) row[k++] = row[u2];
+            for (; k < PF_IEW; ++k) row[k] = 0.0;
+        }
+        v.resize(v.size() + 8, 0.0);
+    };
+    compact(ie, mO);
+    compact(ieI, mI);
+    PFCHK(c, up((void **)&c->d_ieO, ie.data(), ie.size() * sizeof(double)));
+    PFCHK(c, up((void **)&c->d_ieI, ieI.data(), ieI.size() * sizeof(double)));
     PFCHK(c, up((void **)&c->d_items, items.data(), items.size() * sizeof(uint32_t)));
     PFCHK(c, up((void **)&c->d_mO, mO.data(), mO.size() * sizeof(uint32_t)));
     PFCHK(c, up((void **)&c->d_mI, mI.data(), mI.size() * sizeof(uint32_t)));

@@ -897,39 +897,49 @@ __device__ __forceinline__ long long rdl64(long long v, int l) {
     return (long long)(((unsigned long long)hi << 32) | lo);
 }
 
-// r + e1[u2] * x(u2) for each set bit u2 of mk in ascending order (the reference's u2 order), where
-// lane predicate on(u2) holds; four terms per round, so that their loads are in flight together
+// r + w_k * x(u2_k) for the set bits u2_0 < u2_1 < ... of mk (the reference's u2 order), where lane
+// predicate on(u2) holds.  w = the row's weights compacted to the mask's set bits (ccj_pf.cc), so a
+// round's weights are one scalar load; up to 8 terms per round, their loads in flight together.
 template <class LDX, class P>
-__device__ __forceinline__ double window_row(double r, uint32_t mk, const double *e1, LDX ldx, P on) {
-    while (mk) {
-        const int q0 = __builtin_ctz(mk);
+__device__ __forceinline__ double window_row(double r, uint32_t mk, const double *w, LDX ldx, P on) {
+    for (int k = 0; mk; k += 8) {
+        int q[8];
+        bool v[8];
+        q[0] = __builtin_ctz(mk);
+        v[0] = true;
         mk &= mk - 1;
-        const bool v1 = mk != 0;
-        const int q1 = v1 ? __builtin_ctz(mk) : q0;
-        mk &= mk - 1;
-        const bool v2 = v1 && mk != 0;
-        const int q2 = v2 ? __builtin_ctz(mk) : q0;
-        mk &= mk - 1;
-        const bool v3 = v2 && mk != 0;
-        const int q3 = v3 ? __builtin_ctz(mk) : q0;
-        mk &= mk - 1;
-        if (!v3) mk = 0;
-        const int x0 = ldx(q0), x1 = ldx(q1), x2 = ldx(q2), x3 = ldx(q3);
-        const double w0 = e1[q0], w1 = e1[q1], w2 = e1[q2], w3 = e1[q3];
-        if (on(q0)) r += w0 * x0 * 1.0;
-        if (v1 && on(q1)) r += w1 * x1 * 1.0;
-        if (v2 && on(q2)) r += w2 * x2 * 1.0;
-        if (v3 && on(q3)) r += w3 * x3 * 1.0;
+#pragma unroll
+        for (int e = 1; e < 8; ++e) {
+            v[e] = mk != 0;
+            q[e] = v[e] ? __builtin_ctz(mk) : q[0];
+            mk &= mk - 1;
+        }
+        int x[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = ldx(q[e]);
+        if (v[4]) {
+#pragma unroll
+            for (int e = 4; e < 8; ++e) x[e] = ldx(q[e]);
+        } else {
+#pragma unroll
+            for (int e = 4; e < 8; ++e) x[e] = 0;
+        }
+        double wv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wv[e] = w[k + e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (v[e] && on(q[e])) r += wv[e] * x[e] * 1.0;
     }
     return r;
 }
 
 // The partner of candidate (u1, u2) (dt = 2+u1+u2, source level t-dt) is one int per lane at
-//   copy + X(dt) + Y(u1, dt) + lane offset,
-// where X(dt) (the level's block base, 64-bit) sits in lane dt of a per-wave table built once from
-// the level descriptors, so a candidate costs two readlanes and a few scalar adds instead of a
-// dependent scalar load of its level descriptor and 64-bit index arithmetic (the kernel was bound by
-// its scalar instruction stream: ~37 SALU per candidate).
+//   row(u1)[dt] + lane offset,
+// where row(u1)[dt] (a pointer) sits in lane dt of a per-wave table: the level's block base from its
+// descriptor (once per wave) plus the u1 row's terms (once per row).  A candidate then costs two
+// readlanes and one vector address add; as a dependent descriptor load plus 64-bit index arithmetic
+// per candidate the kernel was bound by its scalar instruction stream.
 __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long first, int nitems) {
     const int wv = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
     if (wv >= nitems) return;
@@ -944,6 +954,7 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
     // lane dt: level t-dt's descriptor (dt = 2 .. t; other lanes unused)
     const bool lv = lane >= 2 && lane <= t;
     const PfLvl Ll = D.ld[lv ? t - lane : t];
+    auto at = [&](const int *rowp, int dt) { return (const int *)rdl64((long long)rowp, dt); };
     double r = 0;
     long long dst;  // the cell in R
     bool act;
@@ -958,20 +969,20 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             r += x * D.est[a * rs + i];
         }
         // d = i+1+u1 < min(j, i+30); dp = j-1-u2 > max(d+3, j-30): u1 <= min(a,30)-2, u2 <= min(a-u1-6, 28)
-        // PLx(t-dt, a-dt, h+1+u2, d) at X(dt) + (i+u1)*m - (i+u1)(i+u1-1)/2 + u1*dt + u2 + hc with
-        // X(dt) = lbx + (a-dt)*M + 1 + i*dt; u1*dt + u2 = u1*(u1+2) + (u1+1)*u2
-        const long long X = Ll.lbx + (long long)(a - lane) * Ll.M + 1 + (long long)i * lane;
+        // PLx(t-dt, a-dt, h+1+u2, d) = cx[lbx + (a-dt)M + (d-1)(m+dt) - (d-1)(d-2)/2 + hc + 1 + u2]
+        const long long X = Ll.lbx + (long long)(a - lane) * Ll.M + 1 + (long long)i * lane;  // + i*dt
         const size_t pr = (size_t)a * rs + i;
         const double *ew = D.ieO + pr * W2;
         const uint32_t *mw = D.mO + pr * PF_IEW;
         const int u1m = imin(a, MAXLOOP) - 2;
         for (int u1 = 0; u1 <= u1m; ++u1) {
             const int u2m = imin(a - u1 - 6, PF_IEW - 1), d1 = i + u1;
-            const long long Y = (long long)d1 * m - (((long long)d1 * (d1 - 1)) >> 1) + u1 * (u1 + 2);
-            r = window_row(r, mw[u1] & low_bits(u2m), ew + u1 * PF_IEW, [&](int u2) {
-                const int dt = 2 + u1 + u2;
-                return *(gint *)(cx + (rdl64(X, dt) + Y + (u1 + 1) * u2) + hc);
-            }, [](int) { return true; });
+            const uint32_t mk = mw[u1] & low_bits(u2m);
+            if (!mk) continue;
+            // + (i+u1)m - (i+u1)(i+u1-1)/2 + u1*dt + u2, u2 = dt-2-u1
+            const int *rowp = cx + (X + (long long)d1 * m - (((long long)d1 * (d1 - 1)) >> 1) + u1 * lane + (lane - 2 - u1));
+            r = window_row(r, mk, ew + u1 * PF_IEW, [&](int u2) { return *(gint *)(at(rowp, 2 + u1 + u2) + hc); },
+                           [](int) { return true; });
         }
     } else if (role == 1) {  // PR: q = i+h-1 fixed, lanes i <= q+1
         const int a = f1, q = f2, b = t - a, k = q + a + 3, i = ch * 64 + lane + 1;
@@ -983,7 +994,7 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             const int x = *(gint *)(cx + L2.lbx + L2.C + (long long)a * L2.M + (((q + 1) * (q + 2)) >> 1) + ic - 1);
             r += x * D.est[b * rs + k];
         }
-        // PRx(t-dt, a, h+1+u1, i) at X(dt) + qq(qq+1)/2 + ic, qq = q+1+u1, X(dt) = lbx + C + a*M - 1
+        // PRx(t-dt, a, h+1+u1, i) = cx[lbx + C + a*M + qq(qq+1)/2 + ic - 1], qq = q+1+u1
         const long long X = Ll.lbx + Ll.C + (long long)a * Ll.M - 1;
         const size_t pr = (size_t)b * rs + k;
         const double *ew = D.ieO + pr * W2;
@@ -991,10 +1002,11 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
         const int u1m = imin(b, MAXLOOP) - 2;
         for (int u1 = 0; u1 <= u1m; ++u1) {
             const int u2m = imin(b - u1 - 6, PF_IEW - 1), qq = q + 1 + u1;
-            const int rowo = ((qq * (qq + 1)) >> 1) + ic;
-            r = window_row(r, mw[u1] & low_bits(u2m), ew + u1 * PF_IEW, [&](int u2) {
-                return *(gint *)(cx + rdl64(X, 2 + u1 + u2) + rowo);
-            }, [](int) { return true; });
+            const uint32_t mk = mw[u1] & low_bits(u2m);
+            if (!mk) continue;
+            const int *rowp = cx + (X + ((qq * (qq + 1)) >> 1));
+            r = window_row(r, mk, ew + u1 * PF_IEW, [&](int u2) { return *(gint *)(at(rowp, 2 + u1 + u2) + ic); },
+                           [](int) { return true; });
         }
     } else {  // PM: pair (j, k = j+h+2), lanes a in [alo, ahi]
         const int h = f1, j = f2, k = j + h + 2;
@@ -1009,8 +1021,7 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             r += x * D.est[(h + 4) * rs + (j - 1)];
         }
         // d = j-1-u1 > max(i, j-30), dp = k+1+u2 < min(l, k+30): u1 <= min(a-2, 28), u2 <= min(b-2, 28)
-        // PMx(tp, h+dt, d, min(ap, tp)) at X(dt) - u1*(tp+1) + min(ap, tp), tp = t-dt,
-        // X(dt) = pmb + ((h+dt)*n + j-2) * (tp+1)
+        // PMx(tp, h+dt, d, min(ap, tp)) = pmx[pmb + ((h+dt)n + j-2-u1)(tp+1) + min(ap, tp)], tp = t-dt
         const long long X = Ll.pmb + ((long long)(h + lane) * n + j - 2) * (t - lane + 1);
         const size_t pr = (size_t)(h + 2) * rs + j;
         const double *ew = D.ieI + pr * W2;
@@ -1021,9 +1032,12 @@ __global__ __launch_bounds__(256) void k_pf_iloop(PfDev D, int t, long long firs
             const bool on1 = u1 <= ac - 2;
             const int ap = imax(ac - 1 - u1, 0);
             const int u2e = imin(u2m, t - 4 - u1);  // a lane with u1 <= a-2 has b-2 <= t-4-u1
-            r = window_row(r, u2e >= 0 ? mw[u1] & low_bits(u2e) : 0u, ew + u1 * PF_IEW, [&](int u2) {
-                const int dt = 2 + u1 + u2, tp = t - dt;
-                return *(gint *)(pmx + (rdl64(X, dt) - (long long)u1 * (tp + 1)) + imin(ap, tp));
+            const uint32_t mk = u2e >= 0 ? mw[u1] & low_bits(u2e) : 0u;
+            if (!mk) continue;
+            const int *rowp = pmx + (X - (long long)u1 * (t - lane + 1));
+            r = window_row(r, mk, ew + u1 * PF_IEW, [&](int u2) {
+                const int dt = 2 + u1 + u2;
+                return *(gint *)(at(rowp, dt) + imin(ap, t - dt));
             }, [&](int u2) { return on1 && u2 <= u2l; });
         }
     }
