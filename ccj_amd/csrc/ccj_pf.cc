@@ -222,7 +222,7 @@ struct ccj_pf_ctx {
 extern "C" void ccj_pf_footprint(int n, unsigned long long *device_bytes, unsigned long long *host_bytes) {
     if (n < 1) n = 1;
     const unsigned long long rs = (unsigned long long)n + 2, plane = (unsigned long long)(n + 1) * rs;
-    const unsigned long long ie = 2ull * (PF_IEW * PF_IEW * plane + 8) * sizeof(double);  // ieO + ieI (+ tail pad)
+    const unsigned long long ie = 2ull * (PF_IEW * PF_IEW * plane + PF_ILW) * sizeof(double);  // ieO + ieI (+ tail pad)
     unsigned long long d4 = 0, cx = 0, pmx = 0, maxC = 1, rows = 0;
     for (int t = 0; t <= n - 3; ++t) {
         const unsigned long long m = (unsigned long long)(n - t - 2), C = (unsigned long long)(t + 1) * (m * (m + 1) / 2);
@@ -662,7 +662,7 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     PFCHK(c, up((void **)&c->d_est, est.data(), plane * sizeof(double)));
     // k_pf_iloop reads the weights of a window row only at the row's mask bits, in ascending order:
     // store them compacted (k-th set bit -> slot k), so that a round's weights are one scalar load;
-    // 8 zero doubles of tail padding cover the last row's 8-wide reads
+    // PF_ILW zero doubles of tail padding cover the last row's round-wide reads
     auto compact = [&](std::vector<double> &v, const std::vector<uint32_t> &mk) {
         for (size_t r = 0; r < mk.size(); ++r) {
             double *row = v.data() + r * PF_IEW;
@@ -671,7 +671,7 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
                 if (mk[r] >> u2 & 1u) row[k++] = row[u2];
             for (; k < PF_IEW; ++k) row[k] = 0.0;
         }
-        v.resize(v.size() + 8, 0.0);
+        v.resize(v.size() + PF_ILW, 0.0);
     };
     compact(ie, mO);
     compact(ieI, mI);

@@ -902,33 +902,36 @@ __device__ __forceinline__ long long rdl64(long long v, int l) {
 // round's weights are one scalar load; up to 8 terms per round, their loads in flight together.
 template <class LDX, class P>
 __device__ __forceinline__ double window_row(double r, uint32_t mk, const double *w, LDX ldx, P on) {
-    for (int k = 0; mk; k += 8) {
-        int q[8];
-        bool v[8];
+    for (int k = 0; mk; k += PF_ILW) {
+        int q[PF_ILW];
+        bool v[PF_ILW];
         q[0] = __builtin_ctz(mk);
         v[0] = true;
         mk &= mk - 1;
 #pragma unroll
-        for (int e = 1; e < 8; ++e) {
+        for (int e = 1; e < PF_ILW; ++e) {
             v[e] = mk != 0;
             q[e] = v[e] ? __builtin_ctz(mk) : q[0];
             mk &= mk - 1;
         }
-        int x[8];
+        int x[PF_ILW];
 #pragma unroll
         for (int e = 0; e < 4; ++e) x[e] = ldx(q[e]);
-        if (v[4]) {
 #pragma unroll
-            for (int e = 4; e < 8; ++e) x[e] = ldx(q[e]);
-        } else {
+        for (int g = 4; g < PF_ILW; g += 4) {  // the round's later quarters only when they hold a term
+            if (v[g]) {
 #pragma unroll
-            for (int e = 4; e < 8; ++e) x[e] = 0;
+                for (int e = g; e < g + 4; ++e) x[e] = ldx(q[e]);
+            } else {
+#pragma unroll
+                for (int e = g; e < g + 4; ++e) x[e] = 0;
+            }
         }
-        double wv[8];
+        double wv[PF_ILW];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) wv[e] = w[k + e];
+        for (int e = 0; e < PF_ILW; ++e) wv[e] = w[k + e];
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
+        for (int e = 0; e < PF_ILW; ++e)
             if (v[e] && on(q[e])) r += wv[e] * x[e] * 1.0;
     }
     return r;

@@ -28,6 +28,11 @@ enum {
 };
 
 constexpr int PF_IEW = MAXLOOP - 1;  // interior-loop window per side: u <= 28
+#ifndef CCJ_PF_ILW
+#define CCJ_PF_ILW 8
+#endif
+constexpr int PF_ILW = CCJ_PF_ILW;   // k_pf_iloop: window terms per round (multiple of 4); the compacted
+                                     // weight rows carry PF_ILW doubles of tail padding
 
 struct PfLvl {
     long long lb;  // element offset of level t
