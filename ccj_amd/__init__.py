@@ -641,9 +641,13 @@ class W_final_pf:
         self._check(lib().ccj_pf_timing(self._h, ctypes.byref(t)))
         return t.value
 
-    # family 2, the P terms: k_pf_ppush (pushed by level, the default) or k_pf_pterm (CCJ_PF_PULL=1)
-    PF_KERNELS = ("k_pf_iloop", "k_pf_level",
-                  "k_pf_pterm" if os.environ.get("CCJ_PF_PULL", "0") not in ("", "0") else "k_pf_ppush", "k_pf_diag")
+    @property
+    def PF_KERNELS(self) -> tuple:
+        """The four kernel families of kernel_ms / work_model.  Family 2, the P terms, is k_pf_ppush
+        (pushed by level, the default) or k_pf_pterm (CCJ_PF_PULL=1); ccj_pf.cc reads the variable on
+        every fill, so it is read here at call time too."""
+        pull = os.environ.get("CCJ_PF_PULL", "0") not in ("", "0")
+        return ("k_pf_iloop", "k_pf_level", "k_pf_pterm" if pull else "k_pf_ppush", "k_pf_diag")
 
     def set_timing(self, on: bool = True):
         """Event pairs around every launch of the following fills (ccj_pf_set_timing)."""

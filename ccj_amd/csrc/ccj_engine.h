@@ -34,6 +34,9 @@ constexpr int IL_B = CCJ_ILB;  // interior-loop candidates per load batch (k_ilo
 constexpr int IL_CAP = (IE_U * IE_U + IL_B + 7) / 8 * 8;  // candidate-list capacity per pair (+ IL_B null tail)
 constexpr int IL_SEG = 64;   // per pair: seg[dt] = first list entry of source-level distance dt
 
+// k_ppush: spans per wave, i.e. consecutive partner levels a wave reads through one buffer resource
+constexpr int PPUSH_S = 8;
+
 struct LevelDesc {
     int16_t *base;  // first element of level t (matrix 0)
     int C;          // cells per matrix in this level

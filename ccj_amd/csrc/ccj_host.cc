@@ -1708,6 +1708,13 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     c->total4 = off;
     if ((uint64_t)off != (uint64_t)NMAT4 * ccj_num_cells(n))
         return set_err(c.get(), CCJ_E_ARG, "layout size mismatch");
+    // k_ppush addresses the PK rows of PPUSH_S consecutive levels as 32-bit byte offsets from the
+    // lowest one's start (one buffer resource per wave): that span must stay below 4 GB
+    for (int t = 0; t < c->nlev; ++t) {
+        const int tt = std::min(t + PPUSH_S - 1, c->nlev - 1);
+        if (2 * (c->lv_off[tt] + (long long)c->lv_host[tt].C - c->lv_off[t]) >= (1LL << 32))
+            return set_err(c.get(), CCJ_E_ARG, "n=%d: the PK rows of %d levels exceed 4 GB (k_ppush offsets)", n, PPUSH_S);
+    }
 
     ccj_ctx *cp = c.get();
     HIPCHK(cp, hipSetDevice(c->device));

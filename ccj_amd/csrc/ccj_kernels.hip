@@ -16,6 +16,43 @@
 
 using namespace ccj;
 
+#ifdef CCJ_WG_TIMELINE
+// Measurement build only (tools/wg_timeline.py): around one armed level L, every wave of the fill's
+// kernels stamps the 100 MHz constant clock at entry and exit, with a tag (a-block and roles for the
+// level kernels) and its hardware slot (HW_ID: wave / SIMD / CU / SE bits; XCD by round robin), one
+// 32-byte entry per wave, written by lane 0 through a plain vector store.  g_tl[kind][blockIdx *
+// waves per block + wave in block]; kinds: 0 k_level4d(L), 1 k_level4d_lead(L), 2..4 k_iloop(L+1..L+3),
+// 5..6 k_ppush(L-1..L), 7 k_diag2d(L-1..L) (sigma in the tag).
+constexpr int TL_CAP = 1 << 15, TL_KINDS = 8;
+__device__ int g_tl_level = -1;
+__device__ ulonglong4 g_tl[TL_KINDS][TL_CAP];
+struct TLStamp {
+    int slot;
+    unsigned long long t0;
+    unsigned meta = 0xffffffffu;  // level-kernel grid-tail waves that return before their a-block is known
+    // kind_of(L) -> the kind of this launch when level L is armed, or -1
+    template <class K>
+    __device__ __forceinline__ explicit TLStamp(K kind_of) {
+        const int kind = kind_of(g_tl_level);
+        const int wpb = (int)(blockDim.x >> 6);
+        const int s = (int)blockIdx.x * wpb + (int)(threadIdx.x >> 6);
+        slot = (g_tl_level >= 0 && kind >= 0 && s < TL_CAP && (threadIdx.x & 63) == 0) ? kind * TL_CAP + s : -1;
+        t0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ __forceinline__ ~TLStamp() {
+        if (slot < 0) return;
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID, all 32 bits
+        (&g_tl[0][0])[slot] = make_ulonglong4(t0, t1, meta, hw | (unsigned long long)(blockIdx.x % 8) << 32);
+    }
+};
+#define TL_STAMP(expr_) TLStamp tl_stamp_([&](int L_) -> int { return (expr_); })
+#define TL_META(v_) (tl_stamp_.meta = (unsigned)(v_))
+#else
+#define TL_STAMP(expr_)
+#define TL_META(v_)
+#endif
+
 namespace {
 
 __device__ __forceinline__ int clamp_store(int v) { return v >= INTERN_INF ? INTERN_INF : v; }
@@ -193,6 +230,8 @@ __global__ __launch_bounds__(256) void k_diag2d(DevTables T, int sigma, int G, i
 #ifdef CCJ_DEBUG_BOUNDS
     g_dbg_err = T.err;
 #endif
+    TL_STAMP(sigma == L_ - 1 || sigma == L_ ? 7 : -1);
+    TL_META(sigma);
     __shared__ int red[4];
     __shared__ int sh_v, sh_p;
     const int n = T.n, rs = T.rs;
@@ -348,7 +387,8 @@ __device__ __forceinline__ unsigned long long rdl64(unsigned long long v, int l)
 // ------------------------------------------------------------------------------------------
 
 // k_ppush's operands as buffer loads: a wave reads PK at level lev and at the PP_S consecutive levels
-// o0 .. o0+ns-1, each set within a few hundred MB of its lowest level's start, so each is one buffer
+// o0 .. o0+ns-1, each set within 4 GB of its lowest level's start (ccj_create checks it; ~300 MB at
+// n=200, above 2 GB from n ~ 470, hence unsigned offsets), so each is one buffer
 // (base = that level's start) and an operand is (uniform byte offset, lane byte offset) = (soffset,
 // voffset): no 64-bit address per load (as row pointers the compiler ran out of SGPRs and formed a
 // 64-bit VGPR address for most of them)
@@ -380,6 +420,8 @@ constexpr int PP_OFF = 1 << 30;
 template <int PP_S, int PP_U>
 __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, int npairs, int hs_len, int blocksA, int G,
                                                int rank, int nout) {
+    TL_STAMP(lev == L_ - 1 ? 5 : lev == L_ ? 6 : -1);
+    TL_META(lev);
     const int n = T.n, rs = T.rs;
     const int lane = threadIdx.x & 63;
     const int partB = (int)blockIdx.x >= blocksA;
@@ -435,7 +477,8 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
         for (int s = 0; s < PP_S; ++s) {
             const int t2 = imin(o0 + s, o0 + ns - 1);
             Ms2[s] = __builtin_amdgcn_readfirstlane(2 * LD[t2].M);  // uniform: a per-lane soffset would be a waterfall loop
-            voB[s] = (int)(2 * (LD[t2].lb - lbo + Grow(n - t2 - 2, b1))) + 2 * (imin(i, n - (lev + 3 + t2)) + jo);
+            // unsigned: below 4 GB by ccj_create's k_ppush span check, possibly above 2 GB (n >~ 470)
+            voB[s] = (int)((unsigned)(2 * (LD[t2].lb - lbo + Grow(n - t2 - 2, b1))) + 2u * (unsigned)(imin(i, n - (lev + 3 + t2)) + jo));
         }
         // PP_U steps per iteration, all PP_U * (PP_S + 1) loads in flight together (the steps of a
         // short tail re-read the last one and are masked)
@@ -487,7 +530,7 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
         for (int s = 0; s < PP_S; ++s) {
             const int t1 = imin(o0 + s, o0 + ns - 1);
             Ms2[s] = __builtin_amdgcn_readfirstlane(2 * LD[t1].M);
-            voA[s] = (int)(2 * (LD[t1].lb - lbo + Grow(n - t1 - 2, a2))) + 2 * (imax(1, lc - (lev + 3 + t1)) - 1);
+            voA[s] = (int)((unsigned)(2 * (LD[t1].lb - lbo + Grow(n - t1 - 2, a2))) + 2u * (unsigned)(imax(1, lc - (lev + 3 + t1)) - 1));
         }
         for (int h2 = hmax; h2 >= h_lo; h2 -= PP_U) {  // PP_U steps per iteration, as in part A
             int vb[PP_U], va[PP_U][PP_S], hh[PP_U];
@@ -939,6 +982,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t il_src(const int16_t *base) {
 // its cells (ccj_items.h, built by k_items in enumeration order)
 constexpr int IL_WPB = 4;  // waves (consecutive items) per k_iloop workgroup (1, 2, 8, 16 measured +3.6 ... +9 ms)
 __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long long first, int nitems, int G_SH, int rank) {
+    TL_STAMP(t >= L_ + 1 && t <= L_ + 3 ? 2 + t - L_ - 1 : -1);
+    TL_META(t);
     const int n = T.n, rs = T.rs, m = n - t - 2;
     const int lane = threadIdx.x & 63;
     const int w = (int)blockIdx.x * IL_WPB + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1151,6 +1196,7 @@ __device__ __forceinline__ void pipe_scan_lead(int s, int step, int last, int ml
     }
 }
 
+
 // ------------------------------------------------------------------------------------------
 // 4-D level t: one lane per cell (i,j,k,l); all lanes of a wave share (t, a) so every loop bound
 // is wave-uniform.  pseudo_loop.cc:181-644, 663-808.
@@ -1173,6 +1219,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #ifdef CCJ_DEBUG_BOUNDS
     g_dbg_err = T.err;
 #endif
+    TL_STAMP(t == L_ ? (LEAD ? 1 : 0) : -1);
     // split > 1 (late, narrow levels): the split waves of one 64-cell chunk share the a/b loops
     // (step s = part + 1, part + 1 + split, ...) and min-reduce their partial results through LDS.
     extern __shared__ int red[];  // [chunk][part-1][22][64], split > 1 only
@@ -1254,7 +1301,9 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     // On sharing levels every wave with a long scan (a leader, or a full scan on either side) runs
     // in its own launch (k_level4d_lead: more registers, scans split over several waves); the plain
     // kernel keeps the cells that only follow (short scans, full occupancy).
+    TL_META((unsigned)a | (unsigned)part << 10 | (unsigned)arole << 13 | (unsigned)brole << 15 | 1u << 20);
     if (grp && LEAD != (arole != 2 || brole != 2)) return;
+    TL_META((unsigned)a | (unsigned)part << 10 | (unsigned)arole << 13 | (unsigned)brole << 15);
     // last split step this cell scans itself
     const int a_stop = arole == 2 ? ra : a;
     const int b_stop = brole == 2 ? rb : b;
@@ -1953,7 +2002,7 @@ extern "C" int ccjk_ppush(const DevTables *T, int lev, int G, int rank, void *st
     const int ngrp = (n - lev - 3 + 63) / 64;
     // spans per wave = partners per reused level-T load (8; 4 and 16 measured slower) and the
     // inner-loop slice per wave (32; 16 and 64 measured the same)
-    constexpr int S = 8, hs_len = 32;
+    constexpr int S = PPUSH_S, hs_len = 32;
     const int nch = (nmax + S - 1) / S;
     int npairs = 0;  // (chunk, inner-loop slice) pairs, as k_ppush enumerates them
     for (int c = 0; c < nch; ++c) npairs += (imin((c + 1) * S, nmax) + hs_len - 1) / hs_len;
@@ -2211,3 +2260,19 @@ extern "C" int ccjk_level4d_lead(const DevTables *T, int t, int G, int rank, voi
                        sp, G, rank, nblk, 1);
     return (int)hipGetLastError();
 }
+
+#ifdef CCJ_WG_TIMELINE
+// measurement build only (tools/wg_timeline.py): arm level t (clears the stamps), read them back
+extern "C" int ccjk_tl_arm(int t) {
+    static ulonglong4 zero[TL_CAP];
+    for (int k = 0; k < TL_KINDS; ++k)
+        if (hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_tl), zero, sizeof(zero), (size_t)k * sizeof(zero))) return (int)e;
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_tl_level), &t, sizeof(int));
+}
+extern "C" int ccjk_tl_read(int kind, void *out, int cap) {
+    if (kind < 0 || kind >= TL_KINDS || cap > TL_CAP) return -1;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tl), (size_t)cap * sizeof(ulonglong4), (size_t)kind * TL_CAP * sizeof(ulonglong4));
+}
+extern "C" int ccjk_tl_cap() { return TL_CAP; }
+extern "C" int ccjk_tl_kinds() { return TL_KINDS; }
+#endif

@@ -217,8 +217,7 @@ struct ccj_pf_ctx {
 };
 
 // The allocations of ccj_pf_create for a sequence of length n, in bytes: device (every hipMalloc
-// of create_impl; the work items, sequence-dependent, are bounded by one 64-lane chunk per PL/PR/PM
-// row) and host (the two get_e_intP window tables, built before they are uploaded).
+// of create_impl; the work items, sequence-dependent, by their count when every pair can pair) and host (the two get_e_intP window tables, built before they are uploaded).
 extern "C" void ccj_pf_footprint(int n, unsigned long long *device_bytes, unsigned long long *host_bytes) {
     if (n < 1) n = 1;
     const unsigned long long rs = (unsigned long long)n + 2, plane = (unsigned long long)(n + 1) * rs;
@@ -230,7 +229,16 @@ extern "C" void ccj_pf_footprint(int n, unsigned long long *device_bytes, unsign
         cx += 2 * C;
         pmx += m * (unsigned long long)n * (t + 1);
         maxC = std::max(maxC, C);
-        rows += (unsigned long long)(t + 1) * m * 3 + m * (unsigned long long)n;  // item bound (rows x chunks)
+        // work items: create_impl's enumeration with every pair able to pair (its upper bound), one item
+        // per 64-lane chunk of each PL / PR / PM row
+        const int mi = (int)m;
+        for (int i = 1; i <= mi; ++i) rows += (unsigned long long)std::max(0, t - 5) * ((mi - i) / 64 + 1);  // PL, a in [6, t]
+        for (int q = 0; q < mi; ++q) rows += (unsigned long long)std::max(0, t - 5) * (q / 64 + 1);         // PR, a in [0, t-6]
+        for (int h = 0; h <= mi - 1; ++h)                                                                   // PM
+            for (int j = 1; j + h + 2 <= n; ++j) {
+                const int k = j + h + 2, alo = std::max(2, t - (n - k)), ahi = std::min(t - 2, j - 1);
+                if (alo <= ahi) rows += (unsigned long long)((ahi - alo) / 64 + 1);
+            }
     }
     unsigned long long dev = ie + (d4 + cx + pmx) * sizeof(int) + 2ull * 3 * maxC * sizeof(double);
     dev += (unsigned long long)CCJ_PF_NMAT2 * plane * sizeof(double) + 2 * plane * sizeof(long long);  // 2-D, Pacc, Pabs

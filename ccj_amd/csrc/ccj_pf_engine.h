@@ -5,8 +5,12 @@
 //   elem(x,t,a,h,i) = lb_t + x*C_t + a*M_t + h*m_t - h(h-1)/2 + (i-1),  m_t = n-t-2,
 //   M_t = m_t(m_t+1)/2, C_t = (t+1) M_t.
 // 2-D matrices: doubles, span-major [w][p] with row stride rs = n+2.
-// Interior-loop weights get_e_intP (part_func.cc:886-891), u1, u2 < PF_IEW, in two layouts whose
-// 29 x 29 window of one pair is contiguous (k_pf_iloop reads a window row with one load):
+// Interior-loop weights get_e_intP (part_func.cc:886-891), u1, u2 < PF_IEW, in two tables whose
+// window rows (one pair, one u1) are compacted to the set bits of the pair's mask row (mO / mI, bit u2
+// set = the weight is nonzero): the k-th set bit of mask row (pair, u1) -> slot k of that row (rows keep
+// their PF_IEW-double stride, zero past the last set bit), PF_ILW doubles of zero tail padding after
+// the last row (k_pf_iloop reads a round
+// of PF_ILW slots with one scalar load).  The un-compacted window is:
 //   ieO[w][p][u1][u2]: the loop closed by (p, p+w) around (p+1+u1, p+w-1-u2)   (PL, PR)
 //   ieI[g][j][u1][u2]: the loop closed by (j-1-u1, j+g+1+u2) around (j, j+g)    (PM)
 #pragma once
@@ -33,6 +37,7 @@ constexpr int PF_IEW = MAXLOOP - 1;  // interior-loop window per side: u <= 28
 #endif
 constexpr int PF_ILW = CCJ_PF_ILW;   // k_pf_iloop: window terms per round (multiple of 4); the compacted
                                      // weight rows carry PF_ILW doubles of tail padding
+static_assert(PF_ILW % 4 == 0 && PF_ILW >= 4, "CCJ_PF_ILW: window_row reads whole groups of 4 terms");
 
 struct PfLvl {
     long long lb;  // element offset of level t

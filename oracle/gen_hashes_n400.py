@@ -60,6 +60,13 @@ def main():
                     "mfe": L.ccj_oracle_W(h, n), "oracle_seconds": t1 - t0, "threads": nthr})
         L.ccj_oracle_free(h)
         print(tag, "done in %.0f s, mfe %d" % (t1 - t0, out[-1]["mfe"]), flush=True)
+        # Merge with the file as it is now: other fields (e.g. the traceback outcome) may have been
+        # added to the other cases while this fold ran.
+        if os.path.exists(out_path):
+            with open(out_path) as f:
+                disk = {c["tag"]: c for c in json.load(f)}
+            mine = {c["tag"] for c in out if c["tag"] in want}
+            out = [c for c in out if c["tag"] in mine] + [c for t, c in disk.items() if t not in mine]
         out.sort(key=lambda c: c["seed"])
         with open(out_path, "w") as f:
             json.dump(out, f, indent=1)

@@ -124,3 +124,36 @@ def test_pf_footprint_counts_the_large_allocations():
         assert host.value == ie
         assert dev.value >= ie + (21 + 2) * cells * 4
         assert dev.value <= 1.3 * (ie + (21 + 2) * cells * 4) + (64 << 20)
+
+
+def _pf_items_upper(n):
+    """k_pf_iloop work items of ccj_pf_create's enumeration (ccj_pf.cc, ccj_items.h item_row) when every
+    pair can pair: one item per 64-lane chunk of each PL / PR / PM row."""
+    tot = 0
+    for t in range(n - 2):
+        m = n - t - 2
+        tot += max(0, t - 5) * sum((m - i) // 64 + 1 for i in range(1, m + 1))   # PL: a in [6, t]
+        tot += max(0, t - 5) * sum(q // 64 + 1 for q in range(m))                # PR: a in [0, t-6]
+        for h in range(m):                                                        # PM
+            for j in range(1, n - h - 1):
+                k = j + h + 2
+                lo, hi = max(2, t - (n - k)), min(t - 2, j - 1)
+                if lo <= hi:
+                    tot += (hi - lo) // 64 + 1
+    return tot
+
+
+def test_pf_footprint_bounds_the_work_items():
+    """rows longer than 64 cells (n=200) hold several items; the footprint must cover the
+    items' exact upper bound on top of the 4-D store, its copies and the window tables."""
+    import ctypes
+    L = ctypes.CDLL(LIB)
+    L.ccj_pf_footprint.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]
+    L.ccj_pf_footprint.restype = None
+    n = 200
+    dev, host = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+    L.ccj_pf_footprint(n, ctypes.byref(dev), ctypes.byref(host))
+    cells = sum((t + 1) * (n - t - 2) * (n - t - 1) // 2 for t in range(n - 2))
+    pmx = sum((n - t - 2) * n * (t + 1) for t in range(n - 2))
+    items = _pf_items_upper(n)
+    assert dev.value >= host.value + (21 + 2) * cells * 4 + pmx * 4 + items * 4
