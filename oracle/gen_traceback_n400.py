@@ -37,17 +37,17 @@ def main():
         wf = W_final(case["seq"], case["dangles"], params=case["params"], noGU=bool(case["noGU"]), host_traceback=True)
         try:
             wf.fill()
+            rec = {"seed": case["seed"], "tag": case["tag"],
+                   "source": "ccj_host.cc host restatement of the reference backtrack over matrices equal to hashes_n400.json"}
+            try:
+                e = wf.result()  # W (host mode: computed here) and the traceback
+                rec.update(structure=wf.structure, energy=e, stdout_msgs=wf.stdout_msgs)
+            except BacktrackExit as ex:
+                rec["exit"] = {"code": ex.exit_code, "msg": ex.msg, "stdout_msgs": ex.stdout}
             got = wf.hashes()
             bad = [k for k in case["hashes"] if got[k] != case["hashes"][k]]
             if bad or wf.W(case["n"]) != case["mfe"]:
                 raise SystemExit(f"seed {case['seed']}: matrices differ from hashes_n400.json ({bad}); nothing recorded")
-            rec = {"seed": case["seed"], "tag": case["tag"],
-                   "source": "ccj_host.cc host restatement of the reference backtrack over matrices equal to hashes_n400.json"}
-            try:
-                e = wf.result()
-                rec.update(structure=wf.structure, energy=e, stdout_msgs=wf.stdout_msgs)
-            except BacktrackExit as ex:
-                rec["exit"] = {"code": ex.exit_code, "msg": ex.msg, "stdout_msgs": ex.stdout}
         finally:
             wf.close()
         done[case["seed"]] = rec
