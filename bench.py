@@ -479,7 +479,7 @@ def main(argv=None):
     wf.set_timing(2)
     wf.ccj()
     tmi = wf.timing()
-    il_ms, diag_ms = tmi["iloop_ms"], tmi["diag2d_ms"]
+    il_ms, diag_ms, pp_ms = tmi["iloop_ms"], tmi["diag2d_ms"], tmi["ppush_ms"]
     elapsed = max_over_ranks(elapsed, dist)
 
     wm = (ctypes.c_double * 4)()
@@ -503,6 +503,8 @@ def main(argv=None):
     il_kernel = "k_iloop"
     il_traffic = None
     tj, tname = find_traffic(a.n, a.seed, a.params) if world == 1 or not shard else (None, None)
+    side_traffic = {}  # kernel -> (counter bytes per launch, launches per fold)
+    fill_counter_bytes = None
     if tj:
         tk = tj["kernels"].get("k_level4d_level")
         if tk:
@@ -511,6 +513,13 @@ def main(argv=None):
         ti = tj["kernels"].get(il_kernel)
         if ti:
             il_traffic = ti["hbm_bytes_per_launch"]
+        if tk:
+            folds = tk["launches"] / nlaunch  # the profiled command's folds
+            for kn, kv in tj["kernels"].items():
+                if kn in ("k_level4d", "k_level4d_lead"):
+                    continue  # inside k_level4d_level
+                side_traffic[kn.split("<")[0]] = (kv["hbm_bytes_per_launch"], kv["launches"] / folds)
+            fill_counter_bytes = sum(b * l for b, l in side_traffic.values())
 
     if rank != 0:
         if dist is not None:
@@ -556,6 +565,7 @@ def main(argv=None):
         "breakdown_ms": {"setup_reset": reset_s / a.steps * 1e3, "fill_device": fill_ms / a.steps,
                          "level4d_levels": level_ms / a.steps,
                          "iloop_kernels_instrumented_fold": il_ms, "diag2d_kernels_instrumented_fold": diag_ms,
+                         "ppush_kernels_instrumented_fold": pp_ms,
                          "fill_instrumented_fold": tmi["fill_ms"]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
@@ -577,6 +587,31 @@ def main(argv=None):
                            "algorithmic_bytes_per_fold": bytes_il, "traffic": il_traffic, "traffic_unit": "bytes/launch",
                            "frac_counter": (il_traffic / il_launch_s / 1e9 / HBM_PEAK_GBS) if il_traffic and il_launch_s > 0 else None},
     }
+    # the side kernels in the fill (instrumented fold: marker events around every launch, so these
+    # are in-fill durations with the level chain beside them, not standalone figures)
+    pp_n = side_traffic.get("k_ppush", (None, max(a.n - 3, 1)))[1]
+    pp_launch_s = pp_ms / 1e3 / pp_n if pp_ms else 0.0
+    pp_tr = side_traffic.get("k_ppush", (None, 0))[0]
+    out["roofline_ppush"] = {
+        "bound": "hbm", "kernel": "k_ppush (P terms pushed by level; one instrumented fold after the timed region)",
+        "launches_per_fold": pp_n, "avg_launch_us": pp_launch_s * 1e6, "algorithmic_bytes_per_fold": wm[1],
+        "achieved": (wm[1] / pp_n) / pp_launch_s / 1e9 if pp_launch_s > 0 else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": (wm[1] / pp_n) / pp_launch_s / 1e9 / HBM_PEAK_GBS if pp_launch_s > 0 else None,
+        "traffic": pp_tr, "traffic_unit": "bytes/launch",
+        "frac_counter": pp_tr / pp_launch_s / 1e9 / HBM_PEAK_GBS if pp_tr and pp_launch_s > 0 else None}
+    dg_n = side_traffic.get("k_diag2d", (None, a.n))[1]
+    dg_launch_s = diag_ms / 1e3 / dg_n if diag_ms else 0.0
+    dg_tr = side_traffic.get("k_diag2d", (None, 0))[0]
+    out["roofline_diag2d"] = {
+        "bound": "latency", "kernel": "k_diag2d (2-D spans, cache-resident; one instrumented fold)",
+        "launches_per_fold": dg_n, "avg_launch_us": dg_launch_s * 1e6, "traffic": dg_tr, "traffic_unit": "bytes/launch",
+        "frac_counter": dg_tr / dg_launch_s / 1e9 / HBM_PEAK_GBS if dg_tr and dg_launch_s > 0 else None}
+    if fill_counter_bytes is not None and traffic:
+        fb = fill_counter_bytes + traffic * nlaunch
+        out["fill_counter"] = {"hbm_bytes_per_fold": fb, "fill_ms": fill_ms / a.steps,
+                               "gbs": fb / (fill_ms / a.steps / 1e3) / 1e9,
+                               "frac": fb / (fill_ms / a.steps / 1e3) / 1e9 / HBM_PEAK_GBS,
+                               "source": traffic_src}
     # the algorithmic model charges every operand read (split-sharing and the caches serve many of
     # them); when its bytes per fold exceed what HBM could move in the fold's time it is an
     # effective-bandwidth figure, not an HBM fraction: say so on the line

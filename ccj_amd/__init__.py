@@ -134,6 +134,8 @@ def lib() -> ctypes.CDLL:
     L.ccj_host_timing.restype = ip
     L.ccj_iloop_ms.argtypes = [vp]
     L.ccj_iloop_ms.restype = ctypes.c_double
+    L.ccj_ppush_ms.argtypes = [vp]
+    L.ccj_ppush_ms.restype = ctypes.c_double
     L.ccj_set_timing.argtypes = [vp, ip]
     L.ccj_set_timing.restype = ip
     L.ccj_comm_unique_id.argtypes = [cp]
@@ -419,7 +421,9 @@ class W_final:
         lib().ccj_last_timing(self._h, ctypes.byref(f), k)
         hst = (ctypes.c_double * 3)()
         lib().ccj_host_timing(self._h, hst)
-        return {"fill_ms": f.value, "level4d_ms": k[0], "iloop_ms": lib().ccj_iloop_ms(self._h), "diag2d_ms": k[1],
+        L = lib()
+        return {"fill_ms": f.value, "level4d_ms": k[0], "iloop_ms": L.ccj_iloop_ms(self._h), "diag2d_ms": k[1],
+                "ppush_ms": L.ccj_ppush_ms(self._h),
                 "precompute_ms": k[2],
                 "host_mirror_wait_ms": hst[0], "W_ms": hst[1], "backtrack_ms": hst[2]}
 

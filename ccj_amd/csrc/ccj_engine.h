@@ -114,30 +114,54 @@ __host__ __device__ __forceinline__ int shard_ceil(int x, int G, int r) {
     return (q / G) * SHARD_GRP + off;
 }
 
-// The level-t exchange slice of a band-sharded fill, in int16 elements: the body
-// [matrix x][own index o][cell c] of nmax blocks per matrix (nmax = the largest rank's block count at
-// t, so every rank's slice has the same size and ONE all-gather moves a level), padded to 8 bytes,
-// then the P tail (XCH_PTAIL: (value, first split) uint64 per interval start 0..n) and the span tail
-// (XCH_DTAIL: XCH_DT_N int32 planes of n+1 entries).  k_pack / k_unpack / k_?tail_* and the host's
-// buffer sizing use these, and ccj_exchange_layout / ccj_exchange_index export them (tests).
+// The band-sharded exchange of level t has two parts, each ONE all-gather of equal
+// slices:
+//   part XCH_EDGE: the rank's blocks with a % SHARD_GRP == SHARD_GRP-1 (own index o % SHARD_GRP ==
+//     SHARD_GRP-1): of level t, another rank's level t+1 reads only these (its group's first block a
+//     reads block a-1 at split step 1, pseudo_loop.cc:357-362), plus the span tail (XCH_DTAIL: span t,
+//     which level t+1 reads).  Gathered on the level stream: the critical path.
+//   part XCH_BULK: the rank's other blocks (read from level t+2 on, and by k_iloop(t+3) / k_ppush(t)),
+//     plus the P tail (XCH_PTAIL: this rank's partials of P(t+2)).  Gathered on a side stream while
+//     level t+1 runs.
+// A part's slice: body [matrix x][part index k][cell c] of nmax blocks per matrix (nmax = the largest
+// rank's block count of that part at t), padded to 8 bytes, then the part's tail.  k_pack / k_unpack /
+// k_?tail_* and the host's buffer sizing use these; ccj_exchange_layout / ccj_exchange_index export
+// them (tests).
+constexpr int XCH_EDGE = 0, XCH_BULK = 1;
 constexpr int XCH_DT_N = 10;  // span tail planes: V, Vt, P, WBP, WB, WPP, WP, WMv, WMp, WM
 __host__ __device__ __forceinline__ long long xch_body(int nmax, int M) { return ((long long)22 * nmax * M + 3) & ~3LL; }
 __host__ __device__ __forceinline__ long long xch_ptail(int n) { return 4LL * (n + 1); }
 __host__ __device__ __forceinline__ long long xch_dtail(int n) { return 2LL * XCH_DT_N * (n + 1); }
-__host__ __device__ __forceinline__ long long xch_slice(int n, int nmax, int M) { return xch_body(nmax, M) + xch_ptail(n) + xch_dtail(n); }
-// body position of matrix x, own block o, cell c
-__host__ __device__ __forceinline__ long long xch_pos(int x, int o, int c, int nmax, int M) {
-    return ((long long)x * nmax + o) * M + c;
+__host__ __device__ __forceinline__ long long xch_tail(int n, int part) { return part == XCH_EDGE ? xch_dtail(n) : xch_ptail(n); }
+__host__ __device__ __forceinline__ long long xch_slice(int n, int nmax, int M, int part) { return xch_body(nmax, M) + xch_tail(n, part); }
+// part of own index o, its index inside the part, and back
+__host__ __device__ __forceinline__ int xch_part(int o) { return o % SHARD_GRP == SHARD_GRP - 1 ? XCH_EDGE : XCH_BULK; }
+__host__ __device__ __forceinline__ int xch_pidx(int o) {
+    return xch_part(o) == XCH_EDGE ? o / SHARD_GRP : (o / SHARD_GRP) * (SHARD_GRP - 1) + o % SHARD_GRP;
 }
-// where block a's cells arrive: its owner's slice, at the owner's own index of a
-__host__ __device__ __forceinline__ void xch_src(int a, int G, int &owner, int &o) {
+__host__ __device__ __forceinline__ int xch_own(int k, int part) {
+    return part == XCH_EDGE ? k * SHARD_GRP + SHARD_GRP - 1 : (k / (SHARD_GRP - 1)) * SHARD_GRP + k % (SHARD_GRP - 1);
+}
+// rank r's blocks of the part at level t (own indices 0 .. shard_count(t)-1)
+__host__ __device__ __forceinline__ int xch_pcount(int t, int G, int r, int part) {
+    const int own = shard_count(t, G, r);
+    return part == XCH_EDGE ? own / SHARD_GRP : own - own / SHARD_GRP;
+}
+// body position of matrix x, part index k, cell c
+__host__ __device__ __forceinline__ long long xch_pos(int x, int k, int c, int nmax, int M) {
+    return ((long long)x * nmax + k) * M + c;
+}
+// where block a's cells arrive: its owner's slice of the block's part, at the block's part index
+__host__ __device__ __forceinline__ void xch_src(int a, int G, int &owner, int &part, int &k) {
     owner = shard_owner(a, G);
-    o = shard_count(a - 1, G, owner);
+    const int o = shard_count(a - 1, G, owner);
+    part = xch_part(o);
+    k = xch_pidx(o);
 }
-// the largest rank's block count at level t
-__host__ __device__ __forceinline__ int xch_nmax(int t, int G) {
+// the largest rank's block count of the part at level t
+__host__ __device__ __forceinline__ int xch_nmax(int t, int G, int part) {
     int nm = 0;
-    for (int r = 0; r < G; ++r) nm = shard_count(t, G, r) > nm ? shard_count(t, G, r) : nm;
+    for (int r = 0; r < G; ++r) nm = xch_pcount(t, G, r, part) > nm ? xch_pcount(t, G, r, part) : nm;
     return nm;
 }
 
@@ -245,8 +269,8 @@ int ccjk_dtail_unpack(const ccj::DevTables *T, int sigma, const int16_t *recv, s
 int ccjk_level4d(const ccj::DevTables *T, int t, int G, int rank, int copies, void *stream);
 int ccjk_level_split(int n, int t, int nblk, int split_target);
 int ccjk_level4d_lead(const ccj::DevTables *T, int t, int G, int rank, void *stream);
-int ccjk_pack(const ccj::DevTables *T, int t, int G, int r, int nmax, int16_t *send, void *stream);
-int ccjk_unpack(const ccj::DevTables *T, int t, int G, int r, int nmax, const int16_t *recv, size_t rstride, void *stream);
+int ccjk_pack(const ccj::DevTables *T, int t, int G, int r, int part, int nmax, int16_t *send, void *stream);
+int ccjk_unpack(const ccj::DevTables *T, int t, int G, int r, int part, int nmax, const int16_t *recv, size_t rstride, void *stream);
 int ccjk_pterm(const ccj::DevTables *T, int sigma, void *stream);
 int ccjk_ppush(const ccj::DevTables *T, int lev, int G, int rank, void *stream);
 int ccjk_ptail_pack(const ccj::DevTables *T, int sigma, int16_t *tail, void *stream);

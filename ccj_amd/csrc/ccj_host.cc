@@ -87,6 +87,10 @@ struct ccj_group {
     }
 };
 
+// timing events per level (timing mode 2): [0,1] k_diag2d, [2,3] k_iloop, [4,5] the level, [6] the
+// edge exchange's start (band-sharded), [7,8] k_ppush, [9,10] the bulk exchange (band-sharded, st_x)
+constexpr int TEV_PER = 11;
+
 struct ccj_ctx {
     // problem
     int n = 0;
@@ -112,7 +116,8 @@ struct ccj_ctx {
     // kernel family launch (k_diag2d, k_iloop, the level span).  The markers of mode 2 are barrier
     // packets on the streams and cost ~3 ms per n=200 fill, so the default is 1.
     int level_timing = 1;
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;    // the edge all-gathers (level stream)
+    ncclComm_t comm_b = nullptr;  // the bulk all-gathers (st_x), split from comm: one communicator per stream
 
     // layout
     std::vector<LevelDesc> lv_host;     // device pointers
@@ -145,8 +150,9 @@ struct ccj_ctx {
     int16_t *d_dummy = nullptr;
     uint32_t *d_items = nullptr;          // k_iloop work items, all levels back to back
     size_t items_cap = 0;
-    int16_t *d_send = nullptr, *d_recv = nullptr;  // band-sharded exchange: own slice, world slices
-    std::vector<int> xnmax;               // per level: the largest rank's block count (slice = 22 x nmax x M)
+    // band-sharded exchange, per part (XCH_EDGE, XCH_BULK): own slice, world slices
+    int16_t *d_send[2] = {nullptr, nullptr}, *d_recv[2] = {nullptr, nullptr};
+    std::vector<int> xnmax[2];            // per level: the largest rank's block count of the part (slice = 22 x nmax x M + tail)
     ccj_group *lgroup = nullptr;          // in-process exchange between contexts (tests), else RCCL
     long long *d_icount = nullptr, *d_ioff = nullptr;  // k_items: items per (t, r), first item
     long long *h_ioff = nullptr;          // pinned staging of it_off
@@ -164,13 +170,15 @@ struct ccj_ctx {
     std::vector<unsigned long long> h_pk;
     int8_t *d_vt = nullptr;
     hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr, st_il = nullptr, st_d = nullptr;
+    hipStream_t st_x = nullptr;          // band-sharded: the bulk part of each level's exchange
+    std::vector<hipEvent_t> bulk_done;   // band-sharded: level t complete on this rank (bulk part unpacked)
     bool join_diag = true;               // k_diag2d(t-1) after k_iloop(t) on st_il (one cross-stream wait per level)
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<hipEvent_t> pp_done; // band-sharded: this rank's P-term push of span sigma done (before the exchange)
-    std::vector<double> lev_ms_v, diag_ms_v, il_ms_v, xch_ms_v;
+    std::vector<double> lev_ms_v, diag_ms_v, il_ms_v, xch_ms_v, xbulk_ms_v, pp_ms_v;
     std::vector<hipEvent_t> il_done, dg_done;  // k_iloop(t) / k_diag2d(sigma) finished
     std::vector<hipEvent_t> lev_done;
-    std::vector<hipEvent_t> tev;  // timing events: 2 per k_level4d, k_iloop and k_diag2d launch
+    std::vector<hipEvent_t> tev;  // timing events (TEV_PER per level): 2 per k_level4d, k_iloop, k_diag2d and k_ppush launch
     hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_pre = nullptr;
     DevTables T{};
 
@@ -188,7 +196,7 @@ struct ccj_ctx {
     BtOut *hr_bo = nullptr;
     std::vector<int> W;
 
-    double fill_ms = 0, level_ms = 0, diag_ms = 0, pre_ms = 0, il_ms = 0;
+    double fill_ms = 0, level_ms = 0, diag_ms = 0, pre_ms = 0, il_ms = 0, pp_ms = 0;
     double sync_ms = 0, w_ms = 0, bt_ms = 0;  // host side of the last fold
     int bt_steps = 0;
     std::string err;
@@ -1416,12 +1424,12 @@ extern "C" uint64_t ccj_num_cells(int n) {
 static thread_local std::string g_create_err;
 
 
-// The exchange of one level through the in-process group: every member pulls each member's
-// packed slice into its own receive buffer (same device), between two barriers, so no slice is
-// overwritten by the next level's pack before every member has read it.
-static int local_allgather(ccj_ctx *c, size_t slice) {
+// One part of a level's exchange through the in-process group: every member pulls each member's
+// packed slice of the part into its own receive buffer (same device) on stream q, between two
+// barriers, so no slice is overwritten by the part's next pack before every member has read it.
+static int local_allgather(ccj_ctx *c, int part, size_t slice, hipStream_t q) {
     ccj_group *g = c->lgroup;
-    HIPCHK(c, hipStreamSynchronize(c->st));  // own slice packed
+    HIPCHK(c, hipStreamSynchronize(q));  // own slice packed
     if (!g->barrier()) return set_err(c, CCJ_E_STATE, "local exchange: a group member failed");
     // take the peers' send buffers under the lock and hold the group busy until the copies are
     // done: ccj_destroy of a peer waits for busy == 0 before it frees anything
@@ -1434,14 +1442,14 @@ static int local_allgather(ccj_ctx *c, size_t slice) {
                 g->cv.notify_all();
                 return set_err(c, CCJ_E_STATE, "local exchange: rank %d has no context", r);
             }
-            src[r] = g->members[r]->d_send;
+            src[r] = g->members[r]->d_send[part];
         }
         ++g->busy;
     }
     hipError_t e = hipSuccess;
     for (int r = 0; r < g->world && e == hipSuccess; ++r)
-        e = hipMemcpyAsync(c->d_recv + (size_t)r * slice, src[r], slice * sizeof(int16_t), hipMemcpyDeviceToDevice, c->st);
-    const hipError_t e2 = hipStreamSynchronize(c->st);
+        e = hipMemcpyAsync(c->d_recv[part] + (size_t)r * slice, src[r], slice * sizeof(int16_t), hipMemcpyDeviceToDevice, q);
+    const hipError_t e2 = hipStreamSynchronize(q);
     {
         std::lock_guard<std::mutex> lk(g->mu);
         --g->busy;
@@ -1723,6 +1731,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_p, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_il, hipStreamNonBlocking));
     HIPCHK(cp, hipStreamCreateWithFlags(&c->st_d, hipStreamNonBlocking));
+    HIPCHK(cp, hipStreamCreateWithFlags(&c->st_x, hipStreamNonBlocking));
     // The cross-stream events only order work on this device, so they are recorded without the
     // default system-scope fence (hipEventDisableSystemFence: fill -0.65 ms at n=200).
     // ev_start / ev_end, which the host waits on, keep it.
@@ -1742,7 +1751,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     for (auto &e : c->p_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
     c->pp_done.resize(n + 1);
     for (auto &e : c->pp_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
-    c->tev.resize(7 * (size_t)n + 7);
+    c->bulk_done.resize(n + 1);
+    for (auto &e : c->bulk_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
+    c->tev.resize(TEV_PER * (size_t)n + TEV_PER);
     for (auto &e : c->tev) HIPCHK(cp, hipEventCreate(&e));
 
     const size_t plane = (size_t)(n + 1) * c->rs;
@@ -1980,18 +1991,21 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         HIPCHK(cp, hipMalloc(&c->d_icount, (size_t)n * G * KI_SPLIT * sizeof(long long)));
         HIPCHK(cp, hipMalloc(&c->d_ioff, (size_t)n * G * KI_SPLIT * sizeof(long long)));
         if (G > 1 && !c->simulate) {
-            // exchange slices: per level, 22 matrices x the largest rank's blocks x M
-            c->xnmax.assign(n, 0);
-            size_t slice = 0;
-            for (int t = 0; t < c->nlev; ++t) {
-                const int nm = xch_nmax(t, G);
-                c->xnmax[t] = nm;
-                slice = std::max(slice, (size_t)xch_slice(n, nm, c->lv_host[t].M));
+            // exchange slices, per part: 22 matrices x the largest rank's blocks of the
+            // part x M, then the part's tail
+            for (int part = 0; part < 2; ++part) {
+                c->xnmax[part].assign(n, 0);
+                size_t slice = 0;
+                for (int t = 0; t < c->nlev; ++t) {
+                    const int nm = xch_nmax(t, G, part);
+                    c->xnmax[part][t] = nm;
+                    slice = std::max(slice, (size_t)xch_slice(n, nm, c->lv_host[t].M, part));
+                }
+                if (hipMalloc(&c->d_send[part], std::max<size_t>(slice, 1) * sizeof(int16_t)) != hipSuccess ||
+                    hipMalloc(&c->d_recv[part], std::max<size_t>(slice * G, 1) * sizeof(int16_t)) != hipSuccess)
+                    return set_err(cp, CCJ_E_OOM, "device allocation of the exchange buffers (%.2f GB) failed",
+                                   slice * (G + 1) * 2e-9);
             }
-            if (hipMalloc(&c->d_send, std::max<size_t>(slice, 1) * sizeof(int16_t)) != hipSuccess ||
-                hipMalloc(&c->d_recv, std::max<size_t>(slice * G, 1) * sizeof(int16_t)) != hipSuccess)
-                return set_err(cp, CCJ_E_OOM, "device allocation of the exchange buffers (%.2f GB) failed",
-                               slice * (G + 1) * 2e-9);
         }
     }
     if (const int rc = seq_setup(cp)) return rc;
@@ -2076,17 +2090,93 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     HIPCHK(c, hipStreamWaitEvent(c->st_d, c->ev_pre, 0));
     HIPCHK(c, hipStreamWaitEvent(c->st_il, c->ev_pre, 0));
     HIPCHK(c, hipStreamWaitEvent(c->st_p, c->ev_pre, 0));
+    const bool xchg = c->world > 1 && !c->simulate;
+    // level t complete on this rank: its lev_done, or, band-sharded, when the bulk part of its
+    // exchange is unpacked (bulk_done[t]; lev_done[t] then only covers the rank's own cells and the
+    // other ranks' edge blocks, which is all level t+1 reads of level t)
+    const std::vector<hipEvent_t> &lvl_full = xchg ? c->bulk_done : c->lev_done;
+    // what follows a level's completion on this rank: P terms pushed by it, the host-mirror copy
+    auto after_level = [&](int s) -> int {
+        if (c->overlap && c->h4) {
+            // stream the finished level to the pinned host mirror while later levels run
+            HIPCHK(c, hipStreamWaitEvent(c->st_copy, lvl_full[s], 0));
+            const size_t bytes = (size_t)NMAT4 * c->lv_host[s].C * sizeof(int16_t);
+            HIPCHK(c, hipMemcpyAsync(c->h4 + c->lv_off[s], c->d4 + c->lv_off[s], bytes, hipMemcpyDeviceToHost, c->st_copy));
+        }
+        // P(s+3) only needs PK levels <= s; band-sharded, this rank's partials are combined in the
+        // bulk exchange of level s+1, which then records p_done[s+3]
+        if (s + 3 < n) {
+            hipEvent_t *ev = &c->tev[TEV_PER * (size_t)s];
+            HIPCHK(c, hipStreamWaitEvent(c->st_p, lvl_full[s], 0));
+            if (c->level_timing == 2) HIPCHK(c, hipEventRecord(ev[7], c->st_p));
+            HIPCHK(c, (hipError_t)pterm_launch(c, s, c->st_p));
+            if (c->level_timing == 2) HIPCHK(c, hipEventRecord(ev[8], c->st_p));
+            HIPCHK(c, hipEventRecord((xchg ? c->pp_done : c->p_done)[s + 3], c->st_p));
+        }
+        return CCJ_OK;
+    };
+    // Band-sharded exchange of level s, part `part` (ccj_engine.h XCH_EDGE / XCH_BULK):
+    // pack the rank's blocks of the part (+ the part's tail), gather, unpack.  The edge part runs on the
+    // level stream; the bulk part on st_x, split into its start (wait, pack; over RCCL also gather and
+    // unpack) and, for the in-process group, its finish one level later (the host-side gather), so
+    // that the host thread does not block on it before the next level is enqueued.
+    auto part_slice = [&](int s, int part) { return (size_t)xch_slice(n, c->xnmax[part][s], c->lv_host[s].M, part); };
+    auto part_body = [&](int s, int part) { return (size_t)xch_body(c->xnmax[part][s], c->lv_host[s].M); };
+    auto gather = [&](int s, int part, hipStream_t q) -> int {
+        if (c->lgroup) return local_allgather(c, part, part_slice(s, part), q);
+        ncclComm_t cm = part == XCH_EDGE ? c->comm : c->comm_b;
+        if (!cm) return set_err(c, CCJ_E_STATE, "sharded context without ccj_comm_init");
+        if (ncclAllGather(c->d_send[part], c->d_recv[part], part_slice(s, part) * sizeof(int16_t), ncclInt8, cm, q) != ncclSuccess)
+            return set_err(c, CCJ_E_COMM, "ncclAllGather (%s) failed at level %d", part == XCH_EDGE ? "edge" : "bulk", s);
+        return CCJ_OK;
+    };
+    auto bulk_unpack = [&](int s) -> int {
+        hipEvent_t *ev = &c->tev[TEV_PER * (size_t)s];
+        const int sig = s + 2;
+        HIPCHK(c, (hipError_t)ccjk_unpack(&c->T, s, c->world, c->rank, XCH_BULK, c->xnmax[XCH_BULK][s], c->d_recv[XCH_BULK],
+                                          part_slice(s, XCH_BULK), c->st_x));
+        if (s >= 1 && sig <= n - 1) {
+            HIPCHK(c, (hipError_t)ccjk_ptail_unpack(&c->T, sig, c->d_recv[XCH_BULK], part_slice(s, XCH_BULK), part_body(s, XCH_BULK),
+                                                    c->world, c->st_x));
+            HIPCHK(c, hipEventRecord(c->p_done[sig], c->st_x));  // P(sig) final on every rank
+        }
+        if (c->level_timing == 2) HIPCHK(c, hipEventRecord(ev[10], c->st_x));
+        HIPCHK(c, hipEventRecord(c->bulk_done[s], c->st_x));
+        return CCJ_OK;
+    };
+    auto bulk_start = [&](int s) -> int {
+        hipEvent_t *ev = &c->tev[TEV_PER * (size_t)s];
+        const int sig = s + 2;  // the P span whose partials ride this part (pushed after level s-1)
+        HIPCHK(c, hipStreamWaitEvent(c->st_x, c->lev_done[s], 0));
+        if (c->level_timing == 2) HIPCHK(c, hipEventRecord(ev[9], c->st_x));
+        if (s >= 1 && sig <= n - 1) {
+            HIPCHK(c, hipStreamWaitEvent(c->st_x, c->pp_done[sig], 0));
+            HIPCHK(c, (hipError_t)ccjk_ptail_pack(&c->T, sig, c->d_send[XCH_BULK] + part_body(s, XCH_BULK), c->st_x));
+        }
+        HIPCHK(c, (hipError_t)ccjk_pack(&c->T, s, c->world, c->rank, XCH_BULK, c->xnmax[XCH_BULK][s], c->d_send[XCH_BULK], c->st_x));
+        if (c->lgroup) return CCJ_OK;  // gathered and unpacked when the next level is enqueued (bulk_finish)
+        if (const int rc = gather(s, XCH_BULK, c->st_x)) return rc;
+        return bulk_unpack(s);
+    };
+    // the in-process group's bulk gather of level s, then what waits for level s to be complete
+    auto bulk_finish = [&](int s) -> int {
+        if (c->lgroup) {
+            if (const int rc = gather(s, XCH_BULK, c->st_x)) return rc;
+            if (const int rc = bulk_unpack(s)) return rc;
+        }
+        return after_level(s);
+    };
     for (int s = 0; s < n; ++s) {
-        hipEvent_t *ev = &c->tev[7 * (size_t)s];
-        // timing markers (ev[0..6]) only when per-kernel timing is on
+        hipEvent_t *ev = &c->tev[TEV_PER * (size_t)s];
+        // timing markers (ev[0..10]) only when per-kernel timing is on
         auto trec = [&](int x, hipStream_t q) { return c->level_timing == 2 ? hipEventRecord(ev[x], q) : hipSuccess; };
         // k_diag2d(sigma) on st_d; or, joined (c->join_diag), on st_il right after k_iloop(sigma+1),
         // so that level sigma+1 waits on one event that covers both
-        const bool xchg = c->world > 1 && !c->simulate;
         auto enqueue_diag = [&](int sg, hipStream_t q) -> int {
-            hipEvent_t *evd = &c->tev[7 * (size_t)sg];
+            hipEvent_t *evd = &c->tev[TEV_PER * (size_t)sg];
             if (sg >= 3) HIPCHK(c, hipStreamWaitEvent(q, c->p_done[sg], 0));
-            // band-sharded: span sg-1 is complete on this rank only after the level-(sg-1) exchange
+            // band-sharded: span sg-1 is complete on this rank only after the level-(sg-1) edge
+            // exchange, which carries it
             if (xchg && sg >= 1 && sg - 1 < c->nlev) HIPCHK(c, hipStreamWaitEvent(q, c->lev_done[sg - 1], 0));
             if (c->level_timing == 2) HIPCHK(c, hipEventRecord(evd[0], q));
             if (c->simulate) {  // every rank's share of the span, in one context
@@ -2108,7 +2198,8 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
             if (const int rc = enqueue_diag(s, c->join_diag ? c->st_il : c->st_d)) return rc;
         }
         if (s < c->nlev) {
-            if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_il, c->lev_done[s - 3], 0));
+            // k_iloop(s) reads levels <= s-3 (complete: band-sharded, their bulk parts unpacked)
+            if (s >= 3) HIPCHK(c, hipStreamWaitEvent(c->st_il, lvl_full[s - 3], 0));
             HIPCHK(c, trec(2, c->st_il));
             const int G = c->world;
             for (int r = 0; r < G; ++r) {  // every rank's launches in simulation, else this rank's
@@ -2124,6 +2215,9 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
             HIPCHK(c, hipEventRecord(c->il_done[s], c->st_il));
             HIPCHK(c, hipStreamWaitEvent(st, c->il_done[s], 0));
             if (s >= 1 && !c->join_diag) HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s - 1], 0));
+            // band-sharded: level s reads the other ranks' blocks of level s-2 from its bulk part (the
+            // edge part of level s-1 arrived on this stream; older levels precede s-2 on st_x)
+            if (xchg && s >= 2) HIPCHK(c, hipStreamWaitEvent(st, c->bulk_done[s - 2], 0));
             HIPCHK(c, trec(4, st));
             // the level: its plain launch, then (sharing levels) the leaders on the same stream, no
             // cross-stream hop between the two launches or between levels
@@ -2135,69 +2229,47 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                 if (!c->simulate && r != c->rank) continue;
                 HIPCHK(c, (hipError_t)ccjk_level4d_lead(&c->T, s, G, r, st));
             }
-            if (G > 1 && !c->simulate) {
-                HIPCHK(c, trec(6, st));  // timing mode 2: the exchange's share of the level span
-                // band-sharded exchange: this rank's cells of the level, all 22
-                // matrices, packed into one slice; ONE all-gather of equal slices; the other ranks'
-                // cells unpacked with their loop records and interior-loop copies
-                // The slice's tail carries this rank's partials of P(s+2) (its share of the P terms,
-                // pushed after level s-1), min-combined on arrival: P rides the level exchange, no
-                // extra collective.
-                const int nmax = c->xnmax[s];
-                const size_t slice4 = (size_t)xch_body(nmax, c->lv_host[s].M);
-                const size_t dt_off = slice4 + (size_t)xch_ptail(n);
-                const size_t slice = (size_t)xch_slice(n, nmax, c->lv_host[s].M);
-                // span s (this rank's intervals) rides the same slice
+            if (xchg) {
+                // the previous level's bulk part (in-process: its gather), the P terms it completes
+                if (s >= 1) {
+                    if (const int rc = bulk_finish(s - 1)) return rc;
+                }
+                HIPCHK(c, trec(6, st));  // timing mode 2: the edge exchange's share of the level span
+                // edge part: the rank's blocks a % 4 == 3 (all 22 matrices) and its intervals of span s
+                const size_t body = part_body(s, XCH_EDGE);
                 HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s], 0));
-                HIPCHK(c, (hipError_t)ccjk_dtail_pack(&c->T, s, G, c->rank, c->d_send + dt_off, st));
-                const int sig = s + 2;
-                const bool ptail = s >= 1 && sig <= n - 1;
-                if (ptail) {
-                    HIPCHK(c, hipStreamWaitEvent(st, c->pp_done[sig], 0));
-                    HIPCHK(c, (hipError_t)ccjk_ptail_pack(&c->T, sig, c->d_send + slice4, st));
-                }
-                HIPCHK(c, (hipError_t)ccjk_pack(&c->T, s, G, c->rank, nmax, c->d_send, st));
-                if (c->lgroup) {
-                    if (const int rc = local_allgather(c, slice)) return rc;
-                } else {
-                    if (!c->comm) return set_err(c, CCJ_E_STATE, "sharded context without ccj_comm_init");
-                    if (ncclAllGather(c->d_send, c->d_recv, slice * sizeof(int16_t), ncclInt8, c->comm, st) != ncclSuccess)
-                        return set_err(c, CCJ_E_COMM, "ncclAllGather failed at level %d", s);
-                }
-                HIPCHK(c, (hipError_t)ccjk_unpack(&c->T, s, G, c->rank, nmax, c->d_recv, slice, st));
-                HIPCHK(c, (hipError_t)ccjk_dtail_unpack(&c->T, s, c->d_recv, slice, dt_off, G, c->rank, st));
-                if (ptail) {
-                    HIPCHK(c, (hipError_t)ccjk_ptail_unpack(&c->T, sig, c->d_recv, slice, slice4, G, st));
-                    HIPCHK(c, hipEventRecord(c->p_done[sig], st));  // P(sig) final on every rank
-                }
+                HIPCHK(c, (hipError_t)ccjk_dtail_pack(&c->T, s, G, c->rank, c->d_send[XCH_EDGE] + body, st));
+                HIPCHK(c, (hipError_t)ccjk_pack(&c->T, s, G, c->rank, XCH_EDGE, c->xnmax[XCH_EDGE][s], c->d_send[XCH_EDGE], st));
+                if (const int rc = gather(s, XCH_EDGE, st)) return rc;
+                HIPCHK(c, (hipError_t)ccjk_unpack(&c->T, s, G, c->rank, XCH_EDGE, c->xnmax[XCH_EDGE][s], c->d_recv[XCH_EDGE],
+                                                  part_slice(s, XCH_EDGE), st));
+                HIPCHK(c, (hipError_t)ccjk_dtail_unpack(&c->T, s, c->d_recv[XCH_EDGE], part_slice(s, XCH_EDGE), body, G, c->rank,
+                                                        st));
             }
             HIPCHK(c, trec(5, st));
             if (c->overlap && c->h4 && !c->T.mat5) HIPCHK(c, (hipError_t)ccjk_mat5(&c->T, s, st));  // for the mirror copy
             HIPCHK(c, hipEventRecord(c->lev_done[s], st));
-            if (c->overlap && c->h4) {
-                // stream the finished level to the pinned host mirror while later levels run
-                HIPCHK(c, hipStreamWaitEvent(c->st_copy, c->lev_done[s], 0));
-                const size_t bytes = (size_t)NMAT4 * c->lv_host[s].C * sizeof(int16_t);
-                HIPCHK(c, hipMemcpyAsync(c->h4 + c->lv_off[s], c->d4 + c->lv_off[s], bytes, hipMemcpyDeviceToHost,
-                                         c->st_copy));
+            if (xchg) {
+                if (const int rc = bulk_start(s)) return rc;
+            } else if (const int rc = after_level(s)) {
+                return rc;
             }
-            // P(s+3) only needs PK levels <= s; band-sharded, this rank's partials are combined in
-            // the exchange of level s+1, which then records p_done[s+3]
-            if (s + 3 < n) {
-                HIPCHK(c, hipStreamWaitEvent(c->st_p, c->lev_done[s], 0));
+        } else {
+            if (xchg && s == c->nlev && s >= 1) {  // the last level's bulk part
+                if (const int rc = bulk_finish(s - 1)) return rc;
+            }
+            if (s + 3 < n && s + 3 >= 3) {
                 HIPCHK(c, (hipError_t)pterm_launch(c, s, c->st_p));
-                HIPCHK(c, hipEventRecord((G > 1 && !c->simulate ? c->pp_done : c->p_done)[s + 3], c->st_p));
+                HIPCHK(c, hipEventRecord(c->p_done[s + 3], c->st_p));
             }
-        } else if (s + 3 < n && s + 3 >= 3) {
-            HIPCHK(c, (hipError_t)pterm_launch(c, s, c->st_p));
-            HIPCHK(c, hipEventRecord(c->p_done[s + 3], c->st_p));
         }
     }
     if (getenv("CCJ_TRACE_ENQUEUE"))
         fprintf(stderr, "ccj_fill_device: enqueue %.2f ms\n",
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - enq0).count());
-    // join: the fill ends when the last level and the last span are done
+    // join: the fill ends when the last level (every rank's part of it) and the last span are done
     HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[n - 1], 0));
+    if (xchg && c->nlev >= 1) HIPCHK(c, hipStreamWaitEvent(st, c->bulk_done[c->nlev - 1], 0));
     HIPCHK(c, hipEventRecord(c->ev_end, st));
     c->pending = true;
     return CCJ_OK;
@@ -2221,12 +2293,17 @@ static int wait_fill_end(ccj_ctx *c) {
         const hipError_t q = hipEventQuery(c->ev_end);
         if (q == hipSuccess) return CCJ_OK;
         if (q != hipErrorNotReady) return set_err(c, CCJ_E_HIP, "fill: %s", hipGetErrorString(q));
-        ncclResult_t ae = ncclSuccess;
-        const ncclResult_t qr = ncclCommGetAsyncError(c->comm, &ae);
+        ncclResult_t ae = ncclSuccess, ae2 = ncclSuccess;
+        ncclResult_t qr = ncclCommGetAsyncError(c->comm, &ae);
+        if (qr == ncclSuccess && ae == ncclSuccess && c->comm_b) {  // the bulk communicator too
+            qr = ncclCommGetAsyncError(c->comm_b, &ae2);
+            ae = ae2;
+        }
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (qr != ncclSuccess || ae != ncclSuccess || el > limit_s) {
+            if (c->comm_b) ncclCommAbort(c->comm_b);
             ncclCommAbort(c->comm);
-            c->comm = nullptr;
+            c->comm = c->comm_b = nullptr;
             if (qr != ncclSuccess || ae != ncclSuccess)
                 return set_err(c, CCJ_E_COMM, "band-sharded exchange failed: %s",
                                ncclGetErrorString(qr != ncclSuccess ? qr : ae));
@@ -2257,6 +2334,9 @@ static int fill_finish(ccj_ctx *c) {
     c->diag_ms_v.assign(n, 0.0);
     c->il_ms_v.assign(n, 0.0);
     c->xch_ms_v.assign(n, 0.0);
+    c->xbulk_ms_v.assign(n, 0.0);
+    c->pp_ms_v.assign(n, 0.0);
+    double psum = 0;
     if (c->level_timing == 1) {
         // level s = from the end of level s-1 (ev_pre for s = 0) to its lev_done on st: the waits for
         // k_iloop(s) / k_diag2d(s-1), the plain launch and the leaders
@@ -2267,7 +2347,7 @@ static int fill_finish(ccj_ctx *c) {
         }
     }
     for (int s = 0; s < n && c->level_timing == 2; ++s) {
-        const hipEvent_t *ev = &c->tev[7 * (size_t)s];
+        const hipEvent_t *ev = &c->tev[TEV_PER * (size_t)s];
         HIPCHK(c, hipEventElapsedTime(&ms, ev[0], ev[1]));
         dsum += ms;
         c->diag_ms_v[s] = ms;
@@ -2279,15 +2359,25 @@ static int fill_finish(ccj_ctx *c) {
             HIPCHK(c, hipEventElapsedTime(&ms, ev[4], ev[5]));
             lsum += ms;
             c->lev_ms_v[s] = ms;
-            if (c->world > 1 && !c->simulate) {  // waits for span s / P tail, packs, all-gather, unpacks
+            if (s + 3 < n) {  // k_ppush(s) on st_p
+                HIPCHK(c, hipEventElapsedTime(&ms, ev[7], ev[8]));
+                psum += ms;
+                c->pp_ms_v[s] = ms;
+            }
+            if (c->world > 1 && !c->simulate) {
+                // the edge part on the level stream: waits for span s, packs, all-gather, unpacks
                 HIPCHK(c, hipEventElapsedTime(&ms, ev[6], ev[5]));
                 c->xch_ms_v[s] = ms;
+                // the bulk part on st_x: from its start (after the level) to its unpack
+                HIPCHK(c, hipEventElapsedTime(&ms, ev[9], ev[10]));
+                c->xbulk_ms_v[s] = ms;
             }
         }
     }
     c->level_ms = lsum;
     c->diag_ms = dsum;
     c->il_ms = isum;
+    c->pp_ms = psum;
     c->filled = true;
     return CCJ_OK;
 }
@@ -2746,13 +2836,22 @@ extern "C" int ccj_iloop_times(const ccj_ctx *c, double *iloop_ms, int cap) {
     return CCJ_OK;
 }
 
-extern "C" int ccj_exchange_times(const ccj_ctx *c, double *xch_ms, int cap) {
-    if (!c || !xch_ms) return CCJ_E_ARG;
-    for (int t = 0; t < cap && t < (int)c->xch_ms_v.size(); ++t) xch_ms[t] = c->xch_ms_v[t];
+extern "C" int ccj_exchange_times(const ccj_ctx *c, double *edge_ms, double *bulk_ms, int cap) {
+    if (!c || (!edge_ms && !bulk_ms)) return CCJ_E_ARG;
+    for (int t = 0; t < cap && t < (int)c->xch_ms_v.size(); ++t) {
+        if (edge_ms) edge_ms[t] = c->xch_ms_v[t];
+        if (bulk_ms) bulk_ms[t] = c->xbulk_ms_v[t];
+    }
     return CCJ_OK;
 }
 
 extern "C" double ccj_iloop_ms(const ccj_ctx *c) { return c ? c->il_ms : 0.0; }
+extern "C" double ccj_ppush_ms(const ccj_ctx *c) { return c ? c->pp_ms : 0.0; }
+extern "C" int ccj_ppush_times(const ccj_ctx *c, double *ppush_ms, int cap) {
+    if (!c || !ppush_ms) return CCJ_E_ARG;
+    for (int t = 0; t < cap && t < (int)c->pp_ms_v.size(); ++t) ppush_ms[t] = c->pp_ms_v[t];
+    return CCJ_OK;
+}
 
 extern "C" int ccj_set_timing(ccj_ctx *c, int mode) {
     if (!c || mode < 0 || mode > 2) return CCJ_E_ARG;
@@ -2776,44 +2875,45 @@ extern "C" int ccj_level_layout(int n, int t, int world, long long *C, int *M) {
     return CCJ_OK;
 }
 
-// The exchange geometry k_pack / k_unpack use (ccj_engine.h xch_*), for tests and integrators.
-extern "C" int ccj_exchange_layout(int n, int t, int world, long long *out4) {
-    if (!out4 || world < 1 || t < 0 || n < 4 || t > n - 3) return CCJ_E_ARG;
-    const int m = n - t - 2, M = m * (m + 1) / 2, nmax = xch_nmax(t, world);
-    out4[0] = nmax;
-    out4[1] = xch_body(nmax, M);                   // P tail offset
-    out4[2] = xch_body(nmax, M) + xch_ptail(n);    // span tail offset
-    out4[3] = xch_slice(n, nmax, M);               // slice elements
+// The exchange geometry k_pack / k_unpack use (ccj_engine.h xch_*), per part (0 = edge, 1 = bulk),
+// for tests and integrators: {nmax, tail offset (= padded body), slice elements}.
+extern "C" int ccj_exchange_layout(int n, int t, int world, int part, long long *out3) {
+    if (!out3 || world < 1 || t < 0 || n < 4 || t > n - 3 || (part != XCH_EDGE && part != XCH_BULK)) return CCJ_E_ARG;
+    const int m = n - t - 2, M = m * (m + 1) / 2, nmax = xch_nmax(t, world, part);
+    out3[0] = nmax;
+    out3[1] = xch_body(nmax, M);                // the part's tail: span t (edge) / P(t+2) partials (bulk)
+    out3[2] = xch_slice(n, nmax, M, part);      // slice elements
     return CCJ_OK;
 }
 
-// which == 0 (pack, rank `rank`): out[k] for every body element k of the rank's slice = the level
-//   element (x * C + a * M + c) k_pack copies there, -1 for padding;
+// which == 0 (pack, rank `rank`): out[k] for every body element k of the rank's slice of the part =
+//   the level element (x * C + a * M + c) k_pack copies there, -1 for padding;
 // which == 1 (unpack at rank `rank`): out[e] for every level element e = x * C + a * M + c = the
-//   position in the gathered buffer (owner * slice + body position) k_unpack reads it from, -1 for
-//   the rank's own cells.
+//   position in the part's gathered buffer (owner * slice + body position) k_unpack reads it from, -1
+//   for the rank's own cells and the other part's.
 // Returns the number of entries (cap: the room in out), or -CCJ_E_ARG.
-extern "C" long long ccj_exchange_index(int n, int t, int world, int rank, int which, long long *out, long long cap) {
-    if (world < 1 || rank < 0 || rank >= world || t < 0 || n < 4 || t > n - 3 || (which != 0 && which != 1))
+extern "C" long long ccj_exchange_index(int n, int t, int world, int rank, int part, int which, long long *out, long long cap) {
+    if (world < 1 || rank < 0 || rank >= world || t < 0 || n < 4 || t > n - 3 || (which != 0 && which != 1) ||
+        (part != XCH_EDGE && part != XCH_BULK))
         return -CCJ_E_ARG;
-    const int m = n - t - 2, M = m * (m + 1) / 2, nmax = xch_nmax(t, world);
-    const long long C = (long long)(t + 1) * M, slice = xch_slice(n, nmax, M);
+    const int m = n - t - 2, M = m * (m + 1) / 2, nmax = xch_nmax(t, world, part);
+    const long long C = (long long)(t + 1) * M, slice = xch_slice(n, nmax, M, part);
     const long long cnt = which == 0 ? (long long)NMAT4 * nmax * M : (long long)NMAT4 * C;
     if (cap < cnt || !out) return cnt;
     if (which == 0) {
         for (long long k = 0; k < cnt; ++k) out[k] = -1;
-        const int own = shard_count(t, world, rank);
+        const int np = xch_pcount(t, world, rank, part);
         for (int x = 0; x < NMAT4; ++x)
-            for (int o = 0; o < own; ++o)
+            for (int k = 0; k < np; ++k)
                 for (int c = 0; c < M; ++c)
-                    out[xch_pos(x, o, c, nmax, M)] = x * C + (long long)shard_a(o, world, rank) * M + c;
+                    out[xch_pos(x, k, c, nmax, M)] = x * C + (long long)shard_a(xch_own(k, part), world, rank) * M + c;
     } else {
         for (int x = 0; x < NMAT4; ++x)
             for (int a = 0; a <= t; ++a) {
-                int ro, o;
-                xch_src(a, world, ro, o);
+                int ro, pa, k;
+                xch_src(a, world, ro, pa, k);
                 for (int c = 0; c < M; ++c)
-                    out[x * C + (long long)a * M + c] = ro == rank ? -1 : ro * slice + xch_pos(x, o, c, nmax, M);
+                    out[x * C + (long long)a * M + c] = (ro == rank || pa != part) ? -1 : ro * slice + xch_pos(x, k, c, nmax, M);
             }
     }
     return cnt;
@@ -2834,10 +2934,15 @@ extern "C" int ccj_comm_init(ccj_ctx *c, const char *id_in) {
     HIPCHK(c, hipSetDevice(c->device));
     ncclUniqueId id;
     memcpy(&id, id_in, sizeof id);
+    if (c->comm_b) ncclCommDestroy(c->comm_b);
     if (c->comm) ncclCommDestroy(c->comm);
-    c->comm = nullptr;
+    c->comm = c->comm_b = nullptr;
     const ncclResult_t r = ncclCommInitRank(&c->comm, c->world, id, c->rank);
     if (r != ncclSuccess) return set_err(c, CCJ_E_HIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    // the bulk all-gathers run on their own stream: their own communicator (same ranks, same order), so
+    // the two streams' collectives never queue behind each other inside one communicator
+    const ncclResult_t r2 = ncclCommSplit(c->comm, 0, c->rank, &c->comm_b, nullptr);
+    if (r2 != ncclSuccess) return set_err(c, CCJ_E_HIP, "ncclCommSplit: %s", ncclGetErrorString(r2));
     return CCJ_OK;
 }
 
@@ -2889,6 +2994,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->st_p) hipStreamSynchronize(c->st_p);
     if (c->st_il) hipStreamSynchronize(c->st_il);
     if (c->st_d) hipStreamSynchronize(c->st_d);
+    if (c->st_x) hipStreamSynchronize(c->st_x);
     hipFree(c->d4);
     hipFree(c->d_ie);
     hipFree(c->d_est);
@@ -2919,8 +3025,10 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_ilm);
     hipFree(c->d_dummy);
     hipFree(c->d_items);
-    if (!leak_send) hipFree(c->d_send);
-    hipFree(c->d_recv);
+    for (int part = 0; part < 2; ++part) {
+        if (!leak_send) hipFree(c->d_send[part]);
+        hipFree(c->d_recv[part]);
+    }
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->h_ioff) hipHostFree(c->h_ioff);
     if (c->h_icount) hipHostFree(c->h_icount);
@@ -2943,7 +3051,10 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     for (auto e : c->lev_done) hipEventDestroy(e);
     for (auto e : c->p_done) hipEventDestroy(e);
     for (auto e : c->pp_done) hipEventDestroy(e);
+    for (auto e : c->bulk_done) hipEventDestroy(e);
     if (c->st_p) hipStreamDestroy(c->st_p);
+    if (c->st_x) hipStreamDestroy(c->st_x);
+    if (c->comm_b) ncclCommDestroy(c->comm_b);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->st_il) hipStreamDestroy(c->st_il);
     if (c->st_d) hipStreamDestroy(c->st_d);

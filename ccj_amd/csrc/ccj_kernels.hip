@@ -2039,33 +2039,36 @@ extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int n
 }
 
 // ------------------------------------------------------------------------------------------
-// Band-sharded exchange of level t.  k_pack: rank r's own cells, all 22 matrices,
-// into one contiguous slice [x][own index][M] of nmax blocks per matrix (nmax = the largest rank's
-// block count at t), so the exchange is ONE all-gather of equal slices.  k_unpack: every cell of the
-// other ranks' blocks from the gathered slices (rank r's at recv + r * rstride) back into the level layout, plus its loop records and
-// interior-loop copies (what k_level4d writes for its own cells).  The slices carry all 22 matrices,
-// the record-only five included (exchange fills keep T.mat5 = 1), so the records are rebuilt from them.
+// Band-sharded exchange of level t, in two parts (ccj_engine.h XCH_EDGE / XCH_BULK).
+// k_pack: rank r's cells of the part's blocks, all 22 matrices, into one contiguous slice
+// [x][part index][M] of nmax blocks per matrix (nmax = the largest rank's count of the part at t), so
+// each part is ONE all-gather of equal slices.  k_unpack: every cell of the other ranks' blocks of the
+// part from the gathered slices (rank r's at recv + r * rstride) back into the level layout, plus its
+// loop records and interior-loop copies (what k_level4d writes for its own cells).  The slices carry
+// all 22 matrices, the record-only five included (exchange fills keep T.mat5 = 1), so the records are
+// rebuilt from them.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pack(DevTables T, int t, int G, int r, int nmax, int16_t *send) {
+__global__ __launch_bounds__(256) void k_pack(DevTables T, int t, int G, int r, int part, int nmax, int16_t *send) {
     const int n = T.n, m = n - t - 2, Mt = (m * (m + 1)) >> 1;
     const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const int o = (int)(gc / Mt);
-    if (o >= shard_count(t, G, r)) return;
-    const int c = (int)(gc - (long long)o * Mt);
+    const int k = (int)(gc / Mt);
+    if (k >= xch_pcount(t, G, r, part)) return;
+    const int c = (int)(gc - (long long)k * Mt);
     const LvlDev Lt = T.ld[t];
-    const int16_t *src = T.d4 + Lt.lb + (long long)shard_a(o, G, r) * Mt + c;
+    const int16_t *src = T.d4 + Lt.lb + (long long)shard_a(xch_own(k, part), G, r) * Mt + c;
 #pragma unroll 2
-    for (int x = 0; x < NMAT4; ++x) send[xch_pos(x, o, c, nmax, Mt)] = src[(long long)x * Lt.C];
+    for (int x = 0; x < NMAT4; ++x) send[xch_pos(x, k, c, nmax, Mt)] = src[(long long)x * Lt.C];
 }
 
-__global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r, int nmax, const int16_t *recv, size_t rstride) {
+__global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r, int part, int nmax, const int16_t *recv,
+                                                size_t rstride) {
     const int n = T.n, m = n - t - 2, Mt = (m * (m + 1)) >> 1;
     const long long gc = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const int a = (int)(gc / Mt);
     if (a > t) return;
-    int ro, o;
-    xch_src(a, G, ro, o);
-    if (ro == r) return;  // own cell: k_level4d wrote it with its records and copies
+    int ro, pa, k;
+    xch_src(a, G, ro, pa, k);
+    if (ro == r || pa != part) return;  // own cell (k_level4d wrote it with its records and copies), or the other part
     const int c = (int)(gc - (long long)a * Mt);
     const float tm = 2.0f * m + 1.0f;
     int h = (int)((tm - sqrtf(tm * tm - 8.0f * (float)c)) * 0.5f);
@@ -2074,7 +2077,7 @@ __global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r
     while (h + 1 < m && (h + 1) * m - (((h + 1) * h) >> 1) <= c) ++h;
     const int Gh = h * m - ((h * (h - 1)) >> 1);
     const int i = c - Gh + 1, b = t - a;
-    const int j = i + a, k = j + h + 2, l = k + b;
+    const int j = i + a, kk = j + h + 2, l = kk + b;
     const LvlDev Lt = T.ld[t];
     const LvlX X = T.ldx[t];
     int16_t *dst = T.d4 + Lt.lb + (long long)a * Mt + c;
@@ -2083,18 +2086,18 @@ __global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r
     const int16_t *sl = recv + (size_t)ro * rstride;
 #pragma unroll
     for (int x = 0; x < NMAT4; ++x) {
-        v[x] = sl[xch_pos(x, o, c, nmax, Mt)];
+        v[x] = sl[xch_pos(x, k, c, nmax, Mt)];
         dst[x * C] = (int16_t)v[x];
     }
     write_records(T, Lt.lr, Lt.C, (unsigned)(a * Mt + c), v[PLmloop00], v[PMmloop00], v[POmloop00], v[PfromL], v[PfromO],
                   v[PLmloop10], v[PfromMprime], v[PK], v[PRmloop00], v[PfromR], imin(v[PL], v[PR]), v[PMmloop10],
                   v[POmloop10]);
     if (ptype(T, i, j) > 0) T.d4x[X.lbx + (long long)a * Mt + (i - 1) * m - (((i - 1) * (i - 2)) >> 1) + h] = (int16_t)v[PL];
-    if (ptype(T, k, l) > 0) {
+    if (ptype(T, kk, l) > 0) {
         const int q = i + h - 1;
         T.d4x[X.lbx + Lt.C + (long long)a * Mt + ((q * (q + 1)) >> 1) + i - 1] = (int16_t)v[PR];
     }
-    if (ptype(T, j, k) > 0) T.pmx[X.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = (int16_t)v[PM];
+    if (ptype(T, j, kk) > 0) T.pmx[X.pmb + ((long long)h * n + j - 1) * (t + 1) + a] = (int16_t)v[PM];
 }
 
 // The P partials of span sigma (each rank pushed only its share of the terms, k_ppush) ride in the
@@ -2135,16 +2138,18 @@ extern "C" int ccjk_ptail_unpack(const DevTables *T, int sigma, const int16_t *r
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_pack(const DevTables *T, int t, int G, int r, int nmax, int16_t *send, void *stream) {
+extern "C" int ccjk_pack(const DevTables *T, int t, int G, int r, int part, int nmax, int16_t *send, void *stream) {
     const int m = T->n - t - 2;
     if (m <= 0) return 0;
-    const long long cells = (long long)shard_count(t, G, r) * (m * (m + 1) / 2);
+    if (xch_pcount(t, G, r, part) > nmax) return (int)hipErrorInvalidValue;
+    const long long cells = (long long)xch_pcount(t, G, r, part) * (m * (m + 1) / 2);
     if (cells <= 0) return 0;
-    hipLaunchKernelGGL(k_pack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, G, r, nmax, send);
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, G, r, part, nmax,
+                       send);
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_unpack(const DevTables *T, int t, int G, int r, int nmax, const int16_t *recv, size_t rstride,
+extern "C" int ccjk_unpack(const DevTables *T, int t, int G, int r, int part, int nmax, const int16_t *recv, size_t rstride,
                            void *stream) {
     const int m = T->n - t - 2;
     if (m <= 0) return 0;
@@ -2152,8 +2157,9 @@ extern "C" int ccjk_unpack(const DevTables *T, int t, int G, int r, int nmax, co
     // matrices: without T.mat5 the five record-only matrices are not in d4 (k_pack would ship stale ones)
     if (!recv || !T->mat5) return (int)hipErrorInvalidValue;
     const long long cells = (long long)(t + 1) * (m * (m + 1) / 2);
-    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, G, r, nmax, recv,
-                       rstride);
+    if (xch_nmax(t, G, part) > nmax) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_unpack, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, G, r, part, nmax,
+                       recv, rstride);
     return (int)hipGetLastError();
 }
 

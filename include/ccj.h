@@ -150,16 +150,22 @@ int  ccj_hashes(const ccj_ctx *ctx, uint64_t *out);
 int  ccj_last_timing(const ccj_ctx *ctx, double *fill_ms, double *kernel_ms3);
 /* Sum of the k_iloop (interior-loop pass) times of the last fill (ms). */
 double ccj_iloop_ms(const ccj_ctx *ctx);
+/* summed k_ppush (P terms) launch times of the last fill in timing mode 2 (ms) */
+double ccj_ppush_ms(const ccj_ctx *ctx);
 /* Host side of the last fold (ms): out3[0] = wait for the host mirror (D2H tail), [1] = W, [2] = backtrack. */
 int  ccj_host_timing(const ccj_ctx *ctx, double *out3);
 /* Per-level kernel times of the last fill (ms): level_ms[t] (k_level4d, level t), diag_ms[s]
  * (k_diag2d, span s); ccj_iloop_times: iloop_ms[t] (k_iloop, level t). */
 int  ccj_level_times(const ccj_ctx *ctx, double *level_ms, double *diag_ms, int cap);
-/* Band-sharded contexts in timing mode 2: per level, the exchange's part of the level span (from
- * the end of the level's launches to the end of its unpack: waits for the span and P tails, packs,
- * the all-gather, unpacks); 0 elsewhere. */
-int  ccj_exchange_times(const ccj_ctx *ctx, double *xch_ms, int cap);
+/* Band-sharded contexts in timing mode 2, per level (0 elsewhere; either pointer may be NULL):
+ * edge_ms[t] = the edge part's share of the level span on the level stream (from the end of the
+ * level's launches to the end of its unpack: the wait for span t, pack, all-gather, unpack); bulk_ms[t]
+ * = the bulk part on its side stream (from the level's end: the wait for the P tail, pack, all-gather,
+ * unpack), which overlaps the next level. */
+int  ccj_exchange_times(const ccj_ctx *ctx, double *edge_ms, double *bulk_ms, int cap);
 int  ccj_iloop_times(const ccj_ctx *ctx, double *iloop_ms, int cap);
+/* ccj_ppush_times: ppush_ms[t] (k_ppush after level t), timing mode 2 */
+int  ccj_ppush_times(const ccj_ctx *ctx, double *ppush_ms, int cap);
 /* What the next fills time (HIP events): 0 = the fill only; 1 (default) = + per-level durations
  * (level_ms, from events the fill records anyway); 2 = + k_diag2d / k_iloop times and level spans
  * from extra marker events around every launch (they slow the fill down by a few percent). */
@@ -177,15 +183,18 @@ int  ccj_comm_init(ccj_ctx *ctx, const char *id);
 int  ccj_shard_blocks(int n, int t, int world, int rank, int *a_out, int cap);
 /* Per-matrix element count C_t of level t and the a-block size M_t (the same for every world). */
 int  ccj_level_layout(int n, int t, int world, long long *C, int *M);
-/* The level-t exchange slice (host helper, no GPU; the geometry k_pack / k_unpack use),
- * in int16 elements: out4 = {nmax (the largest rank's block count), P-tail offset, span-tail offset,
- * slice size}.  The body is [matrix][own block][cell] of nmax blocks per matrix. */
-int  ccj_exchange_layout(int n, int t, int world, long long *out4);
-/* which = 0: for each body element of rank's slice, the level element (x*C + a*M + c) packed there
- * (-1: padding); which = 1: for each level element, its position in the gathered buffer
- * (owner * slice + body position) as rank unpacks it (-1: rank's own cell).  Returns the entry
- * count; fills out only when cap >= that count.  < 0: bad arguments. */
-long long ccj_exchange_index(int n, int t, int world, int rank, int which, long long *out, long long cap);
+/* The level-t exchange is two all-gathers: part 0 ("edge") = each rank's blocks
+ * a % 4 == 3, the only cells of level t another rank's level t+1 reads, + span t (tail), on the level
+ * stream; part 1 ("bulk") = the other blocks + the rank's P(t+2) partials (tail), on a side stream
+ * that overlaps level t+1.  ccj_exchange_layout (host helper, no GPU; the geometry k_pack / k_unpack
+ * use), in int16 elements: out3 = {nmax (the largest rank's block count of the part), tail offset,
+ * slice size}.  The body is [matrix][part index][cell] of nmax blocks per matrix. */
+int  ccj_exchange_layout(int n, int t, int world, int part, long long *out3);
+/* which = 0: for each body element of rank's slice of the part, the level element (x*C + a*M + c)
+ * packed there (-1: padding); which = 1: for each level element, its position in the part's
+ * gathered buffer (owner * slice + body position) as rank unpacks it (-1: rank's own cell or the other
+ * part's).  Returns the entry count; fills out only when cap >= that count.  < 0: bad arguments. */
+long long ccj_exchange_index(int n, int t, int world, int rank, int part, int which, long long *out, long long cap);
 /* In-process exchange group (tests, and several ranks sharing one device): shard_world contexts,
  * each driven by its own host thread, join one group instead of an RCCL communicator. */
 typedef struct ccj_group ccj_group;

@@ -75,8 +75,9 @@ def test_sharded_fold_matches_reference_stdout(case, world):
 
 def _fold_group(seq, params, world):
     """Every rank of a band-sharded fold as its own context, exchanging through an in-process group
-    (the real sharded path: own blocks only, pack, ONE all-gather per level, unpack with records and
-    interior-loop copies); each rank driven by its own thread."""
+    (the real sharded path: own blocks only; per level an edge all-gather on the level stream and a bulk
+    all-gather on a side stream, each packed and unpacked with records and interior-loop copies); each
+    rank driven by its own thread."""
     import threading
     from ccj_amd import LocalGroup, W_final
     g = LocalGroup(world)
@@ -107,9 +108,11 @@ def _close_group(g, ranks):
     g.close()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 @pytest.mark.parametrize("case", HASHES[:2], ids=lambda c: f"n{len(c['seq'])}-{c['params']}")
 def test_exchange_group_every_rank_holds_the_reference_fold(case, world):
+    """The real two-part exchange (edge part on the level stream, bulk part on its side stream one level
+    behind) at worlds 2, 3, 4 and 8: every rank ends with the reference's matrices."""
     g, ranks = _fold_group(case["seq"], case["params"], world)
     try:
         for wf in ranks:

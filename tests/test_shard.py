@@ -3,13 +3,15 @@
 * Ownership: a-block a of every level belongs to rank (a // 4) % world, the same rank on every
   level, so a split-sharing leader (a % 4 == 0) and its followers (a+1 .. a+3, on later levels)
   are on one rank; ccj_shard_blocks lists a rank's blocks, and every level's blocks are partitioned.
-* Exchange: world-size-2 gloo run.  Each rank packs only its own cells of every level (values from
-  the C oracle, which is the checker here) into one slice [matrix][own block][cell] of nmax blocks
-  (nmax = the largest rank's block count), the slices are all-gathered as ONE collective per level
-  (the RCCL path does the same on the GPU), and unpacking the other ranks' slices must rebuild the
-  level exactly as one process writes it.  Pack, unpack and the slice layout go through the shipped
-  index maps (ccj_exchange_index / ccj_exchange_layout: the ccj_engine.h xch_* functions k_pack and
-  k_unpack use), not a model of them.
+* Exchange: world-size-2 gloo run.  Each level's exchange is two all-gathers: the edge
+  part (each rank's blocks a % 4 == 3, the only level-t cells another rank's level t+1 reads, plus
+  span t) and the bulk part (the other blocks plus the P partials).  Each rank packs only its own
+  cells of the part (values from the C oracle, which is the checker here) into one slice
+  [matrix][part index][cell] of nmax blocks (nmax = the largest rank's count of the part), the slices
+  are all-gathered (the RCCL path does the same on the GPU), and unpacking both parts of the other
+  ranks' slices must rebuild the level exactly as one process writes it.  Pack, unpack and the slice
+  layout go through the shipped index maps (ccj_exchange_index / ccj_exchange_layout: the ccj_engine.h
+  xch_* functions k_pack and k_unpack use), not a model of them.
 * 2-D spans: interval i of every span belongs to rank (i-1) % world (k_diag2d); the exchange of
   level t also carries span t (k_dtail_pack / k_dtail_unpack: the 10 int32 planes V, Vt, P, WBP, WB,
   WPP, WP, WMv, WMp, WM of the rank's own intervals, in the kernels' order), and unpacking must give
@@ -88,42 +90,47 @@ def _xlib():
     import ctypes
     from tests.oracle_lib import ROOT
     L = ctypes.CDLL(os.path.join(ROOT, "ccj_amd", "lib", "libccj_hip.so"))
-    L.ccj_exchange_layout.argtypes = [ctypes.c_int] * 3 + [ctypes.POINTER(ctypes.c_longlong)]
-    L.ccj_exchange_index.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_longlong), ctypes.c_longlong]
+    L.ccj_exchange_layout.argtypes = [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_longlong)]
+    L.ccj_exchange_index.argtypes = [ctypes.c_int] * 6 + [ctypes.POINTER(ctypes.c_longlong), ctypes.c_longlong]
     L.ccj_exchange_index.restype = ctypes.c_longlong
     return L
 
 
-def xch_layout(n, t, world):
-    """{nmax, P-tail offset, span-tail offset, slice} in int16 elements (ccj_exchange_layout: the
-    geometry k_pack / k_unpack / the host's slices use, ccj_engine.h xch_*)."""
+EDGE, BULK = 0, 1
+
+
+def xch_layout(n, t, world, part):
+    """{nmax, tail offset, slice} in int16 elements of one part (ccj_exchange_layout: the geometry
+    k_pack / k_unpack / the host's slices use, ccj_engine.h xch_*)."""
     import ctypes
-    out = (ctypes.c_longlong * 4)()
-    assert _xlib().ccj_exchange_layout(n, t, world, out) == 0
+    out = (ctypes.c_longlong * 3)()
+    assert _xlib().ccj_exchange_layout(n, t, world, part, out) == 0
     return list(out)
 
 
-def xch_index(n, t, world, rank, which):
-    """ccj_exchange_index: which 0 = the level element each body element of rank's slice packs
-    (-1 padding); 1 = each level element's position in the gathered buffer (-1 own cell)."""
+def xch_index(n, t, world, rank, part, which):
+    """ccj_exchange_index: which 0 = the level element each body element of rank's slice of the part
+    packs (-1 padding); 1 = each level element's position in the part's gathered buffer (-1: own cell
+    or the other part)."""
     import ctypes
     L = _xlib()
-    cnt = L.ccj_exchange_index(n, t, world, rank, which, None, 0)
+    cnt = L.ccj_exchange_index(n, t, world, rank, part, which, None, 0)
     assert cnt >= 0
     out = np.zeros(cnt, dtype=np.int64)
-    assert L.ccj_exchange_index(n, t, world, rank, which, out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), cnt) == cnt
+    assert L.ccj_exchange_index(n, t, world, rank, part, which, out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)),
+                                cnt) == cnt
     return out
 
 
-def _pack(level, n, t, world, rank):
-    """k_pack through the shipped index map: the body of rank's slice."""
-    idx = xch_index(n, t, world, rank, 0)
+def _pack(level, n, t, world, rank, part):
+    """k_pack through the shipped index map: the body of rank's slice of the part."""
+    idx = xch_index(n, t, world, rank, part, 0)
     return np.where(idx >= 0, level[np.maximum(idx, 0)], 0).astype(np.int16)
 
 
-def _unpack(level, gathered, n, t, world, rank):
-    """k_unpack through the shipped index map: every other rank's cell from the gathered slices."""
-    idx = xch_index(n, t, world, rank, 1)
+def _unpack(level, gathered, n, t, world, rank, part):
+    """k_unpack through the shipped index map: the other ranks' cells of the part from the gathered slices."""
+    idx = xch_index(n, t, world, rank, part, 1)
     other = idx >= 0
     level[other] = gathered[idx[other]]
 
@@ -191,39 +198,60 @@ def _span_tail(fold, n, sigma, world, rank):
     return tail
 
 
+def _gather(own, world, torch, dist):
+    # gloo has no int16 all-gather: the slices travel as bytes (RCCL: ncclInt8 likewise)
+    parts = [torch.empty(2 * len(own), dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(parts, torch.from_numpy(own.view(np.uint8)))
+    return [p.numpy().view(np.int16) for p in parts]
+
+
 def _gloo_body(rank, world, n, seq, torch, dist):
     fold = OracleFold(seq, blob("Turner04"), 2, 0)
     ok = True
     for t in range(n - 2):
         from ccj_amd import shard_blocks
         mine = shard_blocks(n, t, world, rank)
-        nmax, p_off, d_off, slice_n = xch_layout(n, t, world)
         level, C, M = _level(n, t, fold, mine)
-        sig = t + 2  # the P span whose partials ride this exchange (pushed after level t-1)
-        ptail = _p_partials(fold, n, sig, world, rank) if 1 <= t and sig <= n - 1 else np.zeros(n + 1, np.uint64)
-        # this rank's slice, laid out as the host lays out d_send: body, P tail, span tail
-        own = np.zeros(slice_n, dtype=np.int16)
-        body = _pack(level, n, t, world, rank)
+        # edge part (level stream): body, then span t; ONE collective
+        _, d_off, slice_e = xch_layout(n, t, world, EDGE)
+        own = np.zeros(slice_e, dtype=np.int16)
+        body = _pack(level, n, t, world, rank, EDGE)
         own[:len(body)] = body
-        own[p_off:d_off] = ptail.view(np.int16)
         own[d_off:] = _span_tail(fold, n, t, world, rank).reshape(-1).view(np.int16)
-        # gloo has no int16 all-gather: the slices travel as bytes (RCCL: ncclInt8 likewise)
-        parts = [torch.empty(2 * slice_n, dtype=torch.uint8) for _ in range(world)]
-        dist.all_gather(parts, torch.from_numpy(own.view(np.uint8)))  # ONE collective per level: cells + P tail + span t
-        parts = [p.numpy().view(np.int16) for p in parts]
-        gathered = np.concatenate(parts)
-        _unpack(level, gathered, n, t, world, rank)
+        parts_e = _gather(own, world, torch, dist)
+        gathered_e = np.concatenate(parts_e)
+        # bulk part (side stream): body, then this rank's P(t+2) partials (pushed after level t-1); ONE collective
+        sig = t + 2
+        _, p_off, slice_b = xch_layout(n, t, world, BULK)
+        ptail = _p_partials(fold, n, sig, world, rank) if 1 <= t and sig <= n - 1 else np.zeros(n + 1, np.uint64)
+        own = np.zeros(slice_b, dtype=np.int16)
+        body = _pack(level, n, t, world, rank, BULK)
+        own[:len(body)] = body
+        own[p_off:] = ptail.view(np.int16)
+        parts_b = _gather(own, world, torch, dist)
+        gathered_b = np.concatenate(parts_b)
+        # the edge part alone gives every block level t+1 of this rank reads of level t (a-1 and a of
+        # every own block a, pseudo_loop.cc:357-362 at split step 1)
+        edge_only = level.copy()
+        _unpack(edge_only, gathered_e, n, t, world, rank, EDGE)
         full, _, _ = _level(n, t, fold, range(t + 1))
+        for a in shard_blocks(n, t + 1, world, rank) if t + 1 < n - 2 else []:
+            for b in (a - 1, a):
+                if 0 <= b <= t:
+                    for x in range(NMAT4):
+                        ok &= bool(np.array_equal(edge_only[x * C + b * M:x * C + (b + 1) * M], full[x * C + b * M:x * C + (b + 1) * M]))
+        _unpack(level, gathered_e, n, t, world, rank, EDGE)
+        _unpack(level, gathered_b, n, t, world, rank, BULK)
         ok &= bool(np.array_equal(level, full))
-        # k_dtail_unpack: each interval from its owner's slice (the whole span on every rank), and
+        # k_dtail_unpack: each interval from its owner's edge slice (the whole span on every rank), and
         # WBW rebuilt from the WBP / WP planes
         for i in range(1, n - t + 1):
-            sl = gathered[((i - 1) % world) * slice_n + d_off:((i - 1) % world + 1) * slice_n].view(np.int32)
+            sl = gathered_e[((i - 1) % world) * slice_e + d_off:((i - 1) % world + 1) * slice_e].view(np.int32)
             got = [int(sl[x * (n + 1) + i]) for x in range(10)]
             ok &= got == _span_values(fold, i, i + t)
             ok &= (got[3], got[6]) == (_span_values(fold, i, i + t)[3], _span_values(fold, i, i + t)[6])
         if 1 <= t and sig <= n - 1:
-            comb = np.minimum.reduce([p[p_off:d_off].view(np.uint64) for p in parts])
+            comb = np.minimum.reduce([p[p_off:].view(np.uint64) for p in parts_b])
             for i in range(1, n - sig + 1):
                 ref = fold.get2(0, i, i + sig)  # reference P (INF+1 when no term)
                 got = int(comb[i])
@@ -269,31 +297,59 @@ def test_p_term_partition_covers_every_term_once(world):
 
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_exchange_index_maps_rebuild_every_level(world):
-    """The shipped pack / unpack maps (ccj_exchange_index) at every level of n=40: each rank's slice
-    holds exactly its own cells, and unpacking the gathered slices gives every rank every other
-    rank's cell, so own + unpacked = the whole level (values: the element indices themselves)."""
+    """The shipped pack / unpack maps (ccj_exchange_index) at every level of n=40, both parts: each
+    rank's slice of a part holds exactly its own blocks of that part (edge: a % 4 == 3), and unpacking
+    both parts' gathered slices gives every rank every other rank's cell, so own + unpacked = the whole
+    level (values: the element indices themselves)."""
     from ccj_amd import shard_blocks
     n = 40
     for t in range(n - 2):
-        nmax, p_off, d_off, slice_n = xch_layout(n, t, world)
         C = (t + 1) * (n - t - 2) * (n - t - 1) // 2
+        M = (n - t - 2) * (n - t - 1) // 2
         full = np.arange(NMAT4 * C, dtype=np.int64)
-        slices = []
+        got = {r: np.full(NMAT4 * C, -1, dtype=np.int64) for r in range(world)}
+        for part in (EDGE, BULK):
+            nmax, tail_off, slice_n = xch_layout(n, t, world, part)
+            slices = []
+            for r in range(world):
+                idx = xch_index(n, t, world, r, part, 0)
+                assert len(idx) <= tail_off and len(idx) == NMAT4 * nmax * M
+                own = idx[idx >= 0]
+                assert len(np.unique(own)) == len(own)
+                want = [a for a in shard_blocks(n, t, world, r) if (a % GRP == GRP - 1) == (part == EDGE)]
+                assert sorted(set((own % C) // M)) == want
+                sl = np.full(slice_n, -1, dtype=np.int64)
+                sl[:len(idx)] = np.where(idx >= 0, full[np.maximum(idx, 0)], -1)
+                slices.append(sl)
+            gathered = np.concatenate(slices)
+            for r in range(world):
+                u = xch_index(n, t, world, r, part, 1)
+                blk = (np.arange(NMAT4 * C) % C) // M
+                expect = ~np.isin(blk, shard_blocks(n, t, world, r)) & (((blk % GRP) == GRP - 1) == (part == EDGE))
+                assert np.array_equal(u >= 0, expect)
+                got[r][u >= 0] = gathered[u[u >= 0]]
         for r in range(world):
-            idx = xch_index(n, t, world, r, 0)
-            assert len(idx) <= p_off and len(idx) == NMAT4 * nmax * ((n - t - 2) * (n - t - 1) // 2)
-            own = idx[idx >= 0]
-            assert len(np.unique(own)) == len(own)
-            M = (n - t - 2) * (n - t - 1) // 2
-            assert sorted(set((own % C) // M)) == shard_blocks(n, t, world, r)
-            sl = np.full(slice_n, -1, dtype=np.int64)
-            sl[:len(idx)] = np.where(idx >= 0, full[np.maximum(idx, 0)], -1)
-            slices.append(sl)
-        gathered = np.concatenate(slices)
-        for r in range(world):
-            u = xch_index(n, t, world, r, 1)
-            M = (n - t - 2) * (n - t - 1) // 2
             mine = np.isin((np.arange(NMAT4 * C) % C) // M, shard_blocks(n, t, world, r))
-            assert np.array_equal(u < 0, mine)
-            got = np.where(u >= 0, gathered[np.maximum(u, 0)], full)
-            assert np.array_equal(got, full)
+            got[r][mine] = full[mine]
+            assert np.array_equal(got[r], full)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_edge_part_is_a_fraction_of_the_level(world):
+    """The critical-path part of each level's exchange (edge: blocks a % 4 == 3 + span t) against the
+    one-slice exchange of round 5 (every own block + both tails): at n=200, at most 30 % of its elements
+    over the fold, and per level wherever that slice is 128 KB or more (on the last levels the constant
+    span tail dominates slices of a few KB) (VERDICT r5 Next 2)."""
+    n = 200
+    tot_new = tot_old = 0
+    for t in range(n - 2):
+        m = n - t - 2
+        M = m * (m + 1) // 2
+        nmax_all = max(len([a for a in range(t + 1) if _owner(a, world) == r]) for r in range(world))
+        old = ((22 * nmax_all * M + 3) & ~3) + 4 * (n + 1) + 20 * (n + 1)
+        new = xch_layout(n, t, world, EDGE)[2]
+        tot_new += new
+        tot_old += old
+        if 2 * old >= 128 << 10:
+            assert new <= 0.30 * old, (t, new / old)
+    assert tot_new <= 0.30 * tot_old, tot_new / tot_old

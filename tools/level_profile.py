@@ -18,6 +18,15 @@ for _ in range(int(os.environ.get("CCJ_PROFILE_REPS", "5"))):
     wf.ccj()
     fills.append(wf.timing()["fill_ms"])
 lev1 = wf.timing()["level4d_ms"]
+if os.environ.get("CCJ_PROFILE_DUMP"):
+    # every level's span on the level stream in the last uninstrumented fold (lev_done[t-1] -> lev_done[t]:
+    # the level chain's critical path, waits included), for tools/shard_projection.py
+    _L = lib()
+    _L.ccj_level_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    _lv = (ctypes.c_double * n)()
+    _L.ccj_level_times(wf._h, _lv, None, n)
+    with open(os.environ["CCJ_PROFILE_DUMP"], "w") as f:
+        json.dump({"n": n, "seed": 5, "params": "Turner04", "fill_ms": fills[-1], "level_ms": list(_lv)[:n - 2]}, f)
 # one more fold with a marker pair around every launch for the per-kernel breakdown (slower fill)
 wf.set_timing(2)
 wf.ccj()
