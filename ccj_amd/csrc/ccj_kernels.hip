@@ -978,6 +978,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t il_src(const int16_t *base) {
     return __builtin_amdgcn_make_buffer_rsrc((void *)(((unsigned long long)hi << 32) | lo), (short)0, -1, 0x00020000);
 }
 
+#ifdef CCJ_ABLATE_ILHALF
+#define ILHALF(x) ((x) >> 1)  // timing only: every list walked half way (wrong results; the marginal cost of k_iloop's work)
+#else
+#define ILHALF(x) (x)
+#endif
 // one wave per work item: a closing pair that can pair and up to IL_CW (two 64-lane chunks) of
 // its cells (ccj_items.h, built by k_items in enumeration order)
 constexpr int IL_WPB = 4;  // waves (consecutive items) per k_iloop workgroup (1, 2, 8, 16 measured +3.6 ... +9 ms)
@@ -1022,7 +1027,7 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         if (lane == 63) Atab = -B0;
         const int e0 = (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
         const uint2 *le = T.il + pidx * IL_CAP + e0;
-        const int lc = (int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0;
+        const int lc = ILHALF((int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0);
         const int2 bm = G > 1  ? make_int2(il_scan_g<true, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl), INF)
                         : pair ? il_scan<true, false, true>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
                                : il_scan<true, false, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
@@ -1059,7 +1064,7 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         if (lane == 63) Atab = -B0;
         const int e0 = (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
         const uint2 *le = T.il + pidx * IL_CAP + e0;
-        const int lc = (int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0;
+        const int lc = ILHALF((int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0);
         const int2 bm = G > 1  ? make_int2(il_scan_g<false, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl), INF)
                         : pair ? il_scan<false, false, true>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
                                : il_scan<false, false, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
@@ -1103,9 +1108,9 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         const int cnt = (int)ld_const(T.ilmseg + pidx * IL_SEG + imin(t - 1, IL_SEG - 1));
         const int e0 = (int)ld_const(T.ilmseg + pidx * IL_SEG + 3);
         const uint2 *le = T.ilm + pidx * IL_CAP + e0;
-        const int2 bm = G > 1  ? make_int2(il_scan_g<true, true>(T, le, cnt - e0, src, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl), INF)
-                        : pair ? il_scan<true, true, true>(T, le, cnt - e0, src, Atab, Btab, lofs2, as, t - as, lofs2b, ab, t - ab)
-                               : il_scan<true, true, false>(T, le, cnt - e0, src, Atab, Btab, lofs2, as, t - as, 0u, 0, 0);
+        const int2 bm = G > 1  ? make_int2(il_scan_g<true, true>(T, le, ILHALF(cnt - e0), src, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl), INF)
+                        : pair ? il_scan<true, true, true>(T, le, ILHALF(cnt - e0), src, Atab, Btab, lofs2, as, t - as, lofs2b, ab, t - ab)
+                               : il_scan<true, true, false>(T, le, ILHALF(cnt - e0), src, Atab, Btab, lofs2, as, t - as, 0u, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
         if ((act && (a < 0 || a > t || h < 0 || h >= m || (j - a) < 1 || (j - a) > m - h)) ||
             (actb && (ab < 0 || ab > t || (j - ab) < 1 || (j - ab) > m - h))) {

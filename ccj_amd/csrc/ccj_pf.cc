@@ -608,6 +608,13 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
         maxC = std::max(maxC, (t + 1) * M);
         c->cells += (t + 1) * M;
     }
+    // k_pf_ppush addresses the PK rows of PF_PP_S consecutive levels as 32-bit byte offsets from the
+    // lowest one's PK start (one buffer resource per wave): that span must stay below 4 GB
+    for (int t = 0; t <= n - 3; ++t) {
+        const int tt = std::min(t + PF_PP_S - 1, n - 3);
+        const long long lo = c->lv[t].lb + PF_PK * c->lv[t].C, hi = c->lv[tt].lb + PF_PK * c->lv[tt].C + c->lv[tt].C;
+        if (4 * (hi - lo) >= (1LL << 32)) return pf_err(c, CCJ_E_ARG, "n too large: the PK rows of 8 levels exceed 4 GB (k_pf_ppush offsets)");
+    }
     // k_pf_iloop work items: the cells of each pairing closing pair in 64-lane chunks, encoded as
     // ccj_items.h's (unsharded).  PL and PR rows are the MFE engine's; PM rows here start at h = 0,
     // since get_PMiloop has no hairpin bound on (j, k) (part_func.cc:804-824)

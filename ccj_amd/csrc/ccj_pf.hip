@@ -30,6 +30,7 @@
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "ccj_pf_energy.h"
 #include "ccj_pf_engine.h"
@@ -182,25 +183,20 @@ __global__ __launch_bounds__(256) void k_pf_pterm(PfDev D, int s) {
 //   part B wave: (a2 = d-j-1, 64 consecutive l, PF_PP_S consecutive t1), loop h2 = k-d-1:
 //       B = level T, block a2, row h2, position l-h2-T-2;  A = level t1, block t1-h2, row a2, position l-T-3-t1
 // ---------------------------------------------------------------------------------------------
-constexpr int PF_PP_S = 8;
 
-__device__ __forceinline__ const int *pf_pk_row(const PfDev &D, int t, int a, int h) {
+// The operands as buffer loads (the MFE k_ppush's scheme, round 5): a wave reads PK at level lev and at
+// the PF_PP_S consecutive levels o0 .. o0+ns-1, each set within 4 GB of its lowest level's PK start
+// (ccj_pf_create checks it), so each is one buffer resource (base = that level's PK) and an operand is
+// (uniform byte offset, lane byte offset) = (soffset, voffset): no 64-bit row pointer per load (those
+// took two readfirstlanes and a 64-bit address each).  Element (t, a, h, pos) of PK is
+// pk_base(t) + a*M_t + G_t(h) + pos - 1, G_t(h) = h*m_t - h(h-1)/2.
+__device__ __forceinline__ long long pf_pk_base(const PfDev &D, int t) {
     const PfLvlS L = ldc_lvl(D.ld + t);
-    const int m = D.n - t - 2;
-    return D.d4 + L.lb + PF_PK * L.C + (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) - 1;  // + position (1-based)
+    return L.lb + PF_PK * L.C;
 }
-__device__ __forceinline__ const int *pf_uni(const int *p) {
-    const unsigned long long v = (unsigned long long)p;
-    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
-    return (const int *)(((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ int pf_at(const int *row, int pos) {
-    typedef const __attribute__((address_space(1))) char gchar;
-    typedef const __attribute__((address_space(1))) int gint;
-    return *(gint *)((gchar *)row + (unsigned)(pos << 2));  // global_load saddr + voffset
-}
+__device__ __forceinline__ int pf_G(int m, int h) { return h * m - ((h * (h - 1)) >> 1); }
 
+template <int U>
 __global__ __launch_bounds__(256) void k_pf_ppush(PfDev D, int lev, int ngrp, int npairs, int hs_len, int blocksA) {
     const int n = D.n, rs = D.rs;
     const int lane = threadIdx.x & 63;
@@ -234,6 +230,9 @@ __global__ __launch_bounds__(256) void k_pf_ppush(PfDev D, int lev, int ngrp, in
 #pragma unroll
     for (int s = 0; s < PF_PP_S; ++s) acc[s] = 0, aab[s] = 0;
     const int mT = n - lev - 2;
+    const int MT = ldc_lvl(D.ld + lev).M;
+    const long long baseT = pf_pk_base(D, lev), baseO = pf_pk_base(D, o0);
+    const __amdgpu_buffer_rsrc_t srcT = pf_rsrc(D.d4 + baseT), srcO = pf_rsrc(D.d4 + baseO);
     auto add = [&](int s, int x, bool live) {
         const long long v = live ? (long long)x : 0;
         acc[s] += v;
@@ -243,35 +242,35 @@ __global__ __launch_bounds__(256) void k_pf_ppush(PfDev D, int lev, int ngrp, in
         const int jo = outer, b1 = lev - jo;
         const int i = 1 + g * 64 + lane;
         if (1 + g * 64 > n - (lev + 3 + o0)) return;  // no lane has an interval of the shortest span
-        const int *rowA0 = pf_pk_row(D, lev, jo, 0);  // row h: + h*mT - h(h-1)/2
-        const int *rowB[PF_PP_S];
-        int Ms[PF_PP_S], offB[PF_PP_S];
+        // B of span s: level t2, block h1 (soffset h1 * 4 M, per step), row b1, position
+        // min(i, n - (lev+3+t2)) + jo + 1 (voffset, fixed per lane)
+        int voB[PF_PP_S], Ms4[PF_PP_S];
 #pragma unroll
         for (int s = 0; s < PF_PP_S; ++s) {
             const int t2 = imin(o0 + s, o0 + ns - 1);
-            rowB[s] = pf_pk_row(D, t2, 0, b1);  // block h1 added per step
-            Ms[s] = ldc_lvl(D.ld + t2).M;
-            offB[s] = imin(i, n - (lev + 3 + t2)) + jo + 1;
+            Ms4[s] = __builtin_amdgcn_readfirstlane(4 * ldc_lvl(D.ld + t2).M);  // uniform: a per-lane soffset would be a waterfall
+            voB[s] = (int)((unsigned)(4 * (pf_pk_base(D, t2) - baseO + pf_G(n - t2 - 2, b1))) +
+                           4u * (unsigned)(imin(i, n - (lev + 3 + t2)) + jo));
         }
-        // two steps per iteration, all 2 * (PF_PP_S + 1) loads in flight together (the second step of
-        // an odd tail re-reads the first and is masked)
-        for (int h1 = h_lo; h1 <= hmax; h1 += 2) {
-            int va[2], vb[2][PF_PP_S], hh[2];
-            hh[0] = h1;
-            hh[1] = imin(h1 + 1, hmax);
+        // U steps per iteration, all U * (PF_PP_S + 1) loads in flight together (the steps of a short
+        // tail re-read the last one and are masked)
+        for (int h1 = h_lo; h1 <= hmax; h1 += U) {
+            int va[U], vb[U][PF_PP_S], hh[U];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < U; ++u) hh[u] = imin(h1 + u, hmax);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
                 const int h = hh[u];
-                va[u] = pf_at(pf_uni(rowA0 + h * mT - ((h * (h - 1)) >> 1)), imin(i, mT - h));
+                va[u] = bld32(srcT, 4 * (imin(i, mT - h) - 1), 4 * (jo * MT + pf_G(mT, h)));
 #pragma unroll
                 for (int s = 0; s < PF_PP_S; ++s) {
                     const int t2 = imin(o0 + s, o0 + ns - 1), hc = imin(h, t2);
-                    vb[u][s] = pf_at(pf_uni(rowB[s] + (long long)hc * Ms[s]), offB[s]);
+                    vb[u][s] = bld32(srcO, voB[s], hc * Ms4[s]);
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const bool live = u == 0 || h1 + 1 <= hmax;
+            for (int u = 0; u < U; ++u) {
+                const bool live = h1 + u <= hmax;
 #pragma unroll
                 for (int s = 0; s < PF_PP_S; ++s) add(s, imul_wrap(va[u], vb[u][s]), live && s < ns && hh[u] <= o0 + s);
             }
@@ -289,33 +288,33 @@ __global__ __launch_bounds__(256) void k_pf_ppush(PfDev D, int lev, int ngrp, in
         const int l = lev + 4 + o0 + g * 64 + lane;
         if (lev + 4 + o0 + g * 64 > n) return;
         const int lc = imin(l, n);
-        const int *rowB0 = pf_pk_row(D, lev, a2, 0);
-        const int *rowA[PF_PP_S];
-        int Ms[PF_PP_S], offA[PF_PP_S];
+        // A of span s: level t1, block t1-h2 (soffset (t1-h2) * 4 M, per step), row a2, position
+        // max(1, lc - (lev+3+t1)) (voffset, fixed per lane)
+        int voA[PF_PP_S], Ms4[PF_PP_S];
 #pragma unroll
         for (int s = 0; s < PF_PP_S; ++s) {
             const int t1 = imin(o0 + s, o0 + ns - 1);
-            rowA[s] = pf_pk_row(D, t1, t1, a2);  // block t1-h2: minus h2*M per step
-            Ms[s] = ldc_lvl(D.ld + t1).M;
-            offA[s] = imax(1, lc - (lev + 3 + t1));
+            Ms4[s] = __builtin_amdgcn_readfirstlane(4 * ldc_lvl(D.ld + t1).M);
+            voA[s] = (int)((unsigned)(4 * (pf_pk_base(D, t1) - baseO + pf_G(n - t1 - 2, a2))) +
+                           4u * (unsigned)(imax(1, lc - (lev + 3 + t1)) - 1));
         }
-        for (int h2 = hmax; h2 >= h_lo; h2 -= 2) {
-            int vb[2], va[2][PF_PP_S], hh[2];
-            hh[0] = h2;
-            hh[1] = imax(h2 - 1, h_lo);
+        for (int h2 = hmax; h2 >= h_lo; h2 -= U) {  // U steps per iteration, as in part A
+            int vb[U], va[U][PF_PP_S], hh[U];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < U; ++u) hh[u] = imax(h2 - u, h_lo);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
                 const int h = hh[u];
-                vb[u] = pf_at(pf_uni(rowB0 + h * mT - ((h * (h - 1)) >> 1)), imax(1, imin(lc - h - lev - 2, mT - h)));
+                vb[u] = bld32(srcT, 4 * (imax(1, imin(lc - h - lev - 2, mT - h)) - 1), 4 * (a2 * MT + pf_G(mT, h)));
 #pragma unroll
                 for (int s = 0; s < PF_PP_S; ++s) {
                     const int t1 = imin(o0 + s, o0 + ns - 1), hc = imin(h, t1);
-                    va[u][s] = pf_at(pf_uni(rowA[s] - (long long)hc * Ms[s]), offA[s]);
+                    va[u][s] = bld32(srcO, voA[s], (t1 - hc) * Ms4[s]);
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const bool live = u == 0 || h2 - 1 >= h_lo;
+            for (int u = 0; u < U; ++u) {
+                const bool live = h2 - u >= h_lo;
 #pragma unroll
                 for (int s = 0; s < PF_PP_S; ++s) add(s, imul_wrap(va[u][s], vb[u]), live && s < ns && hh[u] <= o0 + s);
             }
@@ -1086,8 +1085,14 @@ extern "C" int ccjk_pf_ppush(const PfDev *D, int lev, void *stream) {
     int npairs = 0;
     for (int c = 0; c < nch; ++c) npairs += (imin((c + 1) * PF_PP_S, nmax) + hs_len - 1) / hs_len;
     const int blocksA = (npairs * ngrp * (lev + 1) + 3) / 4;
-    hipLaunchKernelGGL(k_pf_ppush, dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *D, lev, ngrp, npairs,
-                       hs_len, blocksA);
+    // split steps in flight per wave (CCJ_PF_PP_STEPS, default 4; 2 for the A/B)
+    static const int steps = getenv("CCJ_PF_PP_STEPS") ? atoi(getenv("CCJ_PF_PP_STEPS")) : 4;
+    if (steps >= 4)
+        hipLaunchKernelGGL((k_pf_ppush<4>), dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *D, lev, ngrp,
+                           npairs, hs_len, blocksA);
+    else
+        hipLaunchKernelGGL((k_pf_ppush<2>), dim3((unsigned)(2 * blocksA)), dim3(256), 0, (hipStream_t)stream, *D, lev, ngrp,
+                           npairs, hs_len, blocksA);
     return (int)hipGetLastError();
 }
 

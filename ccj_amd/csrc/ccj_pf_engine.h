@@ -39,6 +39,9 @@ constexpr int PF_ILW = CCJ_PF_ILW;   // k_pf_iloop: window terms per round (mult
                                      // weight rows carry PF_ILW doubles of tail padding
 static_assert(PF_ILW % 4 == 0 && PF_ILW >= 4, "CCJ_PF_ILW: window_row reads whole groups of 4 terms");
 
+// k_pf_ppush: spans per wave = consecutive partner levels a wave reads through one buffer resource
+constexpr int PF_PP_S = 8;
+
 struct PfLvl {
     long long lb;  // element offset of level t
     long long C;   // cells of one matrix at level t

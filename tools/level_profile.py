@@ -9,7 +9,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ccj_amd import W_final, lib  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-r = random.Random(5)
+SEED = int(os.environ.get("CCJ_PROFILE_SEED", "5"))
+r = random.Random(SEED)
 seq = "".join(r.choice("ACGU") for _ in range(n))
 wf = W_final(seq, 2, params="Turner04")
 wf.ccj()
@@ -26,7 +27,7 @@ if os.environ.get("CCJ_PROFILE_DUMP"):
     _lv = (ctypes.c_double * n)()
     _L.ccj_level_times(wf._h, _lv, None, n)
     with open(os.environ["CCJ_PROFILE_DUMP"], "w") as f:
-        json.dump({"n": n, "seed": 5, "params": "Turner04", "fill_ms": fills[-1], "level_ms": list(_lv)[:n - 2]}, f)
+        json.dump({"n": n, "seed": SEED, "params": "Turner04", "fill_ms": fills[-1], "level_ms": list(_lv)[:n - 2]}, f)
 # one more fold with a marker pair around every launch for the per-kernel breakdown (slower fill)
 wf.set_timing(2)
 wf.ccj()
