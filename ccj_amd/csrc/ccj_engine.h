@@ -118,11 +118,13 @@ __host__ __device__ __forceinline__ int shard_ceil(int x, int G, int r) {
 // slices:
 //   part XCH_EDGE: the rank's blocks with a % SHARD_GRP == SHARD_GRP-1 (own index o % SHARD_GRP ==
 //     SHARD_GRP-1): of level t, another rank's level t+1 reads only these (its group's first block a
-//     reads block a-1 at split step 1, pseudo_loop.cc:357-362), plus the span tail (XCH_DTAIL: span t,
+//     reads block a-1 at split step 1, pseudo_loop.cc:357-362); then the tail: the P tail (XCH_PTAIL:
+//     this rank's partials of P(t+1), pushed after level t-2) and the span tail (XCH_DTAIL: span t,
 //     which level t+1 reads).  Gathered on the level stream: the critical path.
 //   part XCH_BULK: the rank's other blocks (read from level t+2 on, and by k_iloop(t+3) / k_ppush(t)),
-//     plus the P tail (XCH_PTAIL: this rank's partials of P(t+2)).  Gathered on a side stream while
-//     level t+1 runs.
+//     no tail.  Gathered on a side stream while level t+1 runs.
+// The partials of P(n-1) (pushed after level n-4; no level n-2 carries them) travel alone after the
+// last level, as a slice of one P tail.
 // A part's slice: body [matrix x][part index k][cell c] of nmax blocks per matrix (nmax = the largest
 // rank's block count of that part at t), padded to 8 bytes, then the part's tail.  k_pack / k_unpack /
 // k_?tail_* and the host's buffer sizing use these; ccj_exchange_layout / ccj_exchange_index export
@@ -132,7 +134,7 @@ constexpr int XCH_DT_N = 10;  // span tail planes: V, Vt, P, WBP, WB, WPP, WP, W
 __host__ __device__ __forceinline__ long long xch_body(int nmax, int M) { return ((long long)22 * nmax * M + 3) & ~3LL; }
 __host__ __device__ __forceinline__ long long xch_ptail(int n) { return 4LL * (n + 1); }
 __host__ __device__ __forceinline__ long long xch_dtail(int n) { return 2LL * XCH_DT_N * (n + 1); }
-__host__ __device__ __forceinline__ long long xch_tail(int n, int part) { return part == XCH_EDGE ? xch_dtail(n) : xch_ptail(n); }
+__host__ __device__ __forceinline__ long long xch_tail(int n, int part) { return part == XCH_EDGE ? xch_ptail(n) + xch_dtail(n) : 0; }
 __host__ __device__ __forceinline__ long long xch_slice(int n, int nmax, int M, int part) { return xch_body(nmax, M) + xch_tail(n, part); }
 // part of own index o, its index inside the part, and back
 __host__ __device__ __forceinline__ int xch_part(int o) { return o % SHARD_GRP == SHARD_GRP - 1 ? XCH_EDGE : XCH_BULK; }

@@ -172,6 +172,9 @@ struct ccj_ctx {
     hipStream_t st = nullptr, st_copy = nullptr, st_p = nullptr, st_il = nullptr, st_d = nullptr;
     hipStream_t st_x = nullptr;          // band-sharded: the bulk part of each level's exchange
     std::vector<hipEvent_t> bulk_done;   // band-sharded: level t complete on this rank (bulk part unpacked)
+    // in-process group: this rank's bulk slice packed / the peers' bulk slices copied (reused every level;
+    // the group's barriers order each record before the peers' waits on it)
+    hipEvent_t ev_bpacked = nullptr, ev_bcopied = nullptr;
     bool join_diag = true;               // k_diag2d(t-1) after k_iloop(t) on st_il (one cross-stream wait per level)
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<hipEvent_t> pp_done; // band-sharded: this rank's P-term push of span sigma done (before the exchange)
@@ -1461,6 +1464,38 @@ static int local_allgather(ccj_ctx *c, int part, size_t slice, hipStream_t q) {
     return CCJ_OK;
 }
 
+// The bulk part of a level's exchange through the in-process group, without blocking the host: after
+// one barrier (every member has recorded its ev_bpacked for this level), each member's bulk slice is
+// copied on this member's side stream behind that member's ev_bpacked, and ev_bcopied marks the copies
+// (a member's next bulk pack waits for every member's ev_bcopied, bulk_start).  The level chain keeps
+// running meanwhile; only the edge part (local_allgather) synchronises the host with the level.
+static int local_bulk_gather(ccj_ctx *c, size_t slice) {
+    ccj_group *g = c->lgroup;
+    if (!g->barrier()) return set_err(c, CCJ_E_STATE, "local exchange: a group member failed");
+    std::lock_guard<std::mutex> lk(g->mu);
+    for (int r = 0; r < g->world; ++r) {
+        const ccj_ctx *p = g->members[r];
+        if (!p) {
+            g->broken = true;
+            g->cv.notify_all();
+            return set_err(c, CCJ_E_STATE, "local exchange: rank %d has no context", r);
+        }
+        HIPCHK(c, hipStreamWaitEvent(c->st_x, p->ev_bpacked, 0));
+        HIPCHK(c, hipMemcpyAsync(c->d_recv[XCH_BULK] + (size_t)r * slice, p->d_send[XCH_BULK], slice * sizeof(int16_t),
+                                 hipMemcpyDeviceToDevice, c->st_x));
+    }
+    HIPCHK(c, hipEventRecord(c->ev_bcopied, c->st_x));
+    return CCJ_OK;
+}
+// before this member's next bulk pack overwrites its send slice: every member's copies of it are done
+static int local_bulk_wait_copied(ccj_ctx *c) {
+    ccj_group *g = c->lgroup;
+    std::lock_guard<std::mutex> lk(g->mu);
+    for (int r = 0; r < g->world; ++r)
+        if (const ccj_ctx *p = g->members[r]) HIPCHK(c, hipStreamWaitEvent(c->st_x, p->ev_bcopied, 0));
+    return CCJ_OK;
+}
+
 // Everything that depends on the sequence itself (not only on n): the encoding, the pair-type,
 // hairpin and e_stP tables, and the k_iloop work items.  ccj_create runs it once, ccj_reset for
 // each new sequence of the same length (the allocations are reused).
@@ -1753,6 +1788,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     for (auto &e : c->pp_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
     c->bulk_done.resize(n + 1);
     for (auto &e : c->bulk_done) HIPCHK(cp, hipEventCreateWithFlags(&e, sync_fl));
+    HIPCHK(cp, hipEventCreateWithFlags(&c->ev_bpacked, sync_fl));
+    HIPCHK(cp, hipEventCreateWithFlags(&c->ev_bcopied, sync_fl));
     c->tev.resize(TEV_PER * (size_t)n + TEV_PER);
     for (auto &e : c->tev) HIPCHK(cp, hipEventCreate(&e));
 
@@ -2132,36 +2169,31 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
     };
     auto bulk_unpack = [&](int s) -> int {
         hipEvent_t *ev = &c->tev[TEV_PER * (size_t)s];
-        const int sig = s + 2;
         HIPCHK(c, (hipError_t)ccjk_unpack(&c->T, s, c->world, c->rank, XCH_BULK, c->xnmax[XCH_BULK][s], c->d_recv[XCH_BULK],
                                           part_slice(s, XCH_BULK), c->st_x));
-        if (s >= 1 && sig <= n - 1) {
-            HIPCHK(c, (hipError_t)ccjk_ptail_unpack(&c->T, sig, c->d_recv[XCH_BULK], part_slice(s, XCH_BULK), part_body(s, XCH_BULK),
-                                                    c->world, c->st_x));
-            HIPCHK(c, hipEventRecord(c->p_done[sig], c->st_x));  // P(sig) final on every rank
-        }
         if (c->level_timing == 2) HIPCHK(c, hipEventRecord(ev[10], c->st_x));
         HIPCHK(c, hipEventRecord(c->bulk_done[s], c->st_x));
         return CCJ_OK;
     };
     auto bulk_start = [&](int s) -> int {
         hipEvent_t *ev = &c->tev[TEV_PER * (size_t)s];
-        const int sig = s + 2;  // the P span whose partials ride this part (pushed after level s-1)
         HIPCHK(c, hipStreamWaitEvent(c->st_x, c->lev_done[s], 0));
-        if (c->level_timing == 2) HIPCHK(c, hipEventRecord(ev[9], c->st_x));
-        if (s >= 1 && sig <= n - 1) {
-            HIPCHK(c, hipStreamWaitEvent(c->st_x, c->pp_done[sig], 0));
-            HIPCHK(c, (hipError_t)ccjk_ptail_pack(&c->T, sig, c->d_send[XCH_BULK] + part_body(s, XCH_BULK), c->st_x));
+        if (c->lgroup) {
+            if (const int rc = local_bulk_wait_copied(c)) return rc;
         }
+        if (c->level_timing == 2) HIPCHK(c, hipEventRecord(ev[9], c->st_x));
         HIPCHK(c, (hipError_t)ccjk_pack(&c->T, s, c->world, c->rank, XCH_BULK, c->xnmax[XCH_BULK][s], c->d_send[XCH_BULK], c->st_x));
-        if (c->lgroup) return CCJ_OK;  // gathered and unpacked when the next level is enqueued (bulk_finish)
+        if (c->lgroup) {  // gathered and unpacked when the next level is enqueued (bulk_finish)
+            HIPCHK(c, hipEventRecord(c->ev_bpacked, c->st_x));
+            return CCJ_OK;
+        }
         if (const int rc = gather(s, XCH_BULK, c->st_x)) return rc;
         return bulk_unpack(s);
     };
     // the in-process group's bulk gather of level s, then what waits for level s to be complete
     auto bulk_finish = [&](int s) -> int {
         if (c->lgroup) {
-            if (const int rc = gather(s, XCH_BULK, c->st_x)) return rc;
+            if (const int rc = local_bulk_gather(c, part_slice(s, XCH_BULK))) return rc;
             if (const int rc = bulk_unpack(s)) return rc;
         }
         return after_level(s);
@@ -2235,16 +2267,27 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                     if (const int rc = bulk_finish(s - 1)) return rc;
                 }
                 HIPCHK(c, trec(6, st));  // timing mode 2: the edge exchange's share of the level span
-                // edge part: the rank's blocks a % 4 == 3 (all 22 matrices) and its intervals of span s
-                const size_t body = part_body(s, XCH_EDGE);
+                // edge part: the rank's blocks a % 4 == 3 (all 22 matrices), its partials of P(s+1)
+                // (pushed after level s-2, so a level of slack) and its intervals of span s
+                const size_t body = part_body(s, XCH_EDGE), dt_off = body + (size_t)xch_ptail(n);
+                const int sig = s + 1;
+                const bool ptail = sig >= 3 && sig <= n - 2;
+                if (ptail) {
+                    HIPCHK(c, hipStreamWaitEvent(st, c->pp_done[sig], 0));
+                    HIPCHK(c, (hipError_t)ccjk_ptail_pack(&c->T, sig, c->d_send[XCH_EDGE] + body, st));
+                }
                 HIPCHK(c, hipStreamWaitEvent(st, c->dg_done[s], 0));
-                HIPCHK(c, (hipError_t)ccjk_dtail_pack(&c->T, s, G, c->rank, c->d_send[XCH_EDGE] + body, st));
+                HIPCHK(c, (hipError_t)ccjk_dtail_pack(&c->T, s, G, c->rank, c->d_send[XCH_EDGE] + dt_off, st));
                 HIPCHK(c, (hipError_t)ccjk_pack(&c->T, s, G, c->rank, XCH_EDGE, c->xnmax[XCH_EDGE][s], c->d_send[XCH_EDGE], st));
                 if (const int rc = gather(s, XCH_EDGE, st)) return rc;
                 HIPCHK(c, (hipError_t)ccjk_unpack(&c->T, s, G, c->rank, XCH_EDGE, c->xnmax[XCH_EDGE][s], c->d_recv[XCH_EDGE],
                                                   part_slice(s, XCH_EDGE), st));
-                HIPCHK(c, (hipError_t)ccjk_dtail_unpack(&c->T, s, c->d_recv[XCH_EDGE], part_slice(s, XCH_EDGE), body, G, c->rank,
+                HIPCHK(c, (hipError_t)ccjk_dtail_unpack(&c->T, s, c->d_recv[XCH_EDGE], part_slice(s, XCH_EDGE), dt_off, G, c->rank,
                                                         st));
+                if (ptail) {
+                    HIPCHK(c, (hipError_t)ccjk_ptail_unpack(&c->T, sig, c->d_recv[XCH_EDGE], part_slice(s, XCH_EDGE), body, G, st));
+                    HIPCHK(c, hipEventRecord(c->p_done[sig], st));  // P(sig) final on every rank
+                }
             }
             HIPCHK(c, trec(5, st));
             if (c->overlap && c->h4 && !c->T.mat5) HIPCHK(c, (hipError_t)ccjk_mat5(&c->T, s, st));  // for the mirror copy
@@ -2257,6 +2300,24 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
         } else {
             if (xchg && s == c->nlev && s >= 1) {  // the last level's bulk part
                 if (const int rc = bulk_finish(s - 1)) return rc;
+            }
+            if (xchg && s == c->nlev && n - 1 >= 3) {
+                // the partials of P(n-1) (pushed after level n-4): no level n-2 carries them, so they
+                // travel alone, as a slice of one P tail in the edge buffers
+                const int sig = n - 1;
+                const size_t pslice = (size_t)xch_ptail(n);
+                HIPCHK(c, hipStreamWaitEvent(st, c->pp_done[sig], 0));
+                HIPCHK(c, (hipError_t)ccjk_ptail_pack(&c->T, sig, c->d_send[XCH_EDGE], st));
+                if (c->lgroup) {
+                    if (const int rc = local_allgather(c, XCH_EDGE, pslice, st)) return rc;
+                } else {
+                    if (!c->comm) return set_err(c, CCJ_E_STATE, "sharded context without ccj_comm_init");
+                    if (ncclAllGather(c->d_send[XCH_EDGE], c->d_recv[XCH_EDGE], pslice * sizeof(int16_t), ncclInt8, c->comm, st) !=
+                        ncclSuccess)
+                        return set_err(c, CCJ_E_COMM, "ncclAllGather (P tail) failed");
+                }
+                HIPCHK(c, (hipError_t)ccjk_ptail_unpack(&c->T, sig, c->d_recv[XCH_EDGE], pslice, 0, c->world, st));
+                HIPCHK(c, hipEventRecord(c->p_done[sig], st));
             }
             if (s + 3 < n && s + 3 >= 3) {
                 HIPCHK(c, (hipError_t)pterm_launch(c, s, c->st_p));
@@ -2881,7 +2942,7 @@ extern "C" int ccj_exchange_layout(int n, int t, int world, int part, long long 
     if (!out3 || world < 1 || t < 0 || n < 4 || t > n - 3 || (part != XCH_EDGE && part != XCH_BULK)) return CCJ_E_ARG;
     const int m = n - t - 2, M = m * (m + 1) / 2, nmax = xch_nmax(t, world, part);
     out3[0] = nmax;
-    out3[1] = xch_body(nmax, M);                // the part's tail: span t (edge) / P(t+2) partials (bulk)
+    out3[1] = xch_body(nmax, M);                // the part's tail (edge: P(t+1) partials, then span t; bulk: none)
     out3[2] = xch_slice(n, nmax, M, part);      // slice elements
     return CCJ_OK;
 }
@@ -2986,6 +3047,9 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
             fprintf(stderr, "ccj_destroy: a group member is still copying after 120 s; leaking its source buffer\n");
             leak_send = true;
         }
+        // the peers' asynchronous bulk copies (local_bulk_gather) from this member's send slice
+        for (ccj_ctx *p : g->members)
+            if (p && p->st_x) hipStreamSynchronize(p->st_x);
         c->lgroup = nullptr;
     }
     hipSetDevice(c->device);
@@ -3052,6 +3116,8 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     for (auto e : c->p_done) hipEventDestroy(e);
     for (auto e : c->pp_done) hipEventDestroy(e);
     for (auto e : c->bulk_done) hipEventDestroy(e);
+    if (c->ev_bpacked) hipEventDestroy(c->ev_bpacked);
+    if (c->ev_bcopied) hipEventDestroy(c->ev_bcopied);
     if (c->st_p) hipStreamDestroy(c->st_p);
     if (c->st_x) hipStreamDestroy(c->st_x);
     if (c->comm_b) ncclCommDestroy(c->comm_b);

@@ -159,8 +159,8 @@ int  ccj_host_timing(const ccj_ctx *ctx, double *out3);
 int  ccj_level_times(const ccj_ctx *ctx, double *level_ms, double *diag_ms, int cap);
 /* Band-sharded contexts in timing mode 2, per level (0 elsewhere; either pointer may be NULL):
  * edge_ms[t] = the edge part's share of the level span on the level stream (from the end of the
- * level's launches to the end of its unpack: the wait for span t, pack, all-gather, unpack); bulk_ms[t]
- * = the bulk part on its side stream (from the level's end: the wait for the P tail, pack, all-gather,
+ * level's launches to the end of its unpack: the waits for the P and span tails, pack, all-gather,
+ * unpack); bulk_ms[t] = the bulk part on its side stream (from the level's end: pack, all-gather,
  * unpack), which overlaps the next level. */
 int  ccj_exchange_times(const ccj_ctx *ctx, double *edge_ms, double *bulk_ms, int cap);
 int  ccj_iloop_times(const ccj_ctx *ctx, double *iloop_ms, int cap);
@@ -184,11 +184,12 @@ int  ccj_shard_blocks(int n, int t, int world, int rank, int *a_out, int cap);
 /* Per-matrix element count C_t of level t and the a-block size M_t (the same for every world). */
 int  ccj_level_layout(int n, int t, int world, long long *C, int *M);
 /* The level-t exchange is two all-gathers: part 0 ("edge") = each rank's blocks
- * a % 4 == 3, the only cells of level t another rank's level t+1 reads, + span t (tail), on the level
- * stream; part 1 ("bulk") = the other blocks + the rank's P(t+2) partials (tail), on a side stream
- * that overlaps level t+1.  ccj_exchange_layout (host helper, no GPU; the geometry k_pack / k_unpack
- * use), in int16 elements: out3 = {nmax (the largest rank's block count of the part), tail offset,
- * slice size}.  The body is [matrix][part index][cell] of nmax blocks per matrix. */
+ * a % 4 == 3, the only cells of level t another rank's level t+1 reads, then its P(t+1) partials
+ * (4(n+1) elements) and span t (20(n+1) elements), on the level stream; part 1 ("bulk") = the other
+ * blocks, no tail, on a side stream that overlaps level t+1.  (P(n-1)'s partials travel alone after
+ * the last level.)  ccj_exchange_layout (host helper, no GPU; the geometry k_pack / k_unpack use), in
+ * int16 elements: out3 = {nmax (the largest rank's block count of the part), tail offset, slice size}.
+ * The body is [matrix][part index][cell] of nmax blocks per matrix. */
 int  ccj_exchange_layout(int n, int t, int world, int part, long long *out3);
 /* which = 0: for each body element of rank's slice of the part, the level element (x*C + a*M + c)
  * packed there (-1: padding); which = 1: for each level element, its position in the part's
