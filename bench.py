@@ -516,8 +516,8 @@ def main(argv=None):
         if tk:
             folds = tk["launches"] / nlaunch  # the profiled command's folds
             for kn, kv in tj["kernels"].items():
-                if kn in ("k_level4d", "k_level4d_lead"):
-                    continue  # inside k_level4d_level
+                if kn.startswith("k_level4d"):
+                    continue  # the level chain: k_level4d_level (= k_level4d + k_level4d_lead), counted below
                 side_traffic[kn.split("<")[0]] = (kv["hbm_bytes_per_launch"], kv["launches"] / folds)
             fill_counter_bytes = sum(b * l for b, l in side_traffic.values())
 

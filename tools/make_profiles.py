@@ -41,8 +41,8 @@ def pmc(path, counter):
 
 
 def kname(full):
-    """'void k_level4d(ccj::DevTables, ...)' -> 'k_level4d'"""
-    return re.sub(r"^void ", "", full.split("(")[0]).strip()
+    """'void k_level4d(ccj::DevTables, ...)' -> 'k_level4d'; template arguments dropped ('k_ppush<8, 4>' -> 'k_ppush')"""
+    return re.sub(r"^void ", "", full.split("(")[0].split("<")[0]).strip()
 
 
 def level_spans(trace_csv):
