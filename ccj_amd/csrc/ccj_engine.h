@@ -33,12 +33,6 @@ constexpr int IE_U = 29;  // u1,u2 in [0,28] for pseudoknot interior loops (pseu
 constexpr int IL_B = CCJ_ILB;  // interior-loop candidates per load batch (k_iloop)
 constexpr int IL_CAP = (IE_U * IE_U + IL_B + 7) / 8 * 8;  // candidate-list capacity per pair (+ IL_B null tail)
 constexpr int IL_SEG = 64;   // per pair: seg[dt] = first list entry of source-level distance dt
-// k_iloop modes (ccj_kernels.hip): every candidate of level t / the fused two-level walk (level t and
-// its PL / PR partner cells of level t+1) / level t's remainder after a fused walk of level t-1
-constexpr int IL_NORMAL = 0, IL_FUSED = 1, IL_REM = 2;
-// IL_REM's short lists (k_build_il): per pair [PL | PR][IL_RCAP] entries (source distance 3, and u1 = 0 /
-// u2 = 0), IL_B null entries after the last, the count in ilrcnt[pair][PL | PR]
-constexpr int IL_RCAP = 72;
 
 // k_ppush: spans per wave, i.e. consecutive partner levels a wave reads through one buffer resource
 constexpr int PPUSH_S = 8;
@@ -223,8 +217,6 @@ struct DevTables {
     const uint32_t *items;         // k_iloop work items (role << 30 | f1 << 20 | f2 << 10 | chunk)
     int mat5;                      // 1: the 5 record-only matrices are stored in d4 too (band-sharded exchange)
     uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
-    uint2 *ilr;                    // [pair][2][IL_RCAP]: IL_REM's lists (PL, PR)
-    uint32_t *ilrcnt;              // [pair][2]
     int *err;                      // device error word
     // split-point sharing (above): levels [g_lo, g_hi) share; partial-record ring of SHARE_R
     // slots x SHARE_NACC x accC
@@ -271,7 +263,7 @@ extern "C" {
 int ccjk_init2d(const ccj::DevTables *T, void *stream);
 int ccjk_precompute_ie(const ccj::DevTables *T, void *stream);
 int ccjk_build_il(const ccj::DevTables *T, void *stream);
-int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, int G, int rank, int mode, void *stream);
+int ccjk_iloop(const ccj::DevTables *T, int t, long long first_item, int nitems, int G, int rank, void *stream);
 int ccjk_diag2d(const ccj::DevTables *T, int sigma, int G, int rank, void *stream);
 int ccjk_dtail_pack(const ccj::DevTables *T, int sigma, int G, int rank, int16_t *tail, void *stream);
 int ccjk_dtail_unpack(const ccj::DevTables *T, int sigma, const int16_t *recv, size_t slice, size_t off, int G, int rank,

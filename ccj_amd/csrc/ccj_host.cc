@@ -161,8 +161,6 @@ struct ccj_ctx {
     hipEvent_t ev_stage = nullptr;        // the uploads from the staging (and h_ioff) are done
     std::vector<long long> it_off;        // first item of (level t, shard r) at t*world + r
     uint32_t *d_ilseg = nullptr, *d_ilmseg = nullptr;
-    uint2 *d_ilr = nullptr;           // k_iloop IL_REM lists [pair][PL | PR][IL_RCAP]
-    uint32_t *d_ilrcnt = nullptr;     // their counts [pair][PL | PR]
     int *d2i = nullptr;       // 9 int 2-D arrays back to back: V WM WMv WMp P WBP WPP WB WP
     unsigned long long *d_pk = nullptr;  // P with its first split (k_pterm), [w][p]
     int *d_W = nullptr, *d_fpair = nullptr;  // device traceback outputs
@@ -178,9 +176,6 @@ struct ccj_ctx {
     // the group's barriers order each record before the peers' waits on it)
     hipEvent_t ev_bpacked = nullptr, ev_bcopied = nullptr;
     bool join_diag = true;               // k_diag2d(t-1) after k_iloop(t) on st_il (one cross-stream wait per level)
-    // k_iloop's two-level mode (even levels IL_FUSED, odd IL_REM; ccj_kernels.hip): unsharded fills and
-    // simulations (a level's partner cells are another block, maybe another rank's); CCJ_ILFUSE=0 disables
-    bool il_fuse = true;
     std::vector<hipEvent_t> p_done;  // P(sigma) reduced
     std::vector<hipEvent_t> pp_done; // band-sharded: this rank's P-term push of span sigma done (before the exchange)
     std::vector<double> lev_ms_v, diag_ms_v, il_ms_v, xch_ms_v, xbulk_ms_v, pp_ms_v;
@@ -1706,7 +1701,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         // (fill -0.25 ms at n=200 in 3/3 alternating runs); band-sharded fills with an exchange
         // partition each span instead, and the level-t exchange carries span t
         c->join_diag = !(c->world > 1 && !c->simulate);
-        c->il_fuse = !(c->world > 1 && !c->simulate) && !(getenv("CCJ_ILFUSE") && atoi(getenv("CCJ_ILFUSE")) == 0);
         const char *g = getenv("CCJ_SHARE_SPLITS");
         c->share = !(g && atoi(g) < 0) && !(opts && opts->share_splits < 0);
     }
@@ -1926,9 +1920,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
             HIPCHK(cp, hipMalloc(&c->d_ilmseg, pairs * IL_SEG * sizeof(uint32_t)));
             HIPCHK(cp, hipMemset(c->d_ilseg, 0, pairs * IL_SEG * sizeof(uint32_t)));
             HIPCHK(cp, hipMemset(c->d_ilmseg, 0, pairs * IL_SEG * sizeof(uint32_t)));
-            HIPCHK(cp, hipMalloc(&c->d_ilr, pairs * 2 * IL_RCAP * sizeof(uint2)));
-            HIPCHK(cp, hipMalloc(&c->d_ilrcnt, pairs * 2 * sizeof(uint32_t)));
-            HIPCHK(cp, hipMemset(c->d_ilrcnt, 0, pairs * 2 * sizeof(uint32_t)));
         }
     }
     HIPCHK(cp, hipMalloc(&c->d2i, A2_N * plane * sizeof(int)));
@@ -2023,8 +2014,6 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.mat5 = ((c->world > 1 && !c->simulate) || (getenv("CCJ_MAT5") && atoi(getenv("CCJ_MAT5")) != 0)) ? 1 : 0;
     T.ilseg = c->d_ilseg;
     T.ilmseg = c->d_ilmseg;
-    T.ilr = c->d_ilr;
-    T.ilrcnt = c->d_ilrcnt;
     T.err = c->d_err;
     T.split_target = c->split_target;
     T.g_lo = g_lo;
@@ -2248,9 +2237,7 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
             for (int r = 0; r < G; ++r) {  // every rank's launches in simulation, else this rank's
                 if (!c->simulate && r != c->rank) continue;
                 const size_t tr = (size_t)s * G + r;
-                // two-level mode: level s even streams its sources once for s and s+1, odd s adds the rest
-                const int mode = !c->il_fuse ? IL_NORMAL : s % 2 == 0 ? (s + 1 < c->nlev ? IL_FUSED : IL_NORMAL) : IL_REM;
-                HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[tr], (int)(c->it_off[tr + 1] - c->it_off[tr]), G, r, mode,
+                HIPCHK(c, (hipError_t)ccjk_iloop(&c->T, s, c->it_off[tr], (int)(c->it_off[tr + 1] - c->it_off[tr]), G, r,
                                                  c->st_il));
             }
             HIPCHK(c, trec(3, c->st_il));
@@ -3117,8 +3104,6 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     if (c->ev_res) hipEventDestroy(c->ev_res);
     hipFree(c->d_ilseg);
     hipFree(c->d_ilmseg);
-    hipFree(c->d_ilr);
-    hipFree(c->d_ilrcnt);
     hipFree(c->d2i);
     hipFree(c->d_pk);
     hipFree(c->d_W);

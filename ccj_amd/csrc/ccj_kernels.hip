@@ -587,7 +587,6 @@ __global__ __launch_bounds__(256) void k_ppush(DevTables T, int lev, int ngrp, i
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
     __shared__ int16_t es[IE_U][IE_U + 1];  // [u1][u2]: the window's energies
-    __shared__ uint32_t ep[IE_U][IE_U + 1];  // il: [u1][u2] the partner closing pairs' energies (lo: (p-1, q), hi: (p, q+1))
     __shared__ uint32_t vb[IE_U];            // [u1]: bit u2 = the candidate is kept
     const int n = T.n, rs = T.rs;
     const int p = blockIdx.x + 1, w = blockIdx.y, kind = blockIdx.z;
@@ -612,17 +611,6 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
                 if (u1 <= imin(w, MAXLOOP) - 2 && u2 <= imin(w - u1 - 6, MAXLOOP - 2) && T.pt[(dp - d) * rs + d] > 0) {
                     valid = true;
                     e = e_intP(T, u1, u2, p, q);
-                    // the same inner pair closed by (p-1, q) (window u1+1, u2) and by (p, q+1) (window
-                    // u1, u2+1): the candidates of the next level's cells k_iloop's fused mode serves
-                    // from this entry's partner load (PL: cell (i-1, j, k, l); PR: (i, j, k, l+1))
-                    int eL = INTERN_INF, eR = INTERN_INF;
-                    if (p >= 2 && T.pt[(size_t)(w + 1) * rs + p - 1] > 0 && u1 + 1 <= imin(w + 1, MAXLOOP) - 2 &&
-                        u2 <= imin(w + 1 - (u1 + 1) - 6, MAXLOOP - 2))
-                        eL = e_intP(T, u1 + 1, u2, p - 1, q);
-                    if (q + 1 <= n && T.pt[(size_t)(w + 1) * rs + p] > 0 && u1 <= imin(w + 1, MAXLOOP) - 2 &&
-                        u2 + 1 <= imin(w + 1 - u1 - 6, MAXLOOP - 2))
-                        eR = e_intP(T, u1, u2 + 1, p, q + 1);
-                    ep[u1][u2] = (uint32_t)(uint16_t)eL | (uint32_t)(uint16_t)eR << 16;
                 }
             } else {
                 const int d = p - 1 - u1, dp = q + 1 + u2;
@@ -643,35 +631,13 @@ __global__ __launch_bounds__(64) void k_build_il(DevTables T) {
         const int u1 = lane, u2 = dt - 2 - lane;
         const bool valid = dt >= 2 && u1 < IE_U && u2 >= 0 && u2 < IE_U && ((vb[u1] >> u2) & 1u);
         const unsigned long long mask = __ballot(valid);
-        // .y: il (kind 0) the partner energies (k_iloop's fused mode; its PL cross term 2*u1*dt is
-        // computed from .x), ilm the cross term
         if (valid)
             ent[cnt + __popcll(mask & ((1ull << lane) - 1))] =
-                make_uint2(((uint32_t)dt << 21) | ((uint32_t)u1 << 16) | (uint32_t)(uint16_t)es[u1][u2],
-                           kind ? (uint32_t)(2 * u1 * dt) : ep[u1][u2]);
+                make_uint2(((uint32_t)dt << 21) | ((uint32_t)u1 << 16) | (uint32_t)(uint16_t)es[u1][u2], (uint32_t)(2 * u1 * dt));
         cnt += __popcll(mask);
     }
     // null tail: dt 63 addresses the sentinel pad (32767), energy 32767 -> 65534, never below a clamped result
-    if (lane < IL_B) ent[cnt + lane] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, kind ? 0u : 0x7fff7fffu);
-    if (kind == 0) {
-        // IL_REM's lists: the candidates of a level t+1 cell no IL_FUSED entry of level t had: source
-        // distance 3, and u1 = 0 (PL, the closing pair's 5' side) / u2 = 0 (PR, its 3' side)
-        for (int r = 0; r < 2; ++r) {
-            uint2 *rl = T.ilr + (pidx * 2 + r) * IL_RCAP;
-            int rc = 0;
-            for (int dt = 3; dt < IL_SEG; ++dt) {
-                const int u1 = lane, u2 = dt - 2 - lane;
-                const bool valid = u1 < IE_U && u2 >= 0 && u2 < IE_U && ((vb[u1] >> u2) & 1u) && (dt == 3 || (r == 0 ? u1 == 0 : u2 == 0));
-                const unsigned long long mask = __ballot(valid);
-                if (valid)
-                    rl[rc + __popcll(mask & ((1ull << lane) - 1))] =
-                        make_uint2(((uint32_t)dt << 21) | ((uint32_t)u1 << 16) | (uint32_t)(uint16_t)es[u1][u2], 0x7fff7fffu);
-                rc += __popcll(mask);
-            }
-            if (lane < IL_B) rl[rc + lane] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0x7fff7fffu);
-            if (lane == 0) T.ilrcnt[pidx * 2 + r] = (uint32_t)rc;
-        }
-    }
+    if (lane < IL_B) ent[cnt + lane] = make_uint2((63u << 21) | (uint32_t)INTERN_INF, 0u);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -796,21 +762,14 @@ __device__ __forceinline__ int il_e(uint32_t x) { return (int)(int16_t)(x & 0xff
 // 64-cell chunks of its row (lane offsets lofs2 and lofs2b) and loads both partners of every
 // entry, so a list entry's decode and address cost is paid once per 128 cells; half as many
 // entries per batch keep the loads in flight (and the registers) at 2*IL_B.
-// CROSS: the partner offset's u1*dt cross term: IL_X_NONE (PR), IL_X_Y (PM: the entry's .y), IL_X_CALC
-// (PL: 2*u1*dt from the entry's .x, scalar).  FUSE (k_iloop's fused mode, PL / PR): each partner value
-// also serves the next level's cell whose closing pair is (i-1, j) (FUSE 1, energy lo16(.y)) or (k, l+1)
-// (FUSE 2, hi16(.y)), accumulated in the .z / .w results.
-constexpr int IL_X_NONE = 0, IL_X_Y = 1, IL_X_CALC = 2;
-__device__ __forceinline__ int il_e2(uint32_t y, int fuse) { return fuse == 1 ? (int)(int16_t)(y & 0xffffu) : (int)(int16_t)(y >> 16); }
-
-template <int CROSS, bool PMWIN, bool PAIR, int FUSE>
-__device__ __forceinline__ int4 il_scan(const DevTables &T, const uint2 *__restrict__ ent, int cnt,
+template <bool CROSS, bool PMWIN, bool PAIR>
+__device__ __forceinline__ int2 il_scan(const DevTables &T, const uint2 *__restrict__ ent, int cnt,
                                         __amdgpu_buffer_rsrc_t src, int Atab, int Btab, unsigned lofs2, int as, int bs,
                                         unsigned lofs2b, int asb, int bsb) {
     constexpr int NB = PAIR ? IL_B / 2 : IL_B;
-    int b1 = INF, b2 = INF, c1 = INF, c2 = INF;
+    int b1 = INF, b2 = INF;
     cnt = __builtin_amdgcn_readfirstlane(cnt);
-    if (cnt <= 0) return make_int4(b1, b2, c1, c2);
+    if (cnt <= 0) return make_int2(b1, b2);
     ent = uni_ptr(ent);
     // a batch of NB entries (8 or 16 bytes x NB) as ONE scalar load: s_load_dwordx16 / x8 (as NB
     // separate dwordx2 loads the compiler computed a 64-bit address per entry)
@@ -832,8 +791,7 @@ __device__ __forceinline__ int4 il_scan(const DevTables &T, const uint2 *__restr
             // 32-bit and wave-uniform, so it is the load's soffset and the lane's offset its voffset
             // (a 64-bit address per candidate cost a 64-bit VALU add and a third readlane)
             unsigned off = (unsigned)__builtin_amdgcn_readlane(Btab, u1) + (unsigned)__builtin_amdgcn_readlane(Atab, dt);
-            if (CROSS == IL_X_Y) off += E[u].y;
-            if (CROSS == IL_X_CALC) off += (unsigned)(2 * u1 * dt);
+            if (CROSS) off += E[u].y;
 #ifdef CCJ_DEBUG_BOUNDS
             {   // the partner must lie inside its copy (the null target is the pad in front of a level)
                 bool bad = false;
@@ -872,11 +830,6 @@ __device__ __forceinline__ int4 il_scan(const DevTables &T, const uint2 *__restr
             } else {
                 b1 = imin(b1, c);
                 if (PAIR) b2 = imin(b2, e + w[u]);
-                if (FUSE) {
-                    const int e2 = il_e2(E[u].y, FUSE);
-                    c1 = imin(c1, e2 + v[u]);
-                    if (PAIR) c2 = imin(c2, e2 + w[u]);
-                }
             }
         }
     };
@@ -908,7 +861,7 @@ __device__ __forceinline__ int4 il_scan(const DevTables &T, const uint2 *__restr
         reduce(Eb, vb, wb);
         e0 += NB;
     }
-    return make_int4(b1, b2, c1, c2);
+    return make_int2(b1, b2);
 }
 
 // The same minimum for a wave whose row has at most 32 cells: the wave is G groups of W lanes
@@ -923,25 +876,18 @@ __device__ __forceinline__ int bperm(int v, int l) { return __builtin_amdgcn_ds_
 #define CCJ_ILG_B 4
 #endif
 constexpr int ILG_B = CCJ_ILG_B;  // entries per lane per batch in the grouped walk (registers: 8 waves/SIMD)
-template <int CROSS, bool PMWIN, int FUSE>
-__device__ __forceinline__ int2 il_scan_g(const DevTables &T, const uint2 *__restrict__ ent, int cnt, __amdgpu_buffer_rsrc_t src,
-                                          int Atab, int Btab, unsigned lofs2, int as, int bs, int G, int W, int g, int rl) {
-    int b1 = INF, c1 = INF;
-    if (cnt <= 0) return make_int2(b1, c1);
-    // only the packed word is loaded (the cross term 2*u1*dt is recomputed): half the registers;
-    // the fused mode also loads the partner energies (.y)
+template <bool CROSS, bool PMWIN>
+__device__ __forceinline__ int il_scan_g(const DevTables &T, const uint2 *__restrict__ ent, int cnt, __amdgpu_buffer_rsrc_t src,
+                                         int Atab, int Btab, unsigned lofs2, int as, int bs, int G, int W, int g, int rl) {
+    int b1 = INF;
+    if (cnt <= 0) return b1;
+    // only the packed word is loaded (the cross term 2*u1*dt is recomputed): half the registers
     const uint32_t nul = (63u << 21) | (uint32_t)INTERN_INF;
-    auto fetch = [&](int e0, uint32_t *E, uint32_t *Y) {
+    auto fetch = [&](int e0, uint32_t *E) {
 #pragma unroll
         for (int u = 0; u < ILG_B; ++u) {
             const int e = e0 + g + G * u;
-            if (FUSE) {
-                const uint2 v = ent[imin(e, cnt - 1)];
-                E[u] = v.x;
-                Y[u] = e >= cnt ? 0x7fff7fffu : v.y;
-            } else {
-                E[u] = ent[imin(e, cnt - 1)].x;
-            }
+            E[u] = ent[imin(e, cnt - 1)].x;
             if (e >= cnt) E[u] = nul;
         }
     };
@@ -951,7 +897,7 @@ __device__ __forceinline__ int2 il_scan_g(const DevTables &T, const uint2 *__res
             const int dt = il_dt(E[u]), u1 = il_u1(E[u]);
             // per-lane entries: the offset from the wave's buffer base is per lane (voffset)
             unsigned off = (unsigned)bperm(Btab, u1) + (unsigned)bperm(Atab, dt) + lofs2;
-            if (CROSS != IL_X_NONE) off += (unsigned)(2 * u1 * dt);
+            if (CROSS) off += (unsigned)(2 * u1 * dt);
 #ifdef CCJ_DEBUG_BOUNDS
             if (off >= (unsigned)T.xspan || (dt != 63 && (dt < 2 || dt > 2 * MAXLOOP - 2))) {
                 if (atomicOr(T.err, 64) == 0) printf("k_iloop (grouped, G %d) OOB: dt %d u1 %d\n", G, dt, u1);
@@ -965,7 +911,7 @@ __device__ __forceinline__ int2 il_scan_g(const DevTables &T, const uint2 *__res
             v[u] = (int)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(src, (int)off, 0, 0);
         }
     };
-    auto reduce = [&](const uint32_t *E, const uint32_t *Y, const int *v) {
+    auto reduce = [&](const uint32_t *E, const int *v) {
 #pragma unroll
         for (int u = 0; u < ILG_B; ++u) {
             const int c = il_e(E[u]) + v[u];
@@ -974,7 +920,6 @@ __device__ __forceinline__ int2 il_scan_g(const DevTables &T, const uint2 *__res
                 b1 = imin(b1, c + (((u1 > as - 2) | (u2 > bs - 2)) ? INF : 0));
             } else {
                 b1 = imin(b1, c);
-                if (FUSE) c1 = imin(c1, il_e2(Y[u], FUSE) + v[u]);
             }
         }
     };
@@ -982,37 +927,34 @@ __device__ __forceinline__ int2 il_scan_g(const DevTables &T, const uint2 *__res
     // loads return in order, so waiting for batch k+1's entries also waits for batch k's partners;
     // issuing k+1's partners together with k+2's entries keeps two loads per lane in flight
     // across each wait instead of one.
-    uint32_t Ea[ILG_B], Eb[ILG_B], Ya[ILG_B], Yb[ILG_B];
+    uint32_t Ea[ILG_B], Eb[ILG_B];
     int va[ILG_B], vb[ILG_B];
     const int stepE = G * ILG_B;
-    fetch(0, Ea, Ya);
+    fetch(0, Ea);
     issue(Ea, va);
-    fetch(stepE, Eb, Yb);
+    fetch(stepE, Eb);
     int e0 = stepE;
 #pragma unroll 1
     while (true) {
         if (e0 >= cnt) {
-            reduce(Ea, Ya, va);
+            reduce(Ea, va);
             break;
         }
         issue(Eb, vb);
-        reduce(Ea, Ya, va);
-        fetch(e0 + stepE, Ea, Ya);
+        reduce(Ea, va);
+        fetch(e0 + stepE, Ea);
         e0 += stepE;
         if (e0 >= cnt) {
-            reduce(Eb, Yb, vb);
+            reduce(Eb, vb);
             break;
         }
         issue(Ea, va);
-        reduce(Eb, Yb, vb);
-        fetch(e0 + stepE, Eb, Yb);
+        reduce(Eb, vb);
+        fetch(e0 + stepE, Eb);
         e0 += stepE;
     }
-    for (int off = W; off < 64; off <<= 1) {
-        b1 = imin(b1, __shfl_xor(b1, off));
-        if (FUSE) c1 = imin(c1, __shfl_xor(c1, off));
-    }
-    return make_int2(b1, c1);
+    for (int off = W; off < 64; off <<= 1) b1 = imin(b1, __shfl_xor(b1, off));
+    return b1;
 }
 
 // Lane groups for a row of nact cells: W lanes per group (one per cell, W >= nact, a power of two
@@ -1044,15 +986,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t il_src(const int16_t *base) {
 // one wave per work item: a closing pair that can pair and up to IL_CW (two 64-lane chunks) of
 // its cells (ccj_items.h, built by k_items in enumeration order)
 constexpr int IL_WPB = 4;  // waves (consecutive items) per k_iloop workgroup (1, 2, 8, 16 measured +3.6 ... +9 ms)
-// Two-level mode (k_iloop(t) with mode IL_FUSED, then k_iloop(t+1) with IL_REM; unsharded fills): the
-// cell (i-1, j, k, l) of level t+1 (PL) or (i, j, k, l+1) (PR) reads the same source cells as (i, j, k, l)
-// of level t, one u1 (PL) / u2 (PR) further out (pseudo_loop.cc:694-700, 729-735), so a source level is
-// streamed once for two target levels: IL_FUSED walks the list of (i, j) / (k, l), min-reducing every
-// partner value with the entry's own energy (level t) and with its partner energy (k_build_il, .y) into
-// the level t+1 cell's slot; IL_REM then adds, per level t+1 cell, only the candidates no level-t entry
-// had: source distance 3 (level t-2, not yet written when IL_FUSED ran) and u1 = 0 (PL) / u2 = 0 (PR).
-__global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long long first, int nitems, int G_SH, int rank,
-                                                       int mode) {
+__global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long long first, int nitems, int G_SH, int rank) {
     TL_STAMP(t >= L_ + 1 && t <= L_ + 3 ? 2 + t - L_ - 1 : -1);
     TL_META(t);
     const int n = T.n, rs = T.rs, m = n - t - 2;
@@ -1073,10 +1007,6 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
     if (role == 0) {
         // PL: wave = (a, i, h-chunk), lanes h; closing pair (i, j)
         const int a = f1, i = f2, len = m - i + 1, h0 = zc * IL_CW;
-        const int j = i + a;
-        // IL_REM on a cell whose level t-1 partner (the pair (i+1, j)) had no IL_FUSED walk: the whole list
-        const bool partner = mode == IL_REM && a - 1 >= 6 && T.pt[(size_t)(a - 1) * rs + i + 1] > 0;
-        const int md = mode == IL_REM && !partner ? IL_NORMAL : mode;
         const ILGroups lg = il_groups(imin(64, len - h0), lane);
         const int G = lg.G, gq = lg.gq;
         const bool pair = len - h0 > 64;  // a second 64-cell chunk (wave-uniform)
@@ -1095,26 +1025,12 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
                                         (long long)i * lane + lane - 1 - BIAS));
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
         if (lane == 63) Atab = -B0;
-        // IL_REM walks the pair's short remainder list instead (k_build_il)
-        const int e0 = md == IL_REM ? 0 : (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
-        const uint2 *le = md == IL_REM ? T.ilr + (pidx * 2 + 0) * IL_RCAP : T.il + pidx * IL_CAP + e0;
-        const int lc = md == IL_REM ? (int)ld_const(T.ilrcnt + pidx * 2 + 0)
-                                    : ILHALF((int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0);
-        int4 bm;
-        if (md == IL_FUSED) {
-            if (G > 1) {
-                const int2 g2 = il_scan_g<IL_X_CALC, false, 1>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl);
-                bm = make_int4(g2.x, INF, g2.y, INF);
-            } else {
-                bm = pair ? il_scan<IL_X_CALC, false, true, 1>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
-                          : il_scan<IL_X_CALC, false, false, 1>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
-            }
-        } else {
-            bm = G > 1  ? make_int4(il_scan_g<IL_X_CALC, false, 0>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl).x,
-                                    INF, INF, INF)
-               : pair ? il_scan<IL_X_CALC, false, true, 0>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
-                      : il_scan<IL_X_CALC, false, false, 0>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
-        }
+        const int e0 = (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
+        const uint2 *le = T.il + pidx * IL_CAP + e0;
+        const int lc = ILHALF((int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0);
+        const int2 bm = G > 1  ? make_int2(il_scan_g<true, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl), INF)
+                        : pair ? il_scan<true, false, true>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
+                               : il_scan<true, false, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
         if ((act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) || (actb && hb >= m)) {
             atomicOr(T.err, 128);
@@ -1122,32 +1038,14 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         }
 #endif
         int16_t *dl = T.d4 + Lt.lb + (long long)PL * Lt.C + a * Lt.M + i - 1;
-        const int sl = h * m - ((h * (h - 1)) >> 1), slb = hb * m - ((hb * (hb - 1)) >> 1);
-        if (md == IL_REM) {  // min with the partial IL_FUSED(t-1) left in the slot
-            if (act && gq == 0) dl[sl] = (int16_t)clamp_store(imin(bm.x, (int)dl[sl]));
-            if (actb) dl[slb] = (int16_t)clamp_store(imin(bm.y, (int)dl[slb]));
-        } else {
-            if (act && gq == 0) dl[sl] = (int16_t)clamp_store(bm.x);
-            if (actb) dl[slb] = (int16_t)clamp_store(bm.y);
-        }
-        if (md == IL_FUSED && i >= 2 && T.pt[(size_t)(a + 1) * rs + i - 1] > 0) {
-            // the partner cell (i-1, j, k, l) of level t+1: block a+1, row h, position i-1 (m - 1 rows)
-            const LvlDev L1 = T.ld[t + 1];
-            const int m1 = m - 1;
-            int16_t *d1 = T.d4 + L1.lb + (long long)PL * L1.C + (a + 1) * L1.M + i - 2;
-            if (act && gq == 0) d1[h * m1 - ((h * (h - 1)) >> 1)] = (int16_t)clamp_store(bm.z);
-            if (actb) d1[hb * m1 - ((hb * (hb - 1)) >> 1)] = (int16_t)clamp_store(bm.w);
-        }
-        (void)j;
+        if (act && gq == 0) dl[h * m - ((h * (h - 1)) >> 1)] = (int16_t)clamp_store(bm.x);
+        if (actb) dl[hb * m - ((hb * (hb - 1)) >> 1)] = (int16_t)clamp_store(bm.y);
     } else if (role == 1) {
         // PR: wave = (a, q, i-chunk), lanes i; closing pair (k, l), q = i+h-1 = k-a-3
         const int a = f1, q = f2;
         const int b = t - a;
         const int k = q + a + 3;
         const int i0 = zc * IL_CW;
-        // IL_REM on a cell whose level t-1 partner (the pair (k, l-1)) had no IL_FUSED walk: the whole list
-        const bool partner = mode == IL_REM && b - 1 >= 6 && T.pt[(size_t)(b - 1) * rs + k] > 0;
-        const int md = mode == IL_REM && !partner ? IL_NORMAL : mode;
         const ILGroups lg = il_groups(imin(64, q + 1 - i0), lane);
         const int G = lg.G, gq = lg.gq;
         const bool pair = q + 1 - i0 > 64;
@@ -1164,26 +1062,12 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         if (lvl_ok) Atab = (int)(unsigned)(2 * (T.ldx[tl].lbx - xb + T.ld[tl].C + (long long)a * T.ld[tl].M));
         const int B0 = __builtin_amdgcn_readlane(Btab, 0);
         if (lane == 63) Atab = -B0;
-        // IL_REM walks the pair's short remainder list instead (k_build_il)
-        const int e0 = md == IL_REM ? 0 : (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
-        const uint2 *le = md == IL_REM ? T.ilr + (pidx * 2 + 1) * IL_RCAP : T.il + pidx * IL_CAP + e0;
-        const int lc = md == IL_REM ? (int)ld_const(T.ilrcnt + pidx * 2 + 1)
-                                    : ILHALF((int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0);
-        int4 bm;
-        if (md == IL_FUSED) {
-            if (G > 1) {
-                const int2 g2 = il_scan_g<IL_X_NONE, false, 2>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl);
-                bm = make_int4(g2.x, INF, g2.y, INF);
-            } else {
-                bm = pair ? il_scan<IL_X_NONE, false, true, 2>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
-                          : il_scan<IL_X_NONE, false, false, 2>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
-            }
-        } else {
-            bm = G > 1  ? make_int4(il_scan_g<IL_X_NONE, false, 0>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl).x,
-                                    INF, INF, INF)
-               : pair ? il_scan<IL_X_NONE, false, true, 0>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
-                      : il_scan<IL_X_NONE, false, false, 0>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
-        }
+        const int e0 = (int)ld_const(T.ilseg + pidx * IL_SEG + 3);
+        const uint2 *le = T.il + pidx * IL_CAP + e0;
+        const int lc = ILHALF((int)ld_const(T.ilseg + pidx * IL_SEG + IL_SEG - 1) - e0);
+        const int2 bm = G > 1  ? make_int2(il_scan_g<false, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, G, lg.W, gq, lg.rl), INF)
+                        : pair ? il_scan<false, false, true>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, lofs2b, 0, 0)
+                               : il_scan<false, false, false>(T, le, lc, src, Atab, Btab, lofs2, 0, 0, 0u, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
         if ((act && (a < 0 || a > t || h < 0 || h >= m || i < 1 || i > m - h)) || (actb && (hb < 0 || ib > m - hb))) {
             atomicOr(T.err, 128);
@@ -1191,23 +1075,8 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         }
 #endif
         int16_t *dr = T.d4 + Lt.lb + (long long)PR * Lt.C + a * Lt.M;
-        const int sl = h * m - ((h * (h - 1)) >> 1) + i - 1, slb = hb * m - ((hb * (hb - 1)) >> 1) + ib - 1;
-        if (md == IL_REM) {  // min with the partial IL_FUSED(t-1) left in the slot
-            if (act && gq == 0) dr[sl] = (int16_t)clamp_store(imin(bm.x, (int)dr[sl]));
-            if (actb) dr[slb] = (int16_t)clamp_store(imin(bm.y, (int)dr[slb]));
-        } else {
-            if (act && gq == 0) dr[sl] = (int16_t)clamp_store(bm.x);
-            if (actb) dr[slb] = (int16_t)clamp_store(bm.y);
-        }
-        if (md == IL_FUSED && T.pt[(size_t)(b + 1) * rs + k] > 0) {
-            // the partner cell (i, j, k, l+1) of level t+1: block a, row h, position i (m - 1 rows),
-            // present while i + h <= m - 1
-            const LvlDev L1 = T.ld[t + 1];
-            const int m1 = m - 1;
-            int16_t *d1 = T.d4 + L1.lb + (long long)PR * L1.C + a * L1.M + i - 1;
-            if (act && gq == 0 && i + h <= m1) d1[h * m1 - ((h * (h - 1)) >> 1)] = (int16_t)clamp_store(bm.z);
-            if (actb && ib + hb <= m1) d1[hb * m1 - ((hb * (hb - 1)) >> 1) + 64] = (int16_t)clamp_store(bm.w);
-        }
+        if (act && gq == 0) dr[h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(bm.x);
+        if (actb) dr[hb * m - ((hb * (hb - 1)) >> 1) + ib - 1] = (int16_t)clamp_store(bm.y);
     } else {
         // PM: wave = (h, j, a-chunk), lanes a; pair (j, k), per-lane window u1 <= a-2, u2 <= b-2
         const int h = f1, j = f2;
@@ -1239,9 +1108,9 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
         const int cnt = (int)ld_const(T.ilmseg + pidx * IL_SEG + imin(t - 1, IL_SEG - 1));
         const int e0 = (int)ld_const(T.ilmseg + pidx * IL_SEG + 3);
         const uint2 *le = T.ilm + pidx * IL_CAP + e0;
-        const int4 bm = G > 1  ? make_int4(il_scan_g<IL_X_Y, true, 0>(T, le, ILHALF(cnt - e0), src, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl).x, INF, INF, INF)
-                        : pair ? il_scan<IL_X_Y, true, true, 0>(T, le, ILHALF(cnt - e0), src, Atab, Btab, lofs2, as, t - as, lofs2b, ab, t - ab)
-                               : il_scan<IL_X_Y, true, false, 0>(T, le, ILHALF(cnt - e0), src, Atab, Btab, lofs2, as, t - as, 0u, 0, 0);
+        const int2 bm = G > 1  ? make_int2(il_scan_g<true, true>(T, le, ILHALF(cnt - e0), src, Atab, Btab, lofs2, as, t - as, G, lg.W, gq, lg.rl), INF)
+                        : pair ? il_scan<true, true, true>(T, le, ILHALF(cnt - e0), src, Atab, Btab, lofs2, as, t - as, lofs2b, ab, t - ab)
+                               : il_scan<true, true, false>(T, le, ILHALF(cnt - e0), src, Atab, Btab, lofs2, as, t - as, 0u, 0, 0);
 #ifdef CCJ_DEBUG_BOUNDS
         if ((act && (a < 0 || a > t || h < 0 || h >= m || (j - a) < 1 || (j - a) > m - h)) ||
             (actb && (ab < 0 || ab > t || (j - ab) < 1 || (j - ab) > m - h))) {
@@ -2164,14 +2033,13 @@ extern "C" int ccjk_build_il(const DevTables *T, void *stream) {
     return (int)hipGetLastError();
 }
 
-extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int nitems, int G, int rank, int mode, void *stream) {
+extern "C" int ccjk_iloop(const DevTables *T, int t, long long first_item, int nitems, int G, int rank, void *stream) {
 #ifdef CCJ_ABLATE_ILOOP
     return 0;
 #endif
     if (nitems <= 0) return 0;
-    if (mode < IL_NORMAL || mode > IL_REM || (mode == IL_FUSED && t + 1 >= T->nlev)) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(k_iloop, dim3((unsigned)((nitems + IL_WPB - 1) / IL_WPB)), dim3(64 * IL_WPB), 0, (hipStream_t)stream, *T, t, first_item,
-                       nitems, G, rank, mode);
+                       nitems, G, rank);
     return (int)hipGetLastError();
 }
 
