@@ -7,7 +7,8 @@ constant clock (s_memrealtime) at entry and exit; so does every wave of the side
 level's window ("window": resident waves per kernel family in 20 bins from the plain launch's first start
 to the leader launch's last end).
 
-usage: CCJ_LIB_VARIANT=tl python tools/wg_timeline.py [n] [level ...]  -> one JSON line per level:
+usage: CCJ_LIB_VARIANT=tl python tools/wg_timeline.py [n] [level ...]  -> one JSON line per level
+       (or [n] all: every level, one fold each, compact figures: spans, mean resident waves per family):
   span: first wave start -> last wave end of each launch (us)
   ablk_finish: per a-block, when its last wave ended (us from the plain launch's first start), and its scan roles
   busy: the number of waves resident over time in 20 bins per launch (a level's tail shows as a falling count)
@@ -101,9 +102,35 @@ def analyse(t, plain, lead):
     return res
 
 
+def summary(t, kinds):
+    """Compact per-level figures for a whole-fold scan (usage: ... n all): the level's span, its two
+    launches' spans, and the machine's mean resident waves per family over the level (wave-us / span)."""
+    plain, lead = kinds[0], kinds[1]
+    if not plain and not lead:
+        return None
+    lo = min(w[0] for w in plain + lead)
+    hi = max(w[1] for w in plain + lead)
+    span = (hi - lo) * TICK_US
+    out = {"level": t, "span_us": round(span, 1)}
+    for name, ws in zip(FAMILIES, kinds):
+        if not ws:
+            continue
+        wus = sum(max(0, min(w[1], hi) - max(w[0], lo)) for w in ws) * TICK_US
+        out[name + "_mean_waves"] = round(wus / span, 1) if span > 0 else 0
+    for name, ws in (("plain", plain), ("lead", lead)):
+        if ws:
+            out[name + "_span_us"] = round((max(w[1] for w in ws) - min(w[0] for w in ws)) * TICK_US, 1)
+            work = [w for w in ws if w[2] != 0xFFFFFFFF and not (w[2] >> 20) & 1]
+            if work:
+                out[name + "_wave_us_max"] = round(max((w[1] - w[0]) * TICK_US for w in work), 1)
+                out[name + "_wave_us_mean"] = round(sum((w[1] - w[0]) * TICK_US for w in work) / len(work), 1)
+    return out
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-    levels = [int(x) for x in sys.argv[2:]] or [60, 100, 140]
+    scan_all = len(sys.argv) > 2 and sys.argv[2] == "all"
+    levels = list(range(n - 2)) if scan_all else ([int(x) for x in sys.argv[2:]] or [60, 100, 140])
     L = lib()
     L.ccjk_tl_arm.argtypes = [ctypes.c_int]
     L.ccjk_tl_read.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
@@ -117,6 +144,12 @@ def main():
             raise RuntimeError("ccjk_tl_arm failed")
         wf.ccj()
         kinds = [waves_of(L, k, cap) for k in range(L.ccjk_tl_kinds())]
+        if scan_all:
+            sm = summary(t, kinds)
+            if sm:
+                sm["fill_ms"] = wf.timing()["fill_ms"]
+                print(json.dumps(sm), flush=True)
+            continue
         res = analyse(t, kinds[0], kinds[1])
         lo = min(w[0] for w in kinds[0] + kinds[1])
         hi = max(w[1] for w in kinds[0] + kinds[1])
