@@ -57,14 +57,16 @@ def num_cells(n):
     return m * (m - 1) * (m - 2) * (m - 3) // 24
 
 
-def footprint_gb(n):
-    """Device memory of one context: 4-D matrices, loop records, interior-loop
-    copies, candidate lists, the sharing ring and the 2-D tables."""
+def footprint_gb(n, sharded=False):
+    """Device memory of one context: 4-D matrices (17 stored per level, all 22 when
+    band-sharded), loop records, interior-loop copies, candidate lists, the sharing ring and the 2-D
+    tables."""
     cells = num_cells(n)
+    nm4 = 22 if sharded else 17
     maxc = max(((t + 1) * ((n - t - 2) * (n - t - 1) // 2) for t in range(max(n - 2, 1))), default=0)
     pmx = 2 * sum((n - t - 2) * n * (t + 1) for t in range(max(n - 2, 0)))
     plane = (n + 1) * (n + 2)
-    return (44 * cells + 48 * cells + 4 * cells + pmx + 320 * maxc + 2 * 841 * plane + 2 * 848 * 8 * plane) / 1e9
+    return (2 * nm4 * cells + 48 * cells + 4 * cells + pmx + 320 * maxc + 2 * 841 * plane + 2 * 848 * 8 * plane) / 1e9
 
 
 def rank_seed(base, rank, world, step, distinct):

@@ -68,7 +68,7 @@ struct DV {
         const LvlDev L = T.ld[t];
         const long long cell = (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) + i - 1;
         if (!T.mat5 && rec_only(x)) return rec_get(T, x, L, cell);  // record-only matrix (ccj_engine.h)
-        return (int)T.d4[L.lb + (long long)x * L.C + cell];
+        return (int)T.d4[L.lb + (long long)mslot(x) * L.C + cell];
     }
     __device__ __forceinline__ bool can_pair(int i, int j) const { return (j - i > TURN) && pr(i, j) > 0; }  // pseudo_loop.hh:131-135
     // pseudo_loop.cc:822-840 (lrint = round-half-even in double)

@@ -26,6 +26,24 @@ enum Mat4 {
     PMmloop00, PMmloop01, PMmloop10, POmloop00, POmloop01, POmloop10
 };
 
+// The 5 matrices no fill kernel reads back as matrices (rec_get, below) and the 17 that d4 stores.
+__host__ __device__ constexpr bool rec_only(int x) {
+    return x == PLmloop00 || x == PMmloop00 || x == POmloop00 || x == PfromMprime || x == PRmloop00;
+}
+constexpr int NMAT_REC = 5;
+constexpr int NMAT_ST = NMAT4 - NMAT_REC;
+// Storage slot of matrix x inside a level of d4 and of the host mirror: the 17 stored matrices in
+// enum order, then the 5 record-only ones.  d4 holds slots [0, 17) per level, or all 22 when
+// DevTables::mat5 (band-sharded exchange, a host mirror streamed during the fill); the host mirror
+// always holds 22.  Matrix-major "level element" indices of the exchange API (x*C + a*M + c) are by
+// matrix, not by slot.
+__host__ __device__ constexpr int rec_below(int x) {
+    return (x > PfromMprime) + (x > PLmloop00) + (x > PRmloop00) + (x > PMmloop00) + (x > POmloop00);
+}
+__host__ __device__ constexpr int mslot(int x) { return rec_only(x) ? NMAT_ST + rec_below(x) : x - rec_below(x); }
+static_assert(mslot(PK) == 0 && mslot(PfromM) == 7 && mslot(PfromO) == 8 && mslot(POmloop10) == NMAT_ST - 1, "stored slots");
+static_assert(mslot(PfromMprime) == NMAT_ST && mslot(POmloop00) == NMAT4 - 1, "record-only slots");
+
 constexpr int IE_U = 29;  // u1,u2 in [0,28] for pseudoknot interior loops (pseudo_loop.cc:694-806)
 #ifndef CCJ_ILB
 #define CCJ_ILB 8
@@ -215,7 +233,7 @@ struct DevTables {
     uint2 *il, *ilm;               // il: pair (p,p+w) closes the loop (PL, PR); ilm: pair encloses (PM)
     int16_t *dummy;                // n+64 values 32767: target of the null entries
     const uint32_t *items;         // k_iloop work items (role << 30 | f1 << 20 | f2 << 10 | chunk)
-    int mat5;                      // 1: the 5 record-only matrices are stored in d4 too (band-sharded exchange)
+    int mat5;                      // 1: the 5 record-only matrices are stored in d4 too (22 slots per level, mslot)
     uint32_t *ilseg, *ilmseg;      // [pair][IL_SEG]
     int *err;                      // device error word
     // split-point sharing (above): levels [g_lo, g_hi) share; partial-record ring of SHARE_R
@@ -234,13 +252,10 @@ struct DevTables {
     long long accC;
 };
 
-// The 5 matrices no fill kernel reads back as matrices (PLmloop00, PMmloop00, POmloop00, PfromMprime,
-// PRmloop00) live only in the loop records (RA / RK), unless DevTables::mat5: the level kernel skips
-// their d4 stores.  rec_get reads one from the record of the cell at in-level offset
-// cell (a*M + G(h) + i-1); k_mat5 writes them into d4 where a host mirror needs them.
-__host__ __device__ __forceinline__ bool rec_only(int x) {
-    return x == PLmloop00 || x == PMmloop00 || x == POmloop00 || x == PfromMprime || x == PRmloop00;
-}
+// The 5 record-only matrices (PLmloop00, PMmloop00, POmloop00, PfromMprime, PRmloop00) live only in
+// the loop records (RA / RK), unless DevTables::mat5: the level kernel skips their d4 stores and d4
+// has no slots for them.  rec_get reads one from the record of the cell at in-level
+// offset cell (a*M + G(h) + i-1); k_mat5 writes a level's five into a scratch buffer for the host mirror.
 __device__ __forceinline__ int rec_get(const DevTables &T, int x, const LvlDev &L, long long cell) {
     const uint4 *rp = T.rec + L.lr;
     if (x == PRmloop00) return (int)(int16_t)(rp[L.C + cell].x & 0xffffu);  // RK: Rm00 | Mm00
@@ -251,9 +266,9 @@ __device__ __forceinline__ int rec_get(const DevTables &T, int x, const LvlDev &
     return (int)(int16_t)(r.w & 0xffffu);                                    // PfromMprime
 }
 
-// element offset of cell (a,h,i) of matrix x inside level t (relative to lv[t].base)
+// element offset of cell (a,h,i) of matrix x inside level t of the host mirror (relative to lv_offh[t])
 inline int64_t cell_offset_host(const LevelDesc &L, int x, int a, int h, int i) {
-    return (int64_t)x * L.C + (int64_t)a * L.M + (int64_t)h * L.m - (int64_t)h * (h - 1) / 2 + (i - 1);
+    return (int64_t)mslot(x) * L.C + (int64_t)a * L.M + (int64_t)h * L.m - (int64_t)h * (h - 1) / 2 + (i - 1);
 }
 
 }  // namespace ccj
@@ -280,5 +295,5 @@ int ccjk_ptail_unpack(const ccj::DevTables *T, int sigma, const int16_t *recv, s
 int ccjk_items(const ccj::DevTables *T, int G, int rank, int simulate, long long *counts, const long long *offs,
                uint32_t *items, int pass, void *stream);
 int ccjk_canon(const ccj::DevTables *T, int x, const long long *offij, int16_t *out, void *stream);
-int ccjk_mat5(const ccj::DevTables *T, int t, void *stream);
+int ccjk_mat5(const ccj::DevTables *T, int t, int16_t *out, void *stream);
 }

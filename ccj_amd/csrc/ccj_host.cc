@@ -121,8 +121,12 @@ struct ccj_ctx {
 
     // layout
     std::vector<LevelDesc> lv_host;     // device pointers
-    std::vector<int64_t> lv_off;        // element offset of each level
-    int64_t total4 = 0;                 // elements of the 4-D storage
+    std::vector<int64_t> lv_off;        // element offset of each level in d4 (nm4 slots per level)
+    std::vector<int64_t> lv_offh;       // element offset of each level in the host mirror (NMAT4 slots)
+    int64_t ncell = 0;                  // cells of the 4-D state per matrix, C(n+1, 4)
+    int64_t total4 = 0;                 // elements of d4: nm4 * ncell
+    int nm4 = NMAT_ST;                  // matrix slots per level in d4 (NMAT4 when T.mat5; ccj_engine.h mslot)
+    bool mat5 = false;                  // the record-only matrices stored in d4 too (DevTables::mat5)
     int nlev = 0;                       // levels with cells (0..n-3)
 
     // device
@@ -302,7 +306,7 @@ struct HostView {
         if (i <= 0 || l > n) throw BacktrackExit{134, "CCJ: matrices.hh:167: Assertion `!(i<=0 || l> n_)' failed.\n"};
         const int t = (j - i) + (l - k);
         const LevelDesc &L = c->lv_host[t];
-        const int64_t off = c->lv_off[t] + cell_offset_host(L, x, j - i, k - j - 2, i);
+        const int64_t off = c->lv_offh[t] + cell_offset_host(L, x, j - i, k - j - 2, i);
         return (int)c->h4[off];
     }
     bool can_pair(int i, int j) const {  // pseudo_loop.hh:131-135 (assert(i<=j) live in reference)
@@ -1731,10 +1735,15 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     for (size_t x = 31; x < c->lx.size(); ++x) c->lx[x] = (int)(c->prm.lxc * log((double)x / 30.));
     c->rs = n + 2;
 
-    // level layout
+    // level layout.  d4 stores 17 matrix slots per level, or all 22 (mat5) where the band-sharded
+    // exchange packs them or a host mirror streams them during the fill (ccj_engine.h mslot); the
+    // host mirror always has 22
+    c->mat5 = (c->world > 1 && !c->simulate) || c->overlap || (getenv("CCJ_MAT5") && atoi(getenv("CCJ_MAT5")) != 0);
+    c->nm4 = c->mat5 ? NMAT4 : NMAT_ST;
     c->lv_host.assign(std::max(n, 1), LevelDesc{nullptr, 0, 0, 0, 0});
     c->lv_off.assign(std::max(n, 1), 0);
-    int64_t off = 0;
+    c->lv_offh.assign(std::max(n, 1), 0);
+    int64_t off = 0, cells = 0;
     for (int t = 0; t < n; ++t) {
         const int m = n - t - 2;
         LevelDesc L{nullptr, 0, 0, m > 0 ? m : 0, 0};
@@ -1745,11 +1754,14 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
             c->nlev = t + 1;
         }
         c->lv_off[t] = off;
+        c->lv_offh[t] = (int64_t)NMAT4 * cells;
         c->lv_host[t] = L;
-        off += (int64_t)NMAT4 * L.C;
+        off += (int64_t)c->nm4 * L.C;
+        cells += L.C;
     }
     c->total4 = off;
-    if ((uint64_t)off != (uint64_t)NMAT4 * ccj_num_cells(n))
+    c->ncell = cells;
+    if ((uint64_t)cells != (uint64_t)ccj_num_cells(n))
         return set_err(c.get(), CCJ_E_ARG, "layout size mismatch");
     // k_ppush addresses the PK rows of PPUSH_S consecutive levels as 32-bit byte offsets from the
     // lowest one's start (one buffer resource per wave): that span must stay below 4 GB
@@ -1798,7 +1810,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     if (c->total4 > 0 && hipMalloc(&c->d4, (size_t)c->total4 * sizeof(int16_t)) != hipSuccess)
         return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for 4-D matrices failed", c->total4 * 2e-9);
     // AoS loop records: NREC 16-byte records per cell (ccj_engine.h)
-    c->nrec = c->total4 / NMAT4 * NREC;
+    c->nrec = c->ncell * NREC;
     if (c->nrec > 0 && hipMalloc(&c->d_rec, (size_t)c->nrec * sizeof(uint4)) != hipSuccess)
         return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for loop records failed", c->nrec * 16e-9);
     // split-point sharing: the level range it covers (every level of it runs unsplit, so each leader
@@ -1934,8 +1946,8 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     // the pinned host mirror is only needed by the host traceback and the getters: allocate it up
     // front when the fill streams into it, else on first use (ccj_sync_host)
     if (c->overlap && c->total4 > 0 &&
-        hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
-        return set_err(cp, CCJ_E_OOM, "pinned host allocation of %.2f GB failed", c->total4 * 2e-9);
+        hipHostMalloc(&c->h4, (size_t)NMAT4 * c->ncell * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
+        return set_err(cp, CCJ_E_OOM, "pinned host allocation of %.2f GB failed", NMAT4 * c->ncell * 2e-9);
     c->h2i.assign(A2_N * plane, 0);
     c->hvt.assign(plane, 0);
 
@@ -2010,8 +2022,9 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.ilm = c->d_ilm;
     T.dummy = c->d_dummy;
     T.items = c->d_items;
-    // the exchange packs all 22 matrices from d4; CCJ_MAT5=1 stores them in every fill (A/B timing)
-    T.mat5 = ((c->world > 1 && !c->simulate) || (getenv("CCJ_MAT5") && atoi(getenv("CCJ_MAT5")) != 0)) ? 1 : 0;
+    // the exchange packs all 22 matrices from d4, a mirror streamed during the fill copies them;
+    // CCJ_MAT5=1 stores them in every fill (A/B timing)
+    T.mat5 = c->mat5 ? 1 : 0;
     T.ilseg = c->d_ilseg;
     T.ilmseg = c->d_ilmseg;
     T.err = c->d_err;
@@ -2138,7 +2151,7 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
             // stream the finished level to the pinned host mirror while later levels run
             HIPCHK(c, hipStreamWaitEvent(c->st_copy, lvl_full[s], 0));
             const size_t bytes = (size_t)NMAT4 * c->lv_host[s].C * sizeof(int16_t);
-            HIPCHK(c, hipMemcpyAsync(c->h4 + c->lv_off[s], c->d4 + c->lv_off[s], bytes, hipMemcpyDeviceToHost, c->st_copy));
+            HIPCHK(c, hipMemcpyAsync(c->h4 + c->lv_offh[s], c->d4 + c->lv_off[s], bytes, hipMemcpyDeviceToHost, c->st_copy));
         }
         // P(s+3) only needs PK levels <= s; band-sharded, this rank's partials are combined in the
         // bulk exchange of level s+1, which then records p_done[s+3]
@@ -2290,7 +2303,6 @@ static int fill_enqueue(ccj_ctx *c, const ccj_ctx *after = nullptr) {
                 }
             }
             HIPCHK(c, trec(5, st));
-            if (c->overlap && c->h4 && !c->T.mat5) HIPCHK(c, (hipError_t)ccjk_mat5(&c->T, s, st));  // for the mirror copy
             HIPCHK(c, hipEventRecord(c->lev_done[s], st));
             if (xchg) {
                 if (const int rc = bulk_start(s)) return rc;
@@ -2463,13 +2475,30 @@ extern "C" int ccj_sync_host(ccj_ctx *c) {
     if (c->overlap && c->h4) {
         HIPCHK(c, hipStreamSynchronize(c->st_copy));
     } else if (c->total4 > 0) {
-        if (!c->h4 && hipHostMalloc(&c->h4, (size_t)c->total4 * sizeof(int16_t), hipHostMallocDefault) != hipSuccess)
-            return set_err(c, CCJ_E_OOM, "pinned host allocation of %.2f GB failed", c->total4 * 2e-9);
-        if (!c->T.mat5) {  // the record-only matrices into d4 first (ccj_engine.h rec_only)
-            for (int t = 0; t < c->nlev; ++t) HIPCHK(c, (hipError_t)ccjk_mat5(&c->T, t, c->st));
-            HIPCHK(c, hipStreamSynchronize(c->st));
+        const size_t hbytes = (size_t)NMAT4 * c->ncell * sizeof(int16_t);
+        if (!c->h4 && hipHostMalloc(&c->h4, hbytes, hipHostMallocDefault) != hipSuccess)
+            return set_err(c, CCJ_E_OOM, "pinned host allocation of %.2f GB failed", hbytes * 1e-9);
+        if (c->mat5) {  // d4 has the mirror's layout
+            HIPCHK(c, hipMemcpy(c->h4, c->d4, hbytes, hipMemcpyDeviceToHost));
+        } else {  // per level: the 17 stored slots, then the record-only five read back from the records
+            size_t cmax = 0;
+            for (int t = 0; t < c->nlev; ++t) cmax = std::max(cmax, (size_t)c->lv_host[t].C);
+            int16_t *scr = nullptr;
+            if (hipMalloc(&scr, (size_t)NMAT_REC * cmax * sizeof(int16_t)) != hipSuccess)
+                return set_err(c, CCJ_E_OOM, "ccj_sync_host: device scratch of %.2f GB", NMAT_REC * cmax * 2e-9);
+            int rc = CCJ_OK;
+            for (int t = 0; t < c->nlev && rc == CCJ_OK; ++t) {
+                const size_t C = (size_t)c->lv_host[t].C;
+                if (hipMemcpy(c->h4 + c->lv_offh[t], c->d4 + c->lv_off[t], (size_t)NMAT_ST * C * sizeof(int16_t),
+                              hipMemcpyDeviceToHost) != hipSuccess ||
+                    ccjk_mat5(&c->T, t, scr, c->st) != 0 || hipStreamSynchronize(c->st) != hipSuccess ||
+                    hipMemcpy(c->h4 + c->lv_offh[t] + (size_t)NMAT_ST * C, scr, (size_t)NMAT_REC * C * sizeof(int16_t),
+                              hipMemcpyDeviceToHost) != hipSuccess)
+                    rc = set_err(c, CCJ_E_HIP, "ccj_sync_host: mirror copy of level %d failed", t);
+            }
+            hipFree(scr);
+            if (rc != CCJ_OK) return rc;
         }
-        HIPCHK(c, hipMemcpy(c->h4, c->d4, (size_t)c->total4 * sizeof(int16_t), hipMemcpyDeviceToHost));
     }
     HIPCHK(c, hipMemcpy(c->h2i.data(), c->d2i, A2_N * plane * sizeof(int), hipMemcpyDeviceToHost));
     HIPCHK(c, hipMemcpy(c->hvt.data(), c->d_vt, plane, hipMemcpyDeviceToHost));
@@ -2657,7 +2686,7 @@ extern "C" int ccj_get4(const ccj_ctx *c, int mat, int i, int j, int k, int l) {
     if (!(i <= j && j < k - 1 && k <= l)) return INF;
     if (i < 1 || l > c->n) return INF;
     const int t = (j - i) + (l - k);
-    return (int)c->h4[c->lv_off[t] + cell_offset_host(c->lv_host[t], mat, j - i, k - j - 2, i)];
+    return (int)c->h4[c->lv_offh[t] + cell_offset_host(c->lv_host[t], mat, j - i, k - j - 2, i)];
 }
 
 extern "C" int ccj_get2(const ccj_ctx *c, int mat, int i, int j) {

@@ -70,7 +70,7 @@ __device__ __forceinline__ int ld4(const DevTables &T, int x, int tp, int ap, in
 #endif
     const int mp = T.n - tp - 2;
     const int Mp = (mp * (mp + 1)) >> 1;
-    const int off = x * (tp + 1) * Mp + ap * Mp + hp * mp - ((hp * (hp - 1)) >> 1) + ip - 1;
+    const int off = mslot(x) * (tp + 1) * Mp + ap * Mp + hp * mp - ((hp * (hp - 1)) >> 1) + ip - 1;
     return (int)T.d4[T.lb[tp] + off];
 }
 
@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
             return;
         }
 #endif
-        int16_t *dl = T.d4 + Lt.lb + (long long)PL * Lt.C + a * Lt.M + i - 1;
+        int16_t *dl = T.d4 + Lt.lb + (long long)mslot(PL) * Lt.C + a * Lt.M + i - 1;
         if (act && gq == 0) dl[h * m - ((h * (h - 1)) >> 1)] = (int16_t)clamp_store(bm.x);
         if (actb) dl[hb * m - ((hb * (hb - 1)) >> 1)] = (int16_t)clamp_store(bm.y);
     } else if (role == 1) {
@@ -1074,7 +1074,7 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
             return;
         }
 #endif
-        int16_t *dr = T.d4 + Lt.lb + (long long)PR * Lt.C + a * Lt.M;
+        int16_t *dr = T.d4 + Lt.lb + (long long)mslot(PR) * Lt.C + a * Lt.M;
         if (act && gq == 0) dr[h * m - ((h * (h - 1)) >> 1) + i - 1] = (int16_t)clamp_store(bm.x);
         if (actb) dr[hb * m - ((hb * (hb - 1)) >> 1) + ib - 1] = (int16_t)clamp_store(bm.y);
     } else {
@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(64 * IL_WPB) void k_iloop(DevTables T, int t, long 
             return;
         }
 #endif
-        int16_t *dm = T.d4 + Lt.lb + (long long)PM * Lt.C + h * m - ((h * (h - 1)) >> 1) + j - 1;
+        int16_t *dm = T.d4 + Lt.lb + (long long)mslot(PM) * Lt.C + h * m - ((h * (h - 1)) >> 1) + j - 1;
         if (act && gq == 0) dm[a * Lt.M - a] = (int16_t)clamp_store(bm.x);
         if (actb) dm[ab * Lt.M - ab] = (int16_t)clamp_store(bm.y);
     }
@@ -1272,7 +1272,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     const int2 *__restrict__ WBW = T.WBW;
     const LvlDev *__restrict__ LD = T.ld;
     const int16_t *__restrict__ D4 = T.d4;
-#define LDX(lp, L, x, U, ln) ((int)(lp)[(unsigned)((x) * (L).C + (U)) + (ln)])
+#define LDX(lp, L, x, U, ln) ((int)(lp)[(unsigned)(mslot(x) * (L).C + (U)) + (ln)])
     // WB of an interval of `len` bases from its WBP, as k_diag2d stores it (get_WB,
     // pseudo_loop.cc:647-653: min(cp*len, WBP)): one load fewer per split side
 #define WBD(wbp, len) imin(cp * (len), (wbp))
@@ -1799,7 +1799,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             const int pin = LDX(lp2, L2, PL, Uin, L0 + uh);
             b1 = pin + W2E(T.est, i, j);
 #ifndef CCJ_ABLATE_ILOOP
-            b1 = imin(b1, imin(pin + W2E(T.ie, i, j), (int)dst[PL * C]));
+            b1 = imin(b1, imin(pin + W2E(T.ie, i, j), (int)dst[mslot(PL) * C]));
 #endif
         }
         const int b2 = (a >= 2) ? imin(LDX(lp2, L2, PLmloop10, Uin, L0 + uh), LDX(lp2, L2, PLmloop01, Uin, L0 + uh)) + apbp2 : INF;
@@ -1816,7 +1816,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             const int pin = LDX(lp2, L2, PR, Uin, L0 + uh);  // stack and (d, dp) = (k+1, l-1)
             b1 = pin + W2E(T.est, k, l);
 #ifndef CCJ_ABLATE_ILOOP
-            b1 = imin(b1, imin(pin + W2E(T.ie, k, l), (int)dst[PR * C]));
+            b1 = imin(b1, imin(pin + W2E(T.ie, k, l), (int)dst[mslot(PR) * C]));
 #endif
         }
         const int b2 = (b >= 2) ? imin(LDX(lp2, L2, PRmloop10, Uin, L0 + uh), LDX(lp2, L2, PRmloop01, Uin, L0 + uh)) + apbp2 : INF;
@@ -1834,7 +1834,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             const int pin = LDX(lp2, L2, PM, Uin, L0);  // stack and (d, dp) = (j-1, k+1)
             b1 = pin + W2E(T.est, j - 1, k + 1);
 #ifndef CCJ_ABLATE_ILOOP
-            if (a >= 2 && b >= 2) b1 = imin(b1, imin(pin + W2E(T.ie, j - 1, k + 1), (int)dst[PM * C]));
+            if (a >= 2 && b >= 2) b1 = imin(b1, imin(pin + W2E(T.ie, j - 1, k + 1), (int)dst[mslot(PM) * C]));
 #endif
         }
         const int b2 = inner ? imin(LDX(lp2, L2, PMmloop10, Uin, L0), LDX(lp2, L2, PMmloop01, Uin, L0)) + apbp2 : INF;
@@ -1871,28 +1871,28 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #ifdef CCJ_DEBUG_BOUNDS
     if (i < 1 || i > m - h || h >= m) { atomicOr(T.err, 32); return; }
 #endif
-    dst[PK * C] = (int16_t)clamp_store(vPK);
-    dst[PL * C] = (int16_t)sPL;
-    dst[PR * C] = (int16_t)sPR;
-    dst[PM * C] = (int16_t)sPM;
-    dst[PO * C] = (int16_t)sPO;
-    dst[PfromL * C] = (int16_t)clamp_store(vPfromL);
-    dst[PfromR * C] = (int16_t)clamp_store(vPfromR);
-    dst[PfromM * C] = (int16_t)clamp_store(vPfromM);
-    if (T.mat5) dst[PfromMprime * C] = (int16_t)clamp_store(vPfromMp);  // record-only (ccj_engine.h rec_only)
-    dst[PfromO * C] = (int16_t)clamp_store(vPfromO);
-    if (T.mat5) dst[PLmloop00 * C] = (int16_t)clamp_store(vPLm00);  // record-only (ccj_engine.h rec_only)
-    dst[PLmloop01 * C] = (int16_t)clamp_store(vPLm01);
-    dst[PLmloop10 * C] = (int16_t)clamp_store(vPLm10);
-    if (T.mat5) dst[PRmloop00 * C] = (int16_t)clamp_store(vPRm00);  // record-only (ccj_engine.h rec_only)
-    dst[PRmloop01 * C] = (int16_t)clamp_store(vPRm01);
-    dst[PRmloop10 * C] = (int16_t)clamp_store(vPRm10);
-    if (T.mat5) dst[PMmloop00 * C] = (int16_t)clamp_store(vPMm00);  // record-only (ccj_engine.h rec_only)
-    dst[PMmloop01 * C] = (int16_t)clamp_store(vPMm01);
-    dst[PMmloop10 * C] = (int16_t)clamp_store(vPMm10);
-    if (T.mat5) dst[POmloop00 * C] = (int16_t)clamp_store(vPOm00);  // record-only (ccj_engine.h rec_only)
-    dst[POmloop01 * C] = (int16_t)clamp_store(vPOm01);
-    dst[POmloop10 * C] = (int16_t)clamp_store(vPOm10);
+    dst[mslot(PK) * C] = (int16_t)clamp_store(vPK);
+    dst[mslot(PL) * C] = (int16_t)sPL;
+    dst[mslot(PR) * C] = (int16_t)sPR;
+    dst[mslot(PM) * C] = (int16_t)sPM;
+    dst[mslot(PO) * C] = (int16_t)sPO;
+    dst[mslot(PfromL) * C] = (int16_t)clamp_store(vPfromL);
+    dst[mslot(PfromR) * C] = (int16_t)clamp_store(vPfromR);
+    dst[mslot(PfromM) * C] = (int16_t)clamp_store(vPfromM);
+    if (T.mat5) dst[mslot(PfromMprime) * C] = (int16_t)clamp_store(vPfromMp);  // record-only (ccj_engine.h rec_only)
+    dst[mslot(PfromO) * C] = (int16_t)clamp_store(vPfromO);
+    if (T.mat5) dst[mslot(PLmloop00) * C] = (int16_t)clamp_store(vPLm00);  // record-only (ccj_engine.h rec_only)
+    dst[mslot(PLmloop01) * C] = (int16_t)clamp_store(vPLm01);
+    dst[mslot(PLmloop10) * C] = (int16_t)clamp_store(vPLm10);
+    if (T.mat5) dst[mslot(PRmloop00) * C] = (int16_t)clamp_store(vPRm00);  // record-only (ccj_engine.h rec_only)
+    dst[mslot(PRmloop01) * C] = (int16_t)clamp_store(vPRm01);
+    dst[mslot(PRmloop10) * C] = (int16_t)clamp_store(vPRm10);
+    if (T.mat5) dst[mslot(PMmloop00) * C] = (int16_t)clamp_store(vPMm00);  // record-only (ccj_engine.h rec_only)
+    dst[mslot(PMmloop01) * C] = (int16_t)clamp_store(vPMm01);
+    dst[mslot(PMmloop10) * C] = (int16_t)clamp_store(vPMm10);
+    if (T.mat5) dst[mslot(POmloop00) * C] = (int16_t)clamp_store(vPOm00);  // record-only (ccj_engine.h rec_only)
+    dst[mslot(POmloop01) * C] = (int16_t)clamp_store(vPOm01);
+    dst[mslot(POmloop10) * C] = (int16_t)clamp_store(vPOm10);
     // loop records and interior-loop copies (the copies only where a later k_iloop can read them:
     // its pair can pair); in sharded fills the other ranks' cells get both from k_unpack
     if (!copies) return;
@@ -2062,7 +2062,7 @@ __global__ __launch_bounds__(256) void k_pack(DevTables T, int t, int G, int r, 
     const LvlDev Lt = T.ld[t];
     const int16_t *src = T.d4 + Lt.lb + (long long)shard_a(xch_own(k, part), G, r) * Mt + c;
 #pragma unroll 2
-    for (int x = 0; x < NMAT4; ++x) send[xch_pos(x, k, c, nmax, Mt)] = src[(long long)x * Lt.C];
+    for (int x = 0; x < NMAT4; ++x) send[xch_pos(x, k, c, nmax, Mt)] = src[(long long)mslot(x) * Lt.C];
 }
 
 __global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r, int part, int nmax, const int16_t *recv,
@@ -2092,7 +2092,7 @@ __global__ __launch_bounds__(256) void k_unpack(DevTables T, int t, int G, int r
 #pragma unroll
     for (int x = 0; x < NMAT4; ++x) {
         v[x] = sl[xch_pos(x, k, c, nmax, Mt)];
-        dst[x * C] = (int16_t)v[x];
+        dst[mslot(x) * C] = (int16_t)v[x];
     }
     write_records(T, Lt.lr, Lt.C, (unsigned)(a * Mt + c), v[PLmloop00], v[PMmloop00], v[POmloop00], v[PfromL], v[PfromO],
                   v[PLmloop10], v[PfromMprime], v[PK], v[PRmloop00], v[PfromR], imin(v[PL], v[PR]), v[PMmloop10],
@@ -2190,24 +2190,25 @@ __global__ __launch_bounds__(256) void k_canon(DevTables T, int x, int t, const 
     const int i = c - Gh + 1, j = i + a, k = j + h + 2, l = k + (t - a);
     const long long u = k - (j + 2);
     const long long pos = offij[(long long)i * (n + 1) + j] + u * (n + 1) - u * (2LL * j + 3 + u) / 2 + (l - k);
-    out[pos] = (int16_t)((!T.mat5 && rec_only(x)) ? rec_get(T, x, L, cidx) : (int)T.d4[L.lb + (long long)x * L.C + cidx]);
+    out[pos] = (int16_t)((!T.mat5 && rec_only(x)) ? rec_get(T, x, L, cidx) : (int)T.d4[L.lb + (long long)mslot(x) * L.C + cidx]);
 }
 
-// the record-only matrices of level t written into d4 (for a host mirror of d4)
-__global__ __launch_bounds__(256) void k_mat5(DevTables T, int t) {
+// the record-only matrices of level t, read back from its records into out (slots NMAT_ST.. of the
+// level's host-mirror layout, mslot), for a host mirror of a context without them in d4
+__global__ __launch_bounds__(256) void k_mat5(DevTables T, int t, int16_t *out) {
     const LvlDev L = T.ld[t];
     const long long cidx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (cidx >= (long long)L.C) return;
-    const int xs[5] = {PLmloop00, PMmloop00, POmloop00, PfromMprime, PRmloop00};
+    const int xs[NMAT_REC] = {PLmloop00, PMmloop00, POmloop00, PfromMprime, PRmloop00};
 #pragma unroll
-    for (int q = 0; q < 5; ++q) T.d4[L.lb + (long long)xs[q] * L.C + cidx] = (int16_t)rec_get(T, xs[q], L, cidx);
+    for (int q = 0; q < NMAT_REC; ++q) out[(long long)(mslot(xs[q]) - NMAT_ST) * L.C + cidx] = (int16_t)rec_get(T, xs[q], L, cidx);
 }
 
-extern "C" int ccjk_mat5(const DevTables *T, int t, void *stream) {
+extern "C" int ccjk_mat5(const DevTables *T, int t, int16_t *out, void *stream) {
     const int m = T->n - t - 2;
     if (m <= 0 || t >= T->nlev) return 0;
     const long long C = (long long)(t + 1) * (m * (m + 1) / 2);
-    hipLaunchKernelGGL(k_mat5, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t);
+    hipLaunchKernelGGL(k_mat5, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *T, t, out);
     return (int)hipGetLastError();
 }
 

@@ -53,22 +53,36 @@ def test_work_model_matches_survey_scale():
     assert 0.9 * 6.29e9 < total < 1.05 * 6.29e9
 
 
-def _layout(n):
-    """Python restatement of the level-major layout (ccj_engine.h) — brute-force bijection check."""
+REC_ONLY = (8, 10, 13, 16, 19)  # PfromMprime, PLmloop00, PRmloop00, PMmloop00, POmloop00 (ccj_engine.h rec_only)
+
+
+def _mslot(x):
+    """ccj_engine.h mslot: the 17 stored matrices in enum order, then the 5 record-only ones."""
+    below = sum(x > r for r in REC_ONLY)
+    return 17 + below if x in REC_ONLY else x - below
+
+
+def _layout(n, nm4=22):
+    """Python restatement of the level-major layout (ccj_engine.h) — brute-force bijection check;
+    nm4 = 17 (d4 without the record-only matrices) or 22 (mat5, and the host mirror)."""
     off, lv = 0, {}
     for t in range(n):
         m = n - t - 2
         M = m * (m + 1) // 2 if m > 0 else 0
         lv[t] = (off, (t + 1) * M, M, m)
-        off += 22 * (t + 1) * M
+        off += nm4 * (t + 1) * M
     return lv, off
 
 
 @pytest.mark.parametrize("n", [5, 9, 17, 24])
-def test_level_layout_is_a_bijection(n):
-    lv, total = _layout(n)
+@pytest.mark.parametrize("nm4", [17, 22])
+def test_level_layout_is_a_bijection(n, nm4):
+    lv, total = _layout(n, nm4)
+    assert sorted(_mslot(x) for x in range(22)) == list(range(22))
     seen = set()
     for x in range(22):
+        if _mslot(x) >= nm4:
+            continue
         for i in range(1, n + 1):
             for j in range(i, n + 1):
                 for k in range(j + 2, n + 1):
@@ -76,8 +90,9 @@ def test_level_layout_is_a_bijection(n):
                         a, g, b = j - i, k - j, l - k
                         t, h = a + b, g - 2
                         base, C, M, m = lv[t]
-                        e = base + x * C + a * M + h * m - h * (h - 1) // 2 + i - 1
-                        assert base + x * C <= e < base + (x + 1) * C
+                        s = _mslot(x)
+                        e = base + s * C + a * M + h * m - h * (h - 1) // 2 + i - 1
+                        assert base + s * C <= e < base + (s + 1) * C
                         seen.add(e)
     assert len(seen) == total
 
