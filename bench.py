@@ -58,11 +58,11 @@ def num_cells(n):
 
 
 def footprint_gb(n, sharded=False):
-    """Device memory of one context: 4-D matrices (17 stored per level, all 22 when
+    """Device memory of one context: 4-D matrices (11 stored per level, all 22 when
     band-sharded), loop records, interior-loop copies, candidate lists, the sharing ring and the 2-D
     tables."""
     cells = num_cells(n)
-    nm4 = 22 if sharded else 17
+    nm4 = 22 if sharded else 11
     maxc = max(((t + 1) * ((n - t - 2) * (n - t - 1) // 2) for t in range(max(n - 2, 1))), default=0)
     pmx = 2 * sum((n - t - 2) * n * (t + 1) for t in range(max(n - 2, 0)))
     plane = (n + 1) * (n + 2)

@@ -26,23 +26,25 @@ enum Mat4 {
     PMmloop00, PMmloop01, PMmloop10, POmloop00, POmloop01, POmloop10
 };
 
-// The 5 matrices no fill kernel reads back as matrices (rec_get, below) and the 17 that d4 stores.
-__host__ __device__ constexpr bool rec_only(int x) {
-    return x == PLmloop00 || x == PMmloop00 || x == POmloop00 || x == PfromMprime || x == PRmloop00;
-}
-constexpr int NMAT_REC = 5;
+// The matrices the loop records carry (below), which d4 does not store unless DevTables::mat5: the 5
+// no fill kernel reads back as matrices and 6 more the level kernel's stack terms read from the
+// records (rec_get); d4 stores the other 11.
+constexpr unsigned REC_MASK = (1u << PfromL) | (1u << PfromR) | (1u << PfromMprime) | (1u << PfromO) | (1u << PLmloop00) |
+                              (1u << PLmloop10) | (1u << PRmloop00) | (1u << PMmloop00) | (1u << PMmloop10) |
+                              (1u << POmloop00) | (1u << POmloop10);
+__host__ __device__ constexpr bool rec_only(int x) { return (REC_MASK >> x) & 1u; }
+constexpr int NMAT_REC = __builtin_popcount(REC_MASK);
 constexpr int NMAT_ST = NMAT4 - NMAT_REC;
-// Storage slot of matrix x inside a level of d4 and of the host mirror: the 17 stored matrices in
-// enum order, then the 5 record-only ones.  d4 holds slots [0, 17) per level, or all 22 when
+// Storage slot of matrix x inside a level of d4 and of the host mirror: the 11 stored matrices in
+// enum order, then the 11 record-carried ones.  d4 holds slots [0, 11) per level, or all 22 when
 // DevTables::mat5 (band-sharded exchange, a host mirror streamed during the fill); the host mirror
 // always holds 22.  Matrix-major "level element" indices of the exchange API (x*C + a*M + c) are by
 // matrix, not by slot.
-__host__ __device__ constexpr int rec_below(int x) {
-    return (x > PfromMprime) + (x > PLmloop00) + (x > PRmloop00) + (x > PMmloop00) + (x > POmloop00);
-}
+__host__ __device__ constexpr int rec_below(int x) { return __builtin_popcount(REC_MASK & ((1u << x) - 1u)); }
 __host__ __device__ constexpr int mslot(int x) { return rec_only(x) ? NMAT_ST + rec_below(x) : x - rec_below(x); }
-static_assert(mslot(PK) == 0 && mslot(PfromM) == 7 && mslot(PfromO) == 8 && mslot(POmloop10) == NMAT_ST - 1, "stored slots");
-static_assert(mslot(PfromMprime) == NMAT_ST && mslot(POmloop00) == NMAT4 - 1, "record-only slots");
+static_assert(NMAT_REC == 11 && mslot(PK) == 0 && mslot(PO) == 4 && mslot(PfromM) == 5 && mslot(POmloop01) == NMAT_ST - 1,
+              "stored slots");
+static_assert(mslot(PfromL) == NMAT_ST && mslot(POmloop10) == NMAT4 - 1, "record-carried slots");
 
 constexpr int IE_U = 29;  // u1,u2 in [0,28] for pseudoknot interior loops (pseudo_loop.cc:694-806)
 #ifndef CCJ_ILB
@@ -252,18 +254,32 @@ struct DevTables {
     long long accC;
 };
 
-// The 5 record-only matrices (PLmloop00, PMmloop00, POmloop00, PfromMprime, PRmloop00) live only in
-// the loop records (RA / RK), unless DevTables::mat5: the level kernel skips their d4 stores and d4
-// has no slots for them.  rec_get reads one from the record of the cell at in-level
-// offset cell (a*M + G(h) + i-1); k_mat5 writes a level's five into a scratch buffer for the host mirror.
+// The record-carried matrices (rec_only) live only in the loop records (RA / RK / RL), unless
+// DevTables::mat5: the level kernel skips their d4 stores and d4 has no slots for them.
+// rec_get reads one from the records of the cell at in-level offset cell (a*M + G(h) + i-1); k_mat5
+// writes a level's eleven into a scratch buffer for the host mirror.
+__device__ __forceinline__ int rlo16(unsigned w) { return (int)(int16_t)(w & 0xffffu); }
+__device__ __forceinline__ int rhi16(unsigned w) { return (int)(int16_t)(w >> 16); }
 __device__ __forceinline__ int rec_get(const DevTables &T, int x, const LvlDev &L, long long cell) {
     const uint4 *rp = T.rec + L.lr;
-    if (x == PRmloop00) return (int)(int16_t)(rp[L.C + cell].x & 0xffffu);  // RK: Rm00 | Mm00
-    const uint4 r = rp[cell];                                                // RA: Lm00|Mm00, Om00|fL, fO|Lm10, fMp|K
-    if (x == PLmloop00) return (int)(int16_t)(r.x & 0xffffu);
-    if (x == PMmloop00) return (int)(int16_t)(r.x >> 16);
-    if (x == POmloop00) return (int)(int16_t)(r.y & 0xffffu);
-    return (int)(int16_t)(r.w & 0xffffu);                                    // PfromMprime
+    if (x == PRmloop00 || x == PfromR) {  // RK: Rm00|Mm00, fR|PLR, K|-, -|-
+        const uint4 r = rp[L.C + cell];
+        return x == PRmloop00 ? rlo16(r.x) : rlo16(r.y);
+    }
+    if (x == PMmloop10 || x == POmloop10) {  // RL: Rm00|Mm00, Om00|Mm10, Om10|fR, fO|-
+        const uint4 r = rp[2 * (long long)L.C + cell];
+        return x == PMmloop10 ? rhi16(r.y) : rlo16(r.z);
+    }
+    const uint4 r = rp[cell];  // RA: Lm00|Mm00, Om00|fL, fO|Lm10, fMp|K
+    switch (x) {
+        case PLmloop00: return rlo16(r.x);
+        case PMmloop00: return rhi16(r.x);
+        case POmloop00: return rlo16(r.y);
+        case PfromL: return rhi16(r.y);
+        case PfromO: return rlo16(r.z);
+        case PLmloop10: return rhi16(r.z);
+        default: return rlo16(r.w);  // PfromMprime
+    }
 }
 
 // element offset of cell (a,h,i) of matrix x inside level t of the host mirror (relative to lv_offh[t])

@@ -126,7 +126,7 @@ struct ccj_ctx {
     int64_t ncell = 0;                  // cells of the 4-D state per matrix, C(n+1, 4)
     int64_t total4 = 0;                 // elements of d4: nm4 * ncell
     int nm4 = NMAT_ST;                  // matrix slots per level in d4 (NMAT4 when T.mat5; ccj_engine.h mslot)
-    bool mat5 = false;                  // the record-only matrices stored in d4 too (DevTables::mat5)
+    bool mat5 = false;                  // the record-carried matrices stored in d4 too (DevTables::mat5)
     int nlev = 0;                       // levels with cells (0..n-3)
 
     // device
@@ -1735,7 +1735,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     for (size_t x = 31; x < c->lx.size(); ++x) c->lx[x] = (int)(c->prm.lxc * log((double)x / 30.));
     c->rs = n + 2;
 
-    // level layout.  d4 stores 17 matrix slots per level, or all 22 (mat5) where the band-sharded
+    // level layout.  d4 stores 11 matrix slots per level, or all 22 (mat5) where the band-sharded
     // exchange packs them or a host mirror streams them during the fill (ccj_engine.h mslot); the
     // host mirror always has 22
     c->mat5 = (c->world > 1 && !c->simulate) || c->overlap || (getenv("CCJ_MAT5") && atoi(getenv("CCJ_MAT5")) != 0);
@@ -2480,7 +2480,7 @@ extern "C" int ccj_sync_host(ccj_ctx *c) {
             return set_err(c, CCJ_E_OOM, "pinned host allocation of %.2f GB failed", hbytes * 1e-9);
         if (c->mat5) {  // d4 has the mirror's layout
             HIPCHK(c, hipMemcpy(c->h4, c->d4, hbytes, hipMemcpyDeviceToHost));
-        } else {  // per level: the 17 stored slots, then the record-only five read back from the records
+        } else {  // per level: the NMAT_ST stored slots, then the record-carried ones read back from the records
             size_t cmax = 0;
             for (int t = 0; t < c->nlev; ++t) cmax = std::max(cmax, (size_t)c->lv_host[t].C);
             int16_t *scr = nullptr;

@@ -1774,7 +1774,8 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 vPRm10 = imin(vPRm10, LDX(lp, L, PRmloop10, a * L.M + m + 1, L0) + cp);       // (i,j,k+1,l)
                 vPMm01 = imin(vPMm01, LDX(lp, L, PMmloop01, a * L.M + m + 1, L0) + cp);       // (i,j,k+1,l)
             }
-            if (a >= 1) vPMm10 = imin(vPMm10, LDX(lp, L, PMmloop10, (a - 1) * L.M + m + 1, L0) + cp);  // (i,j-1,k,l)
+            // PMmloop10 from the RL record (d4 does not store it: ccj_engine.h rec_only)
+            if (a >= 1) vPMm10 = imin(vPMm10, hi16(T.rec[L.lr + (unsigned)(2 * L.C + (a - 1) * L.M + m + 1) + L0].y) + cp);  // (i,j-1,k,l)
         }
     }
     const int vPLm00 = pLm00, vPLm01 = pLm01, vPLm10 = pLm10, vPRm00 = pRm00, vPMm00 = pMm00;
@@ -1783,6 +1784,9 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     // ---- level t-2 neighbours of PL/PR/PM/PO (stack terms, get_P?mloop, PfromX)
     const LvlDev L2 = LD[t >= 2 ? t - 2 : 0];
     const int16_t *lp2 = D4 + L2.lb;
+    // the record-carried matrices of those neighbours (PLmloop10, PfromL, PfromR, PMmloop10,
+    // POmloop10, PfromO; ccj_engine.h rec_only) from their loop records: one 16-byte load per cell
+    const uint4 *rp2 = T.rec + L2.lr;
     // own slots of level t: k_iloop(t) left the interior-loop minima of PL/PR/PM there
     const LvlDev Lt = LD[t];
     const int C = Lt.C;
@@ -1802,8 +1806,9 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             b1 = imin(b1, imin(pin + W2E(T.ie, i, j), (int)dst[mslot(PL) * C]));
 #endif
         }
-        const int b2 = (a >= 2) ? imin(LDX(lp2, L2, PLmloop10, Uin, L0 + uh), LDX(lp2, L2, PLmloop01, Uin, L0 + uh)) + apbp2 : INF;
-        const int b3 = (a >= TURN + 1) ? LDX(lp2, L2, PfromL, Uin, L0 + uh) : INF;
+        const uint4 ra = (a >= 2) ? rp2[(unsigned)Uin + L0 + uh] : make_uint4(0, 0, 0, 0);  // RA: ., .|fL, .|Lm10, .
+        const int b2 = (a >= 2) ? imin(hi16(ra.z), LDX(lp2, L2, PLmloop01, Uin, L0 + uh)) + apbp2 : INF;
+        const int b3 = (a >= TURN + 1) ? hi16(ra.y) : INF;
         vPL = imin(imin(b1, b2), b3);
     }
     // ---- PR (:255-275) with get_PRiloop (:717-738, k_iloop), get_PRmloop (:740-750)
@@ -1820,7 +1825,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #endif
         }
         const int b2 = (b >= 2) ? imin(LDX(lp2, L2, PRmloop10, Uin, L0 + uh), LDX(lp2, L2, PRmloop01, Uin, L0 + uh)) + apbp2 : INF;
-        const int b3 = (b >= TURN + 1) ? LDX(lp2, L2, PfromR, Uin, L0 + uh) : INF;
+        const int b3 = (b >= TURN + 1) ? lo16(rp2[(unsigned)(L2.C + Uin) + L0 + uh].y) : INF;  // RK: ., fR|.
         vPR = imin(imin(b1, b2), b3);
     }
     // ---- PM (:277-300) with get_PMiloop (:752-773, k_iloop), get_PMmloop (:775-785)
@@ -1837,7 +1842,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             if (a >= 2 && b >= 2) b1 = imin(b1, imin(pin + W2E(T.ie, j - 1, k + 1), (int)dst[mslot(PM) * C]));
 #endif
         }
-        const int b2 = inner ? imin(LDX(lp2, L2, PMmloop10, Uin, L0), LDX(lp2, L2, PMmloop01, Uin, L0)) + apbp2 : INF;
+        const int b2 = inner ? imin(hi16(rp2[(unsigned)(2 * L2.C + Uin) + L0].y), LDX(lp2, L2, PMmloop01, Uin, L0)) + apbp2 : INF;  // RL: ., .|Mm10
         const int b3 = inner ? LDX(lp2, L2, PfromM, Uin, L0) : INF;
         const int b4 = (a == 0 && b == 0) ? 0 : INF;
         vPM = imin(imin(b1, b2), imin(b3, b4));
@@ -1849,8 +1854,9 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         const int Uin = (a - 1) * L2.M + 1;  // (i+1, j, k, l-1): lane L0 + 2h
         int b1 = INF;
         if (l - i > TURN && inner) b1 = LDX(lp2, L2, PO, Uin, L0 + 2 * uh) + W2E(T.est, i, l);
-        const int b2 = inner ? imin(LDX(lp2, L2, POmloop10, Uin, L0 + 2 * uh), LDX(lp2, L2, POmloop01, Uin, L0 + 2 * uh)) + apbp2 : INF;
-        const int b3 = (inner && l - i >= TURN + 1) ? LDX(lp2, L2, PfromO, Uin, L0 + 2 * uh) : INF;
+        const uint4 rl = inner ? rp2[(unsigned)(2 * L2.C + Uin) + L0 + 2 * uh] : make_uint4(0, 0, 0, 0);  // RL: ., ., Om10|., fO|.
+        const int b2 = inner ? imin(lo16(rl.z), LDX(lp2, L2, POmloop01, Uin, L0 + 2 * uh)) + apbp2 : INF;
+        const int b3 = (inner && l - i >= TURN + 1) ? lo16(rl.w) : INF;
         vPO = imin(imin(b1, b2), b3);
     }
 #undef LDX
@@ -1876,23 +1882,23 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     dst[mslot(PR) * C] = (int16_t)sPR;
     dst[mslot(PM) * C] = (int16_t)sPM;
     dst[mslot(PO) * C] = (int16_t)sPO;
-    dst[mslot(PfromL) * C] = (int16_t)clamp_store(vPfromL);
-    dst[mslot(PfromR) * C] = (int16_t)clamp_store(vPfromR);
+    if (T.mat5) dst[mslot(PfromL) * C] = (int16_t)clamp_store(vPfromL);  // record-carried (ccj_engine.h rec_only)
+    if (T.mat5) dst[mslot(PfromR) * C] = (int16_t)clamp_store(vPfromR);  // record-carried (ccj_engine.h rec_only)
     dst[mslot(PfromM) * C] = (int16_t)clamp_store(vPfromM);
-    if (T.mat5) dst[mslot(PfromMprime) * C] = (int16_t)clamp_store(vPfromMp);  // record-only (ccj_engine.h rec_only)
-    dst[mslot(PfromO) * C] = (int16_t)clamp_store(vPfromO);
-    if (T.mat5) dst[mslot(PLmloop00) * C] = (int16_t)clamp_store(vPLm00);  // record-only (ccj_engine.h rec_only)
+    if (T.mat5) dst[mslot(PfromMprime) * C] = (int16_t)clamp_store(vPfromMp);  // record-carried (ccj_engine.h rec_only)
+    if (T.mat5) dst[mslot(PfromO) * C] = (int16_t)clamp_store(vPfromO);  // record-carried (ccj_engine.h rec_only)
+    if (T.mat5) dst[mslot(PLmloop00) * C] = (int16_t)clamp_store(vPLm00);  // record-carried (ccj_engine.h rec_only)
     dst[mslot(PLmloop01) * C] = (int16_t)clamp_store(vPLm01);
-    dst[mslot(PLmloop10) * C] = (int16_t)clamp_store(vPLm10);
-    if (T.mat5) dst[mslot(PRmloop00) * C] = (int16_t)clamp_store(vPRm00);  // record-only (ccj_engine.h rec_only)
+    if (T.mat5) dst[mslot(PLmloop10) * C] = (int16_t)clamp_store(vPLm10);  // record-carried (ccj_engine.h rec_only)
+    if (T.mat5) dst[mslot(PRmloop00) * C] = (int16_t)clamp_store(vPRm00);  // record-carried (ccj_engine.h rec_only)
     dst[mslot(PRmloop01) * C] = (int16_t)clamp_store(vPRm01);
     dst[mslot(PRmloop10) * C] = (int16_t)clamp_store(vPRm10);
-    if (T.mat5) dst[mslot(PMmloop00) * C] = (int16_t)clamp_store(vPMm00);  // record-only (ccj_engine.h rec_only)
+    if (T.mat5) dst[mslot(PMmloop00) * C] = (int16_t)clamp_store(vPMm00);  // record-carried (ccj_engine.h rec_only)
     dst[mslot(PMmloop01) * C] = (int16_t)clamp_store(vPMm01);
-    dst[mslot(PMmloop10) * C] = (int16_t)clamp_store(vPMm10);
-    if (T.mat5) dst[mslot(POmloop00) * C] = (int16_t)clamp_store(vPOm00);  // record-only (ccj_engine.h rec_only)
+    if (T.mat5) dst[mslot(PMmloop10) * C] = (int16_t)clamp_store(vPMm10);  // record-carried (ccj_engine.h rec_only)
+    if (T.mat5) dst[mslot(POmloop00) * C] = (int16_t)clamp_store(vPOm00);  // record-carried (ccj_engine.h rec_only)
     dst[mslot(POmloop01) * C] = (int16_t)clamp_store(vPOm01);
-    dst[mslot(POmloop10) * C] = (int16_t)clamp_store(vPOm10);
+    if (T.mat5) dst[mslot(POmloop10) * C] = (int16_t)clamp_store(vPOm10);  // record-carried (ccj_engine.h rec_only)
     // loop records and interior-loop copies (the copies only where a later k_iloop can read them:
     // its pair can pair); in sharded fills the other ranks' cells get both from k_unpack
     if (!copies) return;
@@ -2193,15 +2199,16 @@ __global__ __launch_bounds__(256) void k_canon(DevTables T, int x, int t, const 
     out[pos] = (int16_t)((!T.mat5 && rec_only(x)) ? rec_get(T, x, L, cidx) : (int)T.d4[L.lb + (long long)mslot(x) * L.C + cidx]);
 }
 
-// the record-only matrices of level t, read back from its records into out (slots NMAT_ST.. of the
-// level's host-mirror layout, mslot), for a host mirror of a context without them in d4
+// the record-carried matrices of level t (ccj_engine.h rec_only), read back from its records into out
+// (slots NMAT_ST.. of the level's host-mirror layout, mslot), for a host mirror of a context without
+// them in d4
 __global__ __launch_bounds__(256) void k_mat5(DevTables T, int t, int16_t *out) {
     const LvlDev L = T.ld[t];
     const long long cidx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (cidx >= (long long)L.C) return;
-    const int xs[NMAT_REC] = {PLmloop00, PMmloop00, POmloop00, PfromMprime, PRmloop00};
 #pragma unroll
-    for (int q = 0; q < NMAT_REC; ++q) out[(long long)(mslot(xs[q]) - NMAT_ST) * L.C + cidx] = (int16_t)rec_get(T, xs[q], L, cidx);
+    for (int x = 0; x < NMAT4; ++x)
+        if (rec_only(x)) out[(long long)(mslot(x) - NMAT_ST) * L.C + cidx] = (int16_t)rec_get(T, x, L, cidx);
 }
 
 extern "C" int ccjk_mat5(const DevTables *T, int t, int16_t *out, void *stream) {

@@ -53,18 +53,18 @@ def test_work_model_matches_survey_scale():
     assert 0.9 * 6.29e9 < total < 1.05 * 6.29e9
 
 
-REC_ONLY = (8, 10, 13, 16, 19)  # PfromMprime, PLmloop00, PRmloop00, PMmloop00, POmloop00 (ccj_engine.h rec_only)
+REC_ONLY = (5, 6, 8, 9, 10, 12, 13, 16, 18, 19, 21)  # the record-carried matrices (ccj_engine.h REC_MASK)
 
 
 def _mslot(x):
-    """ccj_engine.h mslot: the 17 stored matrices in enum order, then the 5 record-only ones."""
+    """ccj_engine.h mslot: the 11 stored matrices in enum order, then the 11 record-carried ones."""
     below = sum(x > r for r in REC_ONLY)
-    return 17 + below if x in REC_ONLY else x - below
+    return 11 + below if x in REC_ONLY else x - below
 
 
 def _layout(n, nm4=22):
     """Python restatement of the level-major layout (ccj_engine.h) — brute-force bijection check;
-    nm4 = 17 (d4 without the record-only matrices) or 22 (mat5, and the host mirror)."""
+    nm4 = 11 (d4 without the record-carried matrices) or 22 (mat5, and the host mirror)."""
     off, lv = 0, {}
     for t in range(n):
         m = n - t - 2
@@ -75,7 +75,7 @@ def _layout(n, nm4=22):
 
 
 @pytest.mark.parametrize("n", [5, 9, 17, 24])
-@pytest.mark.parametrize("nm4", [17, 22])
+@pytest.mark.parametrize("nm4", [11, 22])
 def test_level_layout_is_a_bijection(n, nm4):
     lv, total = _layout(n, nm4)
     assert sorted(_mslot(x) for x in range(22)) == list(range(22))
