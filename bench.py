@@ -66,7 +66,7 @@ def footprint_gb(n, sharded=False):
     maxc = max(((t + 1) * ((n - t - 2) * (n - t - 1) // 2) for t in range(max(n - 2, 1))), default=0)
     pmx = 2 * sum((n - t - 2) * n * (t + 1) for t in range(max(n - 2, 0)))
     plane = (n + 1) * (n + 2)
-    return (2 * nm4 * cells + 48 * cells + 4 * cells + pmx + 320 * maxc + 2 * 841 * plane + 2 * 848 * 8 * plane) / 1e9
+    return (2 * nm4 * cells + 44 * cells + 4 * cells + pmx + 320 * maxc + 2 * 841 * plane + 2 * 848 * 8 * plane) / 1e9
 
 
 def rank_seed(base, rank, world, step, distinct):

@@ -74,13 +74,16 @@ struct LvlDev {     // per-level descriptor read by the level kernel (one s_load
 };
 
 // AoS loop records: the operands the fused split-point loops of k_level4d read at
-// one neighbour cell, 8 int16 per 16-byte record, so each neighbour costs one dwordx4 load instead
-// of 5-7 int16 loads.  Three record types per level, each indexed like a matrix (a*M + G(h) + i-1):
+// one neighbour cell, int16 fields packed in one record, so each neighbour costs one dwordx4 (dwordx3)
+// load instead of 5-7 int16 loads.  Three record types per level, each indexed like a matrix
+// (a*M + G(h) + i-1): RA and RL (16 bytes) in T.rec, level t at ld[t].lr (RA: C records, then RL),
+// RK (12 bytes) in T.rk at ld[t].lr / 2:
 //   RA (a-loop, both sides): PLmloop00 PMmloop00 | POmloop00 PfromL | PfromO PLmloop10 | PfromMprime PK
-//   RK (b-loop, k side):     PRmloop00 PMmloop00 | PfromR min(PL,PR) | PK -          | -  -
+//   RK (b-loop, k side):     PRmloop00 PMmloop00 | PfromR min(PL,PR) | PK -
 //   RL (b-loop, l side):     PRmloop00 PMmloop00 | POmloop00 PMmloop10 | POmloop10 PfromR | PfromO -
 // Values are the stored (clamped) int16 matrix values; unused slots hold 32767.
-enum RecType { RA = 0, RK = 1, RL = 2, NREC = 3 };
+enum RecType { RA = 0, RL = 1, NREC = 2 };  // 16-byte record types in T.rec (RK lives in T.rk)
+static_assert(sizeof(uint3) == 12, "RK records are 12 bytes");
 
 // Split-point sharing (k_level4d).  The cells of one gap column — same (j,k,l)
 // for the i-side split, (i,k,l) j-side, (i,j,l) k-side, (i,j,k) l-side — sit on consecutive levels
@@ -219,8 +222,9 @@ struct DevTables {
     int16_t *d4;                   // 4-D storage base
     const long long *lb;           // element offset of level t in d4
     const LvlDev *ld;             // per-level descriptors
-    uint4 *rec;                    // AoS loop records, level t at ld[t].lr
+    uint4 *rec;                    // AoS loop records RA, RL: level t at ld[t].lr
     long long nrec;                // records allocated (debug bounds checks)
+    uint3 *rk;                     // RK records: level t at ld[t].lr / 2 (nrec / 2 of them)
     // interior-loop copies of PL / PR / PM, laid out so that the lanes of one k_iloop wave share
     // the loop's closing pair:
     //   PLx(t,a,h,i) = lbx + a*M + G(i-1) + h               (h fastest: fixed (i,j), lanes k)
@@ -262,12 +266,12 @@ __device__ __forceinline__ int rlo16(unsigned w) { return (int)(int16_t)(w & 0xf
 __device__ __forceinline__ int rhi16(unsigned w) { return (int)(int16_t)(w >> 16); }
 __device__ __forceinline__ int rec_get(const DevTables &T, int x, const LvlDev &L, long long cell) {
     const uint4 *rp = T.rec + L.lr;
-    if (x == PRmloop00 || x == PfromR) {  // RK: Rm00|Mm00, fR|PLR, K|-, -|-
-        const uint4 r = rp[L.C + cell];
+    if (x == PRmloop00 || x == PfromR) {  // RK: Rm00|Mm00, fR|PLR, K|-
+        const uint3 r = T.rk[(L.lr >> 1) + cell];
         return x == PRmloop00 ? rlo16(r.x) : rlo16(r.y);
     }
     if (x == PMmloop10 || x == POmloop10) {  // RL: Rm00|Mm00, Om00|Mm10, Om10|fR, fO|-
-        const uint4 r = rp[2 * (long long)L.C + cell];
+        const uint4 r = rp[(long long)L.C + cell];
         return x == PMmloop10 ? rhi16(r.y) : rlo16(r.z);
     }
     const uint4 r = rp[cell];  // RA: Lm00|Mm00, Om00|fL, fO|Lm10, fMp|K

@@ -141,7 +141,8 @@ struct ccj_ctx {
     LvlDev *d_ld = nullptr;
     int16_t *d4x = nullptr, *pmx = nullptr;  // interior-loop copies of PL/PR and PM (IT_PAD into the allocations)
     int16_t *d4x_alloc = nullptr, *pmx_alloc = nullptr;
-    uint4 *d_rec = nullptr;                  // AoS loop records
+    uint4 *d_rec = nullptr;                  // AoS loop records RA, RL (16 bytes)
+    uint3 *d_rk = nullptr;                   // AoS loop records RK (12 bytes)
     uint4 *d_acc = nullptr;                  // partial-record ring (split-point sharing)
     int16_t *d_lord = nullptr;               // long-scan a-blocks per sharing level, longest first
     int *d_lord_off = nullptr;
@@ -1811,8 +1812,10 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
         return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for 4-D matrices failed", c->total4 * 2e-9);
     // AoS loop records: NREC 16-byte records per cell (ccj_engine.h)
     c->nrec = c->ncell * NREC;
-    if (c->nrec > 0 && hipMalloc(&c->d_rec, (size_t)c->nrec * sizeof(uint4)) != hipSuccess)
-        return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for loop records failed", c->nrec * 16e-9);
+    if (c->nrec > 0 && (hipMalloc(&c->d_rec, (size_t)c->nrec * sizeof(uint4)) != hipSuccess ||
+                        hipMalloc(&c->d_rk, (size_t)c->ncell * sizeof(uint3)) != hipSuccess))
+        return set_err(cp, CCJ_E_OOM, "device allocation of %.2f GB for loop records failed",
+                       c->nrec * 16e-9 + c->ncell * 12e-9);
     // split-point sharing: the level range it covers (every level of it runs unsplit, so each leader
     // and its followers run one cell per lane) and the partial-record ring
     int g_lo = 0, g_hi = 0;
@@ -2011,6 +2014,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     T.ld = c->d_ld;
     T.d4x = c->d4x;
     T.rec = c->d_rec;
+    T.rk = c->d_rk;
     T.nrec = c->nrec;
     T.pmx = c->pmx;
     T.nx = c->nx;
@@ -3107,6 +3111,7 @@ extern "C" void ccj_destroy(ccj_ctx *c) {
     hipFree(c->d_icount);
     hipFree(c->d_ioff);
     hipFree(c->d_rec);
+    hipFree(c->d_rk);
     hipFree(c->d_acc);
     hipFree(c->d_wterm);
     hipFree(c->d_lord);

@@ -1149,8 +1149,8 @@ __device__ __forceinline__ void write_records(const DevTables &T, long long lr, 
                                               int PLR, int Mm10, int Om10) {
     uint4 *rp = T.rec + lr;
     rp[cell] = make_uint4(pk16(Lm00, Mm00), pk16(Om00, fL), pk16(fO, Lm10), pk16(fMp, K));
-    rp[(unsigned)C + cell] = make_uint4(pk16(Rm00, Mm00), pk16(fR, PLR), pk16(K, INTERN_INF), pk16(INTERN_INF, INTERN_INF));
-    rp[2u * (unsigned)C + cell] = make_uint4(pk16(Rm00, Mm00), pk16(Om00, Mm10), pk16(Om10, fR), pk16(fO, INTERN_INF));
+    T.rk[(lr >> 1) + cell] = make_uint3(pk16(Rm00, Mm00), pk16(fR, PLR), pk16(K, INTERN_INF));
+    rp[(unsigned)C + cell] = make_uint4(pk16(Rm00, Mm00), pk16(Om00, Mm10), pk16(Om10, fR), pk16(fO, INTERN_INF));
 }
 
 
@@ -1282,11 +1282,14 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         i + (di) > m + (dt) - h - (dh)) atomicOr(T.err, 4)
 #define CHKR(idx) \
     if ((long long)(idx) < 0 || (long long)(idx) >= T.nrec) atomicOr(T.err, 8)
+#define CHKK(idx) \
+    if ((long long)(idx) < 0 || (long long)(idx) >= T.nrec / 2) atomicOr(T.err, 8)
 #define CHKA(idx) \
     if (!T.acc || (long long)(idx) >= T.accC) atomicOr(T.err, 256)
 #else
 #define CHK(dt, ap_, dh, di)
 #define CHKR(idx)
+#define CHKK(idx)
 #define CHKA(idx)
 #endif
 
@@ -1525,7 +1528,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
     // ---- fused b-loop: split point d inside [k, l] ----
     int pRm00 = seed, pRm01 = INF, pRm10 = INF, pMm01 = INF, pOm01 = INF;
     int fR1 = INF, fR2 = INF, fMp = INF, fO2 = INF, pK2 = INF;
-    struct BV { int2 w2k, w2l; uint4 wk, wl; int s; };  // raw loads of one split step
+    struct BV { int2 w2k, w2l; uint3 wk; uint4 wl; int s; };  // raw loads of one split step
     auto load_b = [&](int s) {
         BV v;
         v.s = s;
@@ -1546,10 +1549,11 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         // RK at X(i,j,d,l): x = Rm00|Mm00, y = fR|min(PL,PR), z = K|-
         // RL at X(i,j,k,d): x = Rm00|Mm00, y = Om00|Mm10, z = Om10|fR, w = fO|-
         const uint4 *rp = T.rec + L.lr;
-        CHKR(L.lr + L.C + (unsigned)Uk + L0);
-        CHKR(L.lr + 2 * L.C + (unsigned)Ul + lh);
-        v.wk = rp[(unsigned)(L.C + Uk) + L0];
-        v.wl = rp[(unsigned)(2 * L.C + Ul) + lh];
+        const uint3 *kp = T.rk + (L.lr >> 1);
+        CHKK((L.lr >> 1) + (unsigned)Uk + L0);
+        CHKR(L.lr + L.C + (unsigned)Ul + lh);
+        v.wk = kp[(unsigned)Uk + L0];
+        v.wl = rp[(unsigned)(L.C + Ul) + lh];
         return v;
     };
     auto step_b = [&](const BV &v, int mask) {
@@ -1585,7 +1589,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #pragma unroll
             for (int f = 0; f < 9; ++f) AL_[r][f] = INF;
         }
-        struct LB { uint4 wk, wl; int2 q[SHARE_R], p[SHARE_R]; int s; };  // raw loads of one split step
+        struct LB { uint3 wk; uint4 wl; int2 q[SHARE_R], p[SHARE_R]; int s; };  // raw loads of one split step
         auto ld = [&](int s) {
             LB v;
             v.s = s;
@@ -1594,10 +1598,11 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             const int Ul = a * L.M;
             const unsigned lh = L0 + uh * (unsigned)s;
             const uint4 *rp = T.rec + L.lr;
-            CHKR(L.lr + L.C + (unsigned)Uk + L0);
-            CHKR(L.lr + 2 * L.C + (unsigned)Ul + lh);
-            v.wk = rp[(unsigned)(L.C + Uk) + L0];
-            v.wl = rp[(unsigned)(2 * L.C + Ul) + lh];
+            const uint3 *kp = T.rk + (L.lr >> 1);
+            CHKK((L.lr >> 1) + (unsigned)Uk + L0);
+            CHKR(L.lr + L.C + (unsigned)Ul + lh);
+            v.wk = kp[(unsigned)Uk + L0];
+            v.wl = rp[(unsigned)(L.C + Ul) + lh];
 #pragma unroll
             for (int r = 0; r < SHARE_R; ++r) {
                 const int o = (s - 1 + r) * rs;
@@ -1775,7 +1780,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
                 vPMm01 = imin(vPMm01, LDX(lp, L, PMmloop01, a * L.M + m + 1, L0) + cp);       // (i,j,k+1,l)
             }
             // PMmloop10 from the RL record (d4 does not store it: ccj_engine.h rec_only)
-            if (a >= 1) vPMm10 = imin(vPMm10, hi16(T.rec[L.lr + (unsigned)(2 * L.C + (a - 1) * L.M + m + 1) + L0].y) + cp);  // (i,j-1,k,l)
+            if (a >= 1) vPMm10 = imin(vPMm10, hi16(T.rec[L.lr + (unsigned)(L.C + (a - 1) * L.M + m + 1) + L0].y) + cp);  // (i,j-1,k,l)
         }
     }
     const int vPLm00 = pLm00, vPLm01 = pLm01, vPLm10 = pLm10, vPRm00 = pRm00, vPMm00 = pMm00;
@@ -1825,7 +1830,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
 #endif
         }
         const int b2 = (b >= 2) ? imin(LDX(lp2, L2, PRmloop10, Uin, L0 + uh), LDX(lp2, L2, PRmloop01, Uin, L0 + uh)) + apbp2 : INF;
-        const int b3 = (b >= TURN + 1) ? lo16(rp2[(unsigned)(L2.C + Uin) + L0 + uh].y) : INF;  // RK: ., fR|.
+        const int b3 = (b >= TURN + 1) ? lo16(T.rk[(L2.lr >> 1) + (unsigned)Uin + L0 + uh].y) : INF;  // RK: ., fR|.
         vPR = imin(imin(b1, b2), b3);
     }
     // ---- PM (:277-300) with get_PMiloop (:752-773, k_iloop), get_PMmloop (:775-785)
@@ -1842,7 +1847,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
             if (a >= 2 && b >= 2) b1 = imin(b1, imin(pin + W2E(T.ie, j - 1, k + 1), (int)dst[mslot(PM) * C]));
 #endif
         }
-        const int b2 = inner ? imin(hi16(rp2[(unsigned)(2 * L2.C + Uin) + L0].y), LDX(lp2, L2, PMmloop01, Uin, L0)) + apbp2 : INF;  // RL: ., .|Mm10
+        const int b2 = inner ? imin(hi16(rp2[(unsigned)(L2.C + Uin) + L0].y), LDX(lp2, L2, PMmloop01, Uin, L0)) + apbp2 : INF;  // RL: ., .|Mm10
         const int b3 = inner ? LDX(lp2, L2, PfromM, Uin, L0) : INF;
         const int b4 = (a == 0 && b == 0) ? 0 : INF;
         vPM = imin(imin(b1, b2), imin(b3, b4));
@@ -1854,7 +1859,7 @@ __device__ __forceinline__ void level4d_body(const DevTables &T, int t, int wave
         const int Uin = (a - 1) * L2.M + 1;  // (i+1, j, k, l-1): lane L0 + 2h
         int b1 = INF;
         if (l - i > TURN && inner) b1 = LDX(lp2, L2, PO, Uin, L0 + 2 * uh) + W2E(T.est, i, l);
-        const uint4 rl = inner ? rp2[(unsigned)(2 * L2.C + Uin) + L0 + 2 * uh] : make_uint4(0, 0, 0, 0);  // RL: ., ., Om10|., fO|.
+        const uint4 rl = inner ? rp2[(unsigned)(L2.C + Uin) + L0 + 2 * uh] : make_uint4(0, 0, 0, 0);  // RL: ., ., Om10|., fO|.
         const int b2 = inner ? imin(lo16(rl.z), LDX(lp2, L2, POmloop01, Uin, L0 + 2 * uh)) + apbp2 : INF;
         const int b3 = (inner && l - i >= TURN + 1) ? lo16(rl.w) : INF;
         vPO = imin(imin(b1, b2), b3);
