@@ -180,6 +180,7 @@ struct ccj_pf_ctx {
     long long *d_Pacc = nullptr;
     unsigned long long *d_Pabs = nullptr;
     int *d_d4 = nullptr;
+    int *d_prec = nullptr;  // split-loop operand records (PfDev::r1 .. r4)
     int *d_cx = nullptr, *d_pmx = nullptr;  // k_pf_iloop's copies of PL / PR and PM (ccj_pf_engine.h)
     double *d_R = nullptr;                  // k_pf_iloop's sums of one level, 3 planes of max C_t
     uint32_t *d_items = nullptr, *d_mO = nullptr, *d_mI = nullptr;
@@ -240,7 +241,8 @@ extern "C" void ccj_pf_footprint(int n, unsigned long long *device_bytes, unsign
                 if (alo <= ahi) rows += (unsigned long long)((ahi - alo) / 64 + 1);
             }
     }
-    unsigned long long dev = ie + (d4 + cx + pmx) * sizeof(int) + 2ull * 3 * maxC * sizeof(double);
+    unsigned long long dev = ie + (d4 + cx + pmx + (unsigned long long)PF_RECS * (d4 / PF_NMAT4)) * sizeof(int) +
+                             2ull * 3 * maxC * sizeof(double);  // d4, copies, split-loop records, R
     dev += (unsigned long long)CCJ_PF_NMAT2 * plane * sizeof(double) + 2 * plane * sizeof(long long);  // 2-D, Pacc, Pabs
     dev += 3 * plane * sizeof(double) + plane + 2ull * plane * PF_IEW * sizeof(uint32_t);             // hp, est, cp; pt; mO, mI
     dev += rows * sizeof(uint32_t) + sizeof(PfExp) + (1u << 20);                                      // items; small tables
@@ -329,7 +331,7 @@ void run_threads(int total, int nthr, const std::function<void(int, int)> &f) {
 void free_dev(ccj_pf_ctx *c) {
     void *ptrs[] = {c->d_E, c->d_S, c->d_S1, c->d_pt, c->d_pair, c->d_rtype, c->d_hp, c->d_est, c->d_ieO, c->d_ieI,
                     c->d_mlb, c->d_cpp, c->d_pup, c->d_2d, c->d_Pacc, c->d_Pabs, c->d_d4, c->d_cx, c->d_pmx,
-                    c->d_R, c->d_items, c->d_mO, c->d_mI, c->d_ld};
+                    c->d_prec, c->d_R, c->d_items, c->d_mO, c->d_mI, c->d_ld};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (c->e0) hipEventDestroy(c->e0);
@@ -597,11 +599,11 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
             }
 
     // level layout
-    c->lv.assign(std::max(n - 2, 1), PfLvl{0, 0, 0, 0, 0, 0});
+    c->lv.assign(std::max(n - 2, 1), PfLvl{0, 0, 0, 0, 0, 0, 0});
     long long off = 0, offx = 0, offm = 0, maxC = 1;
     for (int t = 0; t <= n - 3; ++t) {
         const long long m = n - t - 2, M = m * (m + 1) / 2;
-        c->lv[t] = PfLvl{off, (t + 1) * M, (int)M, 0, offx, offm};
+        c->lv[t] = PfLvl{off, (t + 1) * M, (int)M, 0, offx, offm, c->cells};
         off += (long long)PF_NMAT4 * (t + 1) * M;
         offx += 2 * (t + 1) * M;
         offm += m * n * (t + 1);
@@ -706,6 +708,7 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     PFCHK(c, hipMalloc((void **)&c->d_Pacc, plane * sizeof(long long)));
     PFCHK(c, hipMalloc((void **)&c->d_Pabs, plane * sizeof(unsigned long long)));
     PFCHK(c, hipMalloc((void **)&c->d_d4, (size_t)std::max(off, 1LL) * sizeof(int)));
+    PFCHK(c, hipMalloc((void **)&c->d_prec, (size_t)PF_RECS * std::max(c->cells, 1LL) * sizeof(int)));
     // the copies stay 0 where the pair cannot pair (never written): set once per context
     PFCHK(c, hipMalloc((void **)&c->d_cx, (size_t)std::max(offx, 1LL) * sizeof(int)));
     PFCHK(c, hipMalloc((void **)&c->d_pmx, (size_t)std::max(offm, 1LL) * sizeof(int)));
@@ -747,6 +750,10 @@ int create_impl(const ccj_problem *prob, const ccj_pf_raw *raw, int device, ccj_
     D.Pacc = c->d_Pacc;
     D.Pabs = c->d_Pabs;
     D.d4 = c->d_d4;
+    D.r1 = c->d_prec;
+    D.r2 = D.r1 + (size_t)PF_REC1 * c->cells;
+    D.r3 = D.r2 + (size_t)PF_REC2 * c->cells;
+    D.r4 = D.r3 + (size_t)PF_REC3 * c->cells;
     D.cx = c->d_cx;
     D.pmx = c->d_pmx;
     D.items = c->d_items;

@@ -72,10 +72,10 @@ struct PfG {  // getters with the reference's semantics
 __device__ __forceinline__ double ldc_f64(const double *p) {
     return *(const __attribute__((address_space(4))) double *)(unsigned long long)p;
 }
-struct PfLvlS { long long lb, C; int M; };
+struct PfLvlS { long long lb, C; int M; long long lr; };
 __device__ __forceinline__ PfLvlS ldc_lvl(const PfLvl *p) {
     const auto *q = (const __attribute__((address_space(4))) PfLvl *)(unsigned long long)p;
-    return PfLvlS{q->lb, q->C, q->M};
+    return PfLvlS{q->lb, q->C, q->M, q->lr};
 }
 
 // Buffer loads with a wave-uniform 32-bit byte offset (soffset) and a per-lane one (voffset) from a
@@ -92,6 +92,15 @@ __device__ __forceinline__ int bld32(__amdgpu_buffer_rsrc_t r, int voff, int sof
 }
 __device__ __forceinline__ double bld64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+// a split-loop record's first three / next two or three ints (ccj_pf_engine.h PfDev::r1 .. r4)
+typedef unsigned __attribute__((ext_vector_type(3))) pfu3;
+typedef unsigned __attribute__((ext_vector_type(2))) pfu2;
+__device__ __forceinline__ pfu3 bld96(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_amdgcn_raw_buffer_load_b96(r, voff, soff, 0);
+}
+__device__ __forceinline__ pfu2 bld64u(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
 }
 
 // Software-pipelined split loop over s = s0 .. s1: the loads of step s+1 are issued before step s
@@ -593,7 +602,7 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     // split-loop operands as buffer loads: the 2-D tables from their starts (lane offset 8i / 8k),
     // the 4-D values from the start of their level (lane offset 4(off + h*(dt-dh)))
     const __amdgpu_buffer_rsrc_t rWBP = pf_rsrc(WBP), rWPP = pf_rsrc(WPP);
-    const int vi8 = 8 * i, vk8 = 8 * k, rs8 = 8 * rs, voff4 = 4 * off;
+    const int vi8 = 8 * i, vk8 = 8 * k, rs8 = 8 * rs;
     struct SA { double bpi, wppi, bpj, wppj; int lm1, mm1, om1, fl1, fo1, lm2, l102, mm2, fl2, fm2, k2, s; };
     auto ldA = [&](int s) {
         SA v;
@@ -604,23 +613,26 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         v.bpj = bld64(rWBP, vi8, oj);
         v.wppi = bld64(rWPP, vi8, oi);
         v.wppj = bld64(rWPP, vi8, oj);
-        // X1 = X(i+s, j, k, l) = (t-s, a-s, h, i+s): level start + 4((a-s)M + s) + lane 4(off + h s)
-        const __amdgpu_buffer_rsrc_t r1 = pf_rsrc(D.d4 + L1.lb);
-        const int C1 = 4 * (int)L1.C, s1 = 4 * ((a - s) * L1.M + s), v1 = voff4 + 4 * h * s;
-        v.lm1 = bld32(r1, v1, s1 + PF_PLmloop00 * C1);
-        v.mm1 = bld32(r1, v1, s1 + PF_PMmloop00 * C1);
-        v.om1 = bld32(r1, v1, s1 + PF_POmloop00 * C1);
-        v.fl1 = bld32(r1, v1, s1 + PF_PfromL * C1);
-        v.fo1 = bld32(r1, v1, s1 + PF_PfromO * C1);
-        // X2 = X(i, i+s, k, l) = (b+s, s, h+a-s, i): level start + 4(s M + G(a-s)) + lane 4 off
-        const __amdgpu_buffer_rsrc_t r2 = pf_rsrc(D.d4 + L2.lb);
-        const int dh = a - s, C2 = 4 * (int)L2.C, s2 = 4 * (s * L2.M + dh * (m + dh) - ((dh * (dh - 1)) >> 1));
-        v.lm2 = bld32(r2, voff4, s2 + PF_PLmloop00 * C2);
-        v.l102 = bld32(r2, voff4, s2 + PF_PLmloop10 * C2);
-        v.mm2 = bld32(r2, voff4, s2 + PF_PMmloop00 * C2);
-        v.fl2 = bld32(r2, voff4, s2 + PF_PfromL * C2);
-        v.fm2 = bld32(r2, voff4, s2 + PF_PfromM * C2);
-        v.k2 = bld32(r2, voff4, s2 + PF_PK * C2);
+        // X1 = X(i+s, j, k, l) = (t-s, a-s, h, i+s): its r1 record, record (a-s)M + s + lane (off + h s)
+        const __amdgpu_buffer_rsrc_t r1 = pf_rsrc(D.r1 + PF_REC1 * L1.lr);
+        const int s1 = 4 * PF_REC1 * ((a - s) * L1.M + s), v1 = 4 * PF_REC1 * (off + h * s);
+        const pfu3 p1 = bld96(r1, v1, s1);
+        const pfu2 q1 = bld64u(r1, v1, s1 + 12);
+        v.lm1 = (int)p1.x;
+        v.mm1 = (int)p1.y;
+        v.om1 = (int)p1.z;
+        v.fl1 = (int)q1.x;
+        v.fo1 = (int)q1.y;
+        // X2 = X(i, i+s, k, l) = (b+s, s, h+a-s, i): its r2 record, record s M + G(a-s) + lane off
+        const __amdgpu_buffer_rsrc_t r2 = pf_rsrc(D.r2 + PF_REC2 * L2.lr);
+        const int dh = a - s, s2 = 4 * PF_REC2 * (s * L2.M + dh * (m + dh) - ((dh * (dh - 1)) >> 1)), v2 = 4 * PF_REC2 * off;
+        const pfu3 p2 = bld96(r2, v2, s2), q2 = bld96(r2, v2, s2 + 12);
+        v.lm2 = (int)p2.x;
+        v.l102 = (int)p2.y;
+        v.mm2 = (int)p2.z;
+        v.fl2 = (int)q2.x;
+        v.fm2 = (int)q2.y;
+        v.k2 = (int)q2.z;
         return v;
     };
     auto rdA = [&](const SA &v) {
@@ -674,23 +686,26 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         v.bpl = bld64(rWBP, vk8, ol);
         v.wppk = bld64(rWPP, vk8, ok);
         v.wppl = bld64(rWPP, vk8, ol);
-        // X3 = X(i, j, k+s, l) = (t-s, a, h+s, i): level start + 4(a M + G(s) at m+s) + lane 4 off
-        const __amdgpu_buffer_rsrc_t r3 = pf_rsrc(D.d4 + L3.lb);
-        const int C3 = 4 * (int)L3.C, s3 = 4 * (a * L3.M + s * (m + s) - ((s * (s - 1)) >> 1));
-        v.rm3 = bld32(r3, voff4, s3 + PF_PRmloop00 * C3);
-        v.mm3 = bld32(r3, voff4, s3 + PF_PMmloop00 * C3);
-        v.fr3 = bld32(r3, voff4, s3 + PF_PfromR * C3);
-        v.fm3 = bld32(r3, voff4, s3 + PF_PfromM * C3);
-        v.k3 = bld32(r3, voff4, s3 + PF_PK * C3);
-        // X4 = X(i, j, k, k+s) = (a+s, a, h, i): level start + 4 a M + lane 4(off + h (b-s))
-        const __amdgpu_buffer_rsrc_t r4 = pf_rsrc(D.d4 + L4.lb);
-        const int C4 = 4 * (int)L4.C, s4 = 4 * (a * L4.M), v4 = voff4 + 4 * h * (b - s);
-        v.rm4 = bld32(r4, v4, s4 + PF_PRmloop00 * C4);
-        v.mm4 = bld32(r4, v4, s4 + PF_PMmloop00 * C4);
-        v.om4 = bld32(r4, v4, s4 + PF_POmloop00 * C4);
-        v.o104 = bld32(r4, v4, s4 + PF_POmloop10 * C4);
-        v.fr4 = bld32(r4, v4, s4 + PF_PfromR * C4);
-        v.fo4 = bld32(r4, v4, s4 + PF_PfromO * C4);
+        // X3 = X(i, j, k+s, l) = (t-s, a, h+s, i): its r3 record, record a M + G(s) at m+s + lane off
+        const __amdgpu_buffer_rsrc_t r3 = pf_rsrc(D.r3 + PF_REC3 * L3.lr);
+        const int s3 = 4 * PF_REC3 * (a * L3.M + s * (m + s) - ((s * (s - 1)) >> 1)), v3 = 4 * PF_REC3 * off;
+        const pfu3 p3 = bld96(r3, v3, s3);
+        const pfu2 q3 = bld64u(r3, v3, s3 + 12);
+        v.rm3 = (int)p3.x;
+        v.mm3 = (int)p3.y;
+        v.fr3 = (int)p3.z;
+        v.fm3 = (int)q3.x;
+        v.k3 = (int)q3.y;
+        // X4 = X(i, j, k, k+s) = (a+s, a, h, i): its r4 record, record a M + lane (off + h (b-s))
+        const __amdgpu_buffer_rsrc_t r4 = pf_rsrc(D.r4 + PF_REC4 * L4.lr);
+        const int s4 = 4 * PF_REC4 * (a * L4.M), v4 = 4 * PF_REC4 * (off + h * (b - s));
+        const pfu3 p4 = bld96(r4, v4, s4), q4 = bld96(r4, v4, s4 + 12);
+        v.rm4 = (int)p4.x;
+        v.mm4 = (int)p4.y;
+        v.om4 = (int)p4.z;
+        v.o104 = (int)q4.x;
+        v.fr4 = (int)q4.y;
+        v.fo4 = (int)q4.z;
         return v;
     };
     auto rdB = [&](const SB &v) {
@@ -755,18 +770,18 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
     const int xFO = inM ? Xs(L2, PF_PfromO, 2, 1, 0, 1) : 0;
     const double eO = D.est[(t + h + 2) * rs + i];
 
-    put(PF_PLmloop00, cLm00);
+    const int sLm00 = put(PF_PLmloop00, cLm00);
     put(PF_PLmloop01, cLm01);
-    put(PF_PLmloop10, cLm10);
-    put(PF_PRmloop00, cRm00);
+    const int sLm10 = put(PF_PLmloop10, cLm10);
+    const int sRm00 = put(PF_PRmloop00, cRm00);
     put(PF_PRmloop01, cRm01);
     put(PF_PRmloop10, cRm10);
-    put(PF_PMmloop00, cMm00);
+    const int sMm00 = put(PF_PMmloop00, cMm00);
     put(PF_PMmloop01, cMm01);
     put(PF_PMmloop10, cMm10);
-    put(PF_POmloop00, cOm00);
+    const int sOm00 = put(PF_POmloop00, cOm00);
     put(PF_POmloop01, cOm01);
-    put(PF_POmloop10, cOm10);
+    const int sOm10 = put(PF_POmloop10, cOm10);
 
     // PL (:414-430) with get_PLiloop (:736-756) and get_PLmloop (:758-768)
     int PL = 0;
@@ -840,30 +855,31 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         }
         PO = put(PF_PO, c);
     }
+    int sFL, sFR, sFM, sFO, sK;
     {  // PfromL (:488-503): split terms above, then the same-cell P* terms
         double c = cFL;
         c += PR * 1.0 * PB;
         c += PM * 1.0 * PB;
         c += PO * 1.0 * PB;
-        put(PF_PfromL, c);
+        sFL = put(PF_PfromL, c);
     }
     {  // PfromR (:505-518)
         double c = cFR;
         c += PM * 1.0 * PB;
         c += PO * 1.0 * PB;
-        put(PF_PfromR, c);
+        sFR = put(PF_PfromR, c);
     }
     {  // PfromM (:520-535)
         double c = cFM;
         c += PL * 1.0 * PB;
         c += PR * 1.0 * PB;
-        put(PF_PfromM, c);
+        sFM = put(PF_PfromM, c);
     }
     {  // PfromO (:537-552)
         double c = cFO;
         c += PL * 1.0 * PB;
         c += PR * 1.0 * PB;
-        put(PF_PfromO, c);
+        sFO = put(PF_PfromO, c);
     }
     {  // PK (:395-412)
         double c = cK;
@@ -871,8 +887,15 @@ __global__ __launch_bounds__(256) void k_pf_level(PfDev D, int t) {
         c += PM * 1.0 * PB;
         c += PR * 1.0 * PB;
         c += PO * 1.0 * PB;
-        put(PF_PK, c);
+        sK = put(PF_PK, c);
     }
+    // the cell's split-loop records (ccj_pf_engine.h PfDev::r1 .. r4), read by later levels
+    const long long rc = L.lr + off0;
+    int *w1 = D.r1 + PF_REC1 * rc, *w2 = D.r2 + PF_REC2 * rc, *w3 = D.r3 + PF_REC3 * rc, *w4 = D.r4 + PF_REC4 * rc;
+    w1[0] = sLm00; w1[1] = sMm00; w1[2] = sOm00; w1[3] = sFL; w1[4] = sFO;
+    w2[0] = sLm00; w2[1] = sLm10; w2[2] = sMm00; w2[3] = sFL; w2[4] = sFM; w2[5] = sK;
+    w3[0] = sRm00; w3[1] = sMm00; w3[2] = sFR; w3[3] = sFM; w3[4] = sK;
+    w4[0] = sRm00; w4[1] = sMm00; w4[2] = sOm00; w4[3] = sOm10; w4[4] = sFR; w4[5] = sFO;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -49,6 +49,7 @@ struct PfLvl {
     int pad;
     long long lbx; // element offset of level t in the PL/PR copies (PLx then PRx, C each)
     long long pmb; // element offset of level t in the PM copy (m * n * (t+1))
+    long long lr;  // cells of the levels below t: level t's first split-loop record (PfDev::r1 .. r4)
 };
 
 struct PfDev {
@@ -76,7 +77,17 @@ struct PfDev {
     const uint32_t *items;  // k_pf_iloop work items of all levels (ccj_items.h)
     double *R;              // k_pf_iloop's interior-loop sums, two level buffers (t & 1) of [role][a*M + off]
     long long Rst;          // doubles per buffer (3 * max C_t)
+    // split-loop operand records, written by k_pf_level with the cell, indexed like a
+    // matrix (record lr + a*M + off): the values one side of a split step reads at one neighbour,
+    // contiguous, so a step costs two buffer loads per side instead of five or six int loads
+    //   r1 (X1 = X(d,j,k,l), 5 ints): PLmloop00 PMmloop00 POmloop00 PfromL PfromO
+    //   r2 (X2 = X(i,d,k,l), 6 ints): PLmloop00 PLmloop10 PMmloop00 PfromL PfromM PK
+    //   r3 (X3 = X(i,j,d,l), 5 ints): PRmloop00 PMmloop00 PfromR PfromM PK
+    //   r4 (X4 = X(i,j,k,d), 6 ints): PRmloop00 PMmloop00 POmloop00 POmloop10 PfromR PfromO
+    int *r1, *r2, *r3, *r4;
 };
+constexpr int PF_REC1 = 5, PF_REC2 = 6, PF_REC3 = 5, PF_REC4 = 6;
+constexpr int PF_RECS = PF_REC1 + PF_REC2 + PF_REC3 + PF_REC4;  // ints per cell
 
 }  // namespace ccj
 
