@@ -191,8 +191,9 @@ int  ccj_level_layout(int n, int t, int world, long long *C, int *M);
  * int16 elements: out3 = {nmax (the largest rank's block count of the part), tail offset, slice size}.
  * The body is [matrix][part index][cell] of nmax blocks per matrix. */
 int  ccj_exchange_layout(int n, int t, int world, int part, long long *out3);
-/* which = 0: for each body element of rank's slice of the part, the level element (x*C + a*M + c)
- * packed there (-1: padding); which = 1: for each level element, its position in the part's
+/* which = 0: for each body element of rank's slice of the part, the level element (x*C + a*M + c:
+ * matrix-major by matrix index x of ccj_mat4; d4 keeps matrix x at its storage slot) packed there
+ * (-1: padding); which = 1: for each level element, its position in the part's
  * gathered buffer (owner * slice + body position) as rank unpacks it (-1: rank's own cell or the other
  * part's).  Returns the entry count; fills out only when cap >= that count.  < 0: bad arguments. */
 long long ccj_exchange_index(int n, int t, int world, int rank, int part, int which, long long *out, long long cap);
