@@ -33,8 +33,12 @@ struct DV {
     int n, rs;
     const int *W;
     mutable int bad;  // Matrix4D::get_uc assert (matrices.hh:167) hit by this lane
+    // the small tables every candidate reads (k_backtrack: copies in LDS; else T's)
+    const short *S, *S1;
+    const int8_t *pair, *rtype;
+    const LvlDev *ld;
 
-    __device__ __forceinline__ int pr(int i, int j) const { return T.pair[T.S[i] * 8 + T.S[j]]; }
+    __device__ __forceinline__ int pr(int i, int j) const { return pair[S[i] * 8 + S[j]]; }
     __device__ __forceinline__ int a2(const int *A, int i, int j) const { return A[(j - i) * rs + i]; }
     // s_energy_matrix.hh:37-43
     __device__ __forceinline__ int V(int i, int j) const { return i >= j ? INF : a2(T.V, i, j); }
@@ -65,7 +69,7 @@ struct DV {
             return INF;
         }
         const int t = (j - i) + (l - k), m = n - t - 2, h = k - j - 2, a = j - i;
-        const LvlDev L = T.ld[t];
+        const LvlDev L = ld[t];
         const long long cell = (long long)a * L.M + h * m - ((h * (h - 1)) >> 1) + i - 1;
         if (!T.mat5 && rec_only(x)) return rec_get(T, x, L, cell);  // record-only matrix (ccj_engine.h)
         return (int)T.d4[L.lb + (long long)mslot(x) * L.C + cell];
@@ -73,8 +77,8 @@ struct DV {
     __device__ __forceinline__ bool can_pair(int i, int j) const { return (j - i > TURN) && pr(i, j) > 0; }  // pseudo_loop.hh:131-135
     // pseudo_loop.cc:822-840 (lrint = round-half-even in double)
     __device__ __forceinline__ int compute_int(int i, int j, int k, int l) const {
-        return E_IntLoop(T.prm, T.lx, k - i - 1, j - l - 1, pr(i, j), T.rtype[pr(k, l)], T.S1[i + 1], T.S1[j - 1],
-                         T.S1[k - 1], T.S1[l + 1]);
+        return E_IntLoop(T.prm, T.lx, k - i - 1, j - l - 1, pr(i, j), rtype[pr(k, l)], S1[i + 1], S1[j - 1], S1[k - 1],
+                         S1[l + 1]);
     }
     __device__ __forceinline__ int e_stP(int i, int j) const {
         if (i + 1 == j - 1) return INF;
@@ -156,7 +160,7 @@ __device__ __forceinline__ int wmin(int count, F f) {
 
 // W_final.cc:118-173
 __device__ int E_ext_Stem(const DV &H, int dangles, int vij, int vi1j, int vij1, int vi1j1, int i, int j) {
-    const short *S = H.T.S;
+    const short *S = H.S;
     const int n = H.n;
     int e = INF, en;
     int tt = H.pr(i, j);
@@ -189,7 +193,7 @@ __device__ int E_ext_Stem(const DV &H, int dangles, int vij, int vi1j, int vij1,
 // parallel; k_compute_W then runs the recurrence in one wave, j ascending, k over the lanes.
 __global__ __launch_bounds__(256) void k_w_terms(DevTables T, int *S) {
     const int n = T.n;
-    DV H{T, n, T.rs, nullptr, 0};
+    DV H{T, n, T.rs, nullptr, 0, T.S, T.S1, T.pair, T.rtype, T.ld};
     const int j = blockIdx.y + TURN + 1;
     const int k = blockIdx.x * blockDim.x + threadIdx.x + 1;
     if (j > n || k > j - TURN - 1) return;
@@ -395,8 +399,8 @@ __device__ __forceinline__ void Bt::bt_loop(const Interval &cur) {
             const int k = i + 1 + (c >> 5), l = j - 1 - (c & 31);
             const int min_l = imax(k + TURN + 1 + MAXLOOP + 2, k + j - i) - MAXLOOP - 2;
             if (l < min_l) return BIG;
-            return E_IntLoop(H.T.prm, H.T.lx, k - i - 1, j - l - 1, H.pr(i, j), H.T.rtype[H.pr(k, l)], H.T.S1[i + 1],
-                             H.T.S1[j - 1], H.T.S1[k - 1], H.T.S1[l + 1]) + H.V(k, l);
+            return E_IntLoop(H.T.prm, H.T.lx, k - i - 1, j - l - 1, H.pr(i, j), H.rtype[H.pr(k, l)], H.S1[i + 1],
+                             H.S1[j - 1], H.S1[k - 1], H.S1[l + 1]) + H.V(k, l);
         }, bv, bx);
         int best_ip = j, best_jp = i;
         if (bv < INF) {
@@ -413,7 +417,7 @@ __device__ __forceinline__ void Bt::bt_loop(const Interval &cur) {
         }
     } else if (type == T_MULTI) {
         pairup(i, j, T_MULTI);
-        const short *S = H.T.S;
+        const short *S = H.S;
         const ccj_energy_params *P = H.T.prm;
         const int tt = H.pr(j, i);
         // W_final.cc:228-300: per k (ascending) rows 1..8 in order
@@ -458,7 +462,7 @@ __device__ __forceinline__ void Bt::bt_loop(const Interval &cur) {
 __device__ __forceinline__ void Bt::bt_free(const Interval &cur) {
     const int j = cur.j, n = H.n;
     if (j == 1) return;
-    const short *S = H.T.S;
+    const short *S = H.S;
     const int dangles = H.T.dangles;
     const int *W = H.W;
     int mn = INF, best_row = -1, best_i = -1;
@@ -555,7 +559,7 @@ __device__ __forceinline__ void Bt::bt_wm(const Interval &cur) {
 
 __device__ __forceinline__ void Bt::bt_wmv(const Interval &cur) {
     const int i = cur.i, j = cur.j, n = H.n;
-    const short *S = H.T.S;
+    const short *S = H.S;
     const ccj_energy_params *P = H.T.prm;
     const int si = S[i], sj = S[j];
     const int si1 = (i > 1) ? S[i - 1] : -1;
@@ -1135,10 +1139,26 @@ __device__ __forceinline__ void Bt::pl(const Interval &cur) {
 }
 
 // one workgroup of 1..BT_MAXW waves; LDS: the node stack (cap entries)
-__global__ __launch_bounds__(64 * BT_MAXW) void k_backtrack(DevTables T, const int *W, int *f_pair, int8_t *f_type, BtOut *out, int cap) {
+__global__ __launch_bounds__(64 * BT_MAXW) void k_backtrack(DevTables T, const int *W, int *f_pair, int8_t *f_type, BtOut *out, int cap,
+                                                            int lds_ld) {
     extern __shared__ Interval stk[];
     const int n = T.n;
-    DV H{T, n, T.rs, W, 0};
+    // LDS copies of the small tables behind every candidate's first loads (sequence, pair types,
+    // level descriptors), placed after the node stack; the descriptors only when they fit (lds_ld)
+    short *sS = (short *)(stk + cap), *sS1 = sS + (n + 2);
+    int8_t *sPair = (int8_t *)(sS1 + (n + 2)), *sRt = sPair + 64;
+    LvlDev *sLd = (LvlDev *)(((unsigned long long)(sRt + 8) + 15) & ~15ull);
+    for (int x = (int)threadIdx.x; x < n + 2; x += (int)blockDim.x) {
+        sS[x] = T.S[x];
+        sS1[x] = T.S1[x];
+    }
+    for (int x = (int)threadIdx.x; x < 72; x += (int)blockDim.x) {
+        if (x < 64) sPair[x] = T.pair[x];
+        else sRt[x - 64] = T.rtype[x - 64];
+    }
+    if (lds_ld)
+        for (int x = (int)threadIdx.x; x < T.nlev; x += (int)blockDim.x) sLd[x] = T.ld[x];
+    DV H{T, n, T.rs, W, 0, sS, sS1, sPair, sRt, lds_ld ? sLd : T.ld};
     for (int x = (int)threadIdx.x; x <= n; x += (int)blockDim.x) {
         f_pair[x] = -1;
         f_type[x] = (int8_t)T_NONE;
@@ -1193,7 +1213,12 @@ extern "C" int ccjk_backtrack(const void *Tv, const int *W, int *f_pair, int8_t 
         const int w = e ? atoi(e) : BT_WAVES_DEFAULT;
         return w < 1 ? 1 : (w > BT_MAXW ? BT_MAXW : w);
     }();
-    hipLaunchKernelGGL(k_backtrack, dim3(1), dim3(64 * waves), (size_t)stack_cap * sizeof(Interval), (hipStream_t)stream,
-                       *T, W, f_pair, f_type, out, stack_cap);
+    // dynamic LDS: the node stack, then the small tables (k_backtrack); the level descriptors too
+    // while the whole stays within 64 KB
+    const size_t base = (size_t)stack_cap * sizeof(Interval) + 4 * ((size_t)T->n + 2) + 72 + 16;
+    const size_t with_ld = base + (size_t)T->nlev * sizeof(LvlDev);
+    const int lds_ld = with_ld <= 65536 ? 1 : 0;
+    hipLaunchKernelGGL(k_backtrack, dim3(1), dim3(64 * waves), lds_ld ? with_ld : base, (hipStream_t)stream, *T, W, f_pair,
+                       f_type, out, stack_cap, lds_ld);
     return (int)hipGetLastError();
 }
