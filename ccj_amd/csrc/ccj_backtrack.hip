@@ -158,6 +158,33 @@ __device__ __forceinline__ int wmin(int count, F f) {
     return v;
 }
 
+// One pass over candidates that yields both the first minimum (value, position) of f(c).x and the
+// minimum of f(c).y: a get_P?iloop value (pairable inner pairs only, .y) and the argmin its
+// P_P?iloop node takes next over the same candidates (no can_pair filter, .x)
+template <class F>
+__device__ __forceinline__ void scan2(int count, F f, int &fmin, int &bv, int &bx) {
+    int v = BIG, x = BIG, fm = BIG, z = 0;
+    const bool spread = count > REPL_MAX && blockDim.x > 64;
+    const int c0 = spread ? (int)threadIdx.x : (int)(threadIdx.x & 63), dc = spread ? (int)blockDim.x : 64;
+    for (int c = c0; c < count; c += dc) {
+        const int2 t = f(c);
+        if (t.x < v) {
+            v = t.x;
+            x = c;
+        }
+        fm = imin(fm, t.y);
+    }
+    wreduce(v, x);
+    wreduce(fm, z);
+    if (spread) {
+        block_reduce(v, x);
+        block_reduce(fm, z);
+    }
+    fmin = fm;
+    bv = v;
+    bx = x;
+}
+
 // W_final.cc:118-173
 __device__ int E_ext_Stem(const DV &H, int dangles, int vij, int vi1j, int vij1, int vi1j1, int i, int j) {
     const short *S = H.S;
@@ -265,6 +292,19 @@ struct Bt {
     int *f_pair;
     int8_t *f_type;
     BtOut st;  // uniform
+    // the interior-loop argmin a P_PL / PR / PM / PO node computed with its get_P?iloop value, for
+    // the P_P?iloop node it pushes (popped next); type 0: none
+    struct IlCache { int type, i, j, k, l, bv, bx; };
+    mutable IlCache ilc{0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ bool il_cached(int type, int i, int j, int k, int l, int &bv, int &bx) const {
+        const bool hit = ilc.type == type && ilc.i == i && ilc.j == j && ilc.k == k && ilc.l == l;
+        if (hit) {
+            bv = ilc.bv;
+            bx = ilc.bx;
+        }
+        ilc.type = 0;
+        return hit;
+    }
 
     __device__ __forceinline__ void push(int i, int j, int k, int l, int type) {
         if (sp >= cap) {
@@ -302,22 +342,30 @@ struct Bt {
         int mn = INF;
         if (i + TURN + 2 < j) mn = H.g4(PL, i + 1, j - 1, k, l) + H.e_stP(i, j);
         const int nd = imin(j, i + MAXLOOP) - (i + 1);
-        return imin(mn, wmin(imax(nd, 0) * 32, [&](int c) {
+        int fm, bv, bx;
+        scan2(imax(nd, 0) * 32, [&](int c) {
             const int d = i + 1 + (c >> 5), dp = j - 1 - (c & 31);
-            if (dp <= imax(d + TURN, j - MAXLOOP) || !H.can_pair(d, dp)) return BIG;
-            return H.e_intP(i, d, dp, j) + H.g4(PL, d, dp, k, l);
-        }));
+            if (dp <= imax(d + TURN, j - MAXLOOP)) return make_int2(BIG, BIG);
+            const int v = H.e_intP(i, d, dp, j) + H.g4(PL, d, dp, k, l);
+            return make_int2(v, H.can_pair(d, dp) ? v : BIG);
+        }, fm, bv, bx);
+        ilc = IlCache{P_PLiloop, i, j, k, l, bv, bx};
+        return imin(mn, fm);
     }
     __device__ __forceinline__ int get_PRiloop(int i, int j, int k, int l) const {
         if (!order4(i, j, k, l) || !H.can_pair(k, l)) return INF;
         int mn = INF;
         if (k + TURN + 2 < l) mn = H.g4(PR, i, j, k + 1, l - 1) + H.e_stP(k, l);
         const int nd = imin(l, k + MAXLOOP) - (k + 1);
-        return imin(mn, wmin(imax(nd, 0) * 32, [&](int c) {
+        int fm, bv, bx;
+        scan2(imax(nd, 0) * 32, [&](int c) {
             const int d = k + 1 + (c >> 5), dp = l - 1 - (c & 31);
-            if (dp <= imax(d + TURN, l - MAXLOOP) || !H.can_pair(d, dp)) return BIG;
-            return H.e_intP(k, d, dp, l) + H.g4(PR, i, j, d, dp);
-        }));
+            if (dp <= imax(d + TURN, l - MAXLOOP)) return make_int2(BIG, BIG);
+            const int v = H.e_intP(k, d, dp, l) + H.g4(PR, i, j, d, dp);
+            return make_int2(v, H.can_pair(d, dp) ? v : BIG);
+        }, fm, bv, bx);
+        ilc = IlCache{P_PRiloop, i, j, k, l, bv, bx};
+        return imin(mn, fm);
     }
     __device__ __forceinline__ int get_PMiloop(int i, int j, int k, int l) const {
         if (!order4(i, j, k, l) || !H.can_pair(j, k)) return INF;
@@ -325,11 +373,15 @@ struct Bt {
         if (i < j && k < l) mn = H.g4(PM, i, j - 1, k + 1, l) + H.e_stP(j - 1, k + 1);
         const int nd = (j - 1) - imax(i, j - MAXLOOP);
         const int min_dp = imin(l, k + MAXLOOP);
-        return imin(mn, wmin(imax(nd, 0) * 32, [&](int c) {
+        int fm, bv, bx;
+        scan2(imax(nd, 0) * 32, [&](int c) {
             const int d = j - 1 - (c >> 5), dp = k + 1 + (c & 31);
-            if (dp >= min_dp || !H.can_pair(d, dp)) return BIG;
-            return H.e_intP(d, j, k, dp) + H.g4(PM, i, d, dp, l);
-        }));
+            if (dp >= min_dp) return make_int2(BIG, BIG);
+            const int v = H.e_intP(d, j, k, dp) + H.g4(PM, i, d, dp, l);
+            return make_int2(v, H.can_pair(d, dp) ? v : BIG);
+        }, fm, bv, bx);
+        ilc = IlCache{P_PMiloop, i, j, k, l, bv, bx};
+        return imin(mn, fm);
     }
     __device__ __forceinline__ int get_POiloop(int i, int j, int k, int l) const {
         if (!order4(i, j, k, l) || !H.can_pair(i, l)) return INF;
@@ -337,11 +389,15 @@ struct Bt {
         if (i < j && k < l) mn = H.g4(PO, i + 1, j, k, l - 1) + H.e_stP(i, l);
         const int nd = imin(j, i + MAXLOOP) - (i + 1);
         const int min_dp = imax(l - MAXLOOP, k);
-        return imin(mn, wmin(imax(nd, 0) * 32, [&](int c) {
+        int fm, bv, bx;
+        scan2(imax(nd, 0) * 32, [&](int c) {
             const int d = i + 1 + (c >> 5), dp = l - 1 - (c & 31);
-            if (dp <= min_dp || !H.can_pair(d, dp)) return BIG;
-            return H.e_intP(i, d, dp, l) + H.g4(PO, d, j, dp, k);
-        }));
+            if (dp <= min_dp) return make_int2(BIG, BIG);
+            const int v = H.e_intP(i, d, dp, l) + H.g4(PO, d, j, dp, k);
+            return make_int2(v, H.can_pair(d, dp) ? v : BIG);
+        }, fm, bv, bx);
+        ilc = IlCache{P_POiloop, i, j, k, l, bv, bx};
+        return imin(mn, fm);
     }
     __device__ __forceinline__ int get_PXmloop(int m10, int m01, int i2, int j2, int k2, int l2, int i, int j, int k, int l) const {
         if (!order4(i, j, k, l)) return INF;
@@ -842,11 +898,12 @@ __device__ __forceinline__ void Bt::pl(const Interval &cur) {
                 const int tmp = H.g4(PL, i + 1, j - 1, k, l) + H.e_stP(i, j);  // no i+TURN+2<j test here
                 if (tmp < mn) { mn = tmp; best_row = 1; }
                 const int nd = imin(j, i + MAXLOOP) - (i + 1);
-                scan(imax(nd, 0) * 32, [&](int c) {  // d ascending, dp descending; no can_pair filter
-                    const int d = i + 1 + (c >> 5), dp = j - 1 - (c & 31);
-                    if (dp <= imax(d + TURN, j - MAXLOOP)) return BIG;
-                    return H.e_intP(i, d, dp, j) + H.g4(PL, d, dp, k, l);
-                }, bv, bx);
+                if (!il_cached(P_PLiloop, i, j, k, l, bv, bx))
+                    scan(imax(nd, 0) * 32, [&](int c) {  // d ascending, dp descending; no can_pair filter
+                        const int d = i + 1 + (c >> 5), dp = j - 1 - (c & 31);
+                        if (dp <= imax(d + TURN, j - MAXLOOP)) return BIG;
+                        return H.e_intP(i, d, dp, j) + H.g4(PL, d, dp, k, l);
+                    }, bv, bx);
                 if (bv < mn) { mn = bv; best_d = i + 1 + (bx >> 5); best_dp = j - 1 - (bx & 31); best_row = 2; }
             }
             switch (best_row) {
@@ -916,11 +973,12 @@ __device__ __forceinline__ void Bt::pl(const Interval &cur) {
                 const int tmp = H.g4(PR, i, j, k + 1, l - 1) + H.e_stP(k, l);
                 if (tmp < mn) { mn = tmp; best_row = 1; }
                 const int nd = imin(l, k + MAXLOOP) - (k + 1);
-                scan(imax(nd, 0) * 32, [&](int c) {
-                    const int d = k + 1 + (c >> 5), dp = l - 1 - (c & 31);
-                    if (dp <= imax(d + TURN, l - MAXLOOP)) return BIG;
-                    return H.e_intP(k, d, dp, l) + H.g4(PR, i, j, d, dp);
-                }, bv, bx);
+                if (!il_cached(P_PRiloop, i, j, k, l, bv, bx))
+                    scan(imax(nd, 0) * 32, [&](int c) {
+                        const int d = k + 1 + (c >> 5), dp = l - 1 - (c & 31);
+                        if (dp <= imax(d + TURN, l - MAXLOOP)) return BIG;
+                        return H.e_intP(k, d, dp, l) + H.g4(PR, i, j, d, dp);
+                    }, bv, bx);
                 if (bv < mn) { mn = bv; best_d = k + 1 + (bx >> 5); best_dp = l - 1 - (bx & 31); best_row = 2; }
             }
             switch (best_row) {
@@ -995,11 +1053,12 @@ __device__ __forceinline__ void Bt::pl(const Interval &cur) {
                 if (tmp < mn) { mn = tmp; best_row = 1; }
                 const int nd = (j - 1) - imax(i, j - MAXLOOP);
                 const int min_dp = imin(l, k + MAXLOOP);
-                scan(imax(nd, 0) * 32, [&](int c) {  // d descending, dp ascending
-                    const int d = j - 1 - (c >> 5), dp = k + 1 + (c & 31);
-                    if (dp >= min_dp) return BIG;
-                    return H.e_intP(d, j, k, dp) + H.g4(PM, i, d, dp, l);
-                }, bv, bx);
+                if (!il_cached(P_PMiloop, i, j, k, l, bv, bx))
+                    scan(imax(nd, 0) * 32, [&](int c) {  // d descending, dp ascending
+                        const int d = j - 1 - (c >> 5), dp = k + 1 + (c & 31);
+                        if (dp >= min_dp) return BIG;
+                        return H.e_intP(d, j, k, dp) + H.g4(PM, i, d, dp, l);
+                    }, bv, bx);
                 if (bv < mn) { mn = bv; best_d = j - 1 - (bx >> 5); best_dp = k + 1 + (bx & 31); best_row = 2; }
             }
             switch (best_row) {
@@ -1072,11 +1131,12 @@ __device__ __forceinline__ void Bt::pl(const Interval &cur) {
                 if (tmp < mn) { mn = tmp; best_row = 1; }
                 const int nd = imin(j, i + MAXLOOP) - (i + 1);
                 const int min_dp = imax(l - MAXLOOP, k);
-                scan(imax(nd, 0) * 32, [&](int c) {  // reads PO(d,j,dp,k) with dp > k: always INF (A-Q5)
-                    const int d = i + 1 + (c >> 5), dp = l - 1 - (c & 31);
-                    if (dp <= min_dp) return BIG;
-                    return H.e_intP(i, d, dp, l) + H.g4(PO, d, j, dp, k);
-                }, bv, bx);
+                if (!il_cached(P_POiloop, i, j, k, l, bv, bx))
+                    scan(imax(nd, 0) * 32, [&](int c) {  // reads PO(d,j,dp,k) with dp > k: always INF (A-Q5)
+                        const int d = i + 1 + (c >> 5), dp = l - 1 - (c & 31);
+                        if (dp <= min_dp) return BIG;
+                        return H.e_intP(i, d, dp, l) + H.g4(PO, d, j, dp, k);
+                    }, bv, bx);
                 if (bv < mn) { mn = bv; best_row = 2; best_d = i + 1 + (bx >> 5); best_dp = l - 1 - (bx & 31); }
             }
             switch (best_row) {
