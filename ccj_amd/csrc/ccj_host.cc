@@ -109,7 +109,7 @@ struct ccj_ctx {
     bool overlap = true;
     int world = 1, rank = 0, simulate = 0;  // band sharding
     bool host_tb = false;                   // W + traceback on the host over the mirror (else on the GPU)
-    int split_target = 6144;                // k_level4d split heuristic (0: never split)
+    int split_target = 9216;                // k_level4d split heuristic (0: never split)
     bool share = true;                      // split-point sharing
     // fill timing (ccj_set_timing, CCJ_LEVEL_TIMING): 0 = fill only; 1 = + level durations from the
     // lev_done events the fill records anyway (no extra packets); 2 = + a marker pair around every
@@ -1698,7 +1698,7 @@ static int create_impl(const ccj_problem *prob, const ccj_options *opts, std::un
     c->host_tb = opts ? (opts->host_traceback != 0) : false;
     {
         const char *e = getenv("CCJ_SPLIT_TARGET");
-        c->split_target = e ? atoi(e) : 6144;
+        c->split_target = e ? atoi(e) : 9216;
         if (opts && opts->split_target) c->split_target = opts->split_target < 0 ? 0 : opts->split_target;
         const char *lt = getenv("CCJ_LEVEL_TIMING");
         if (lt) c->level_timing = std::max(0, std::min(2, atoi(lt)));

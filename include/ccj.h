@@ -81,7 +81,7 @@ typedef struct ccj_options {
     int host_traceback;
     /* Level-kernel tuning (0 = default for both).
      * split_target: narrow late levels split each cell's split-point loops over up to 8 waves so
-     *   about this many waves run at once (default 6144); < 0 never splits.
+     *   about this many waves run at once (default 9216); < 0 never splits.
      * share_splits: split-point sharing between the cells of one gap column: a
      *   leader cell scans its whole split range once for itself and the next CCJ_SHARE_R-1 cells of
      *   its column; < 0 turns it off (every cell scans its own range). */
