@@ -155,3 +155,33 @@ def test_host_traceback_matches_reference(case):
             assert res[1] == case["rc"] and res[2] == case["stderr"]
     finally:
         wf.close()
+
+
+FUZZ = int(__import__("os").environ.get("CCJ_FUZZ", "0"))
+
+
+@pytest.mark.skipif(FUZZ <= 0, reason="opt-in randomized campaign: CCJ_FUZZ=<cases> (seconds to a minute per case)")
+@pytest.mark.parametrize("k", range(max(FUZZ, 1)))
+def test_fuzz_random_folds(k):
+    """Opt-in randomized parity campaign (round 6): a random sequence (n 20-110, alphabet, parameter
+    set, dangles, noGU) folded on the GPU must give the restatement's 31 matrix hashes (both fill
+    modes of the oracle are pinned against the reference in tests/test_oracle.py), and the device
+    traceback must give the host restatement's structure, energy, side messages or exit."""
+    r = random.Random(90000 + k)
+    n = r.randint(20, 110)
+    seq = _rseq(91000 + k, n, r.choice(["ACGU", "ACGU", "GGCCAU", "GCAU", "AU"]))
+    params = r.choice(["Turner04", "DirksPierce09", "DirksPierce03", "CaoChen09", "Matthews04"])
+    d, g = r.choice([0, 1, 2]), r.random() < 0.25
+    o = OracleFold(seq, blob(params), d, int(g), threads=0)
+    dev = _wf(seq, params, d, g)
+    host = _wf(seq, params, d, g, host_traceback=True)
+    try:
+        dev.fill()
+        rd = _result(dev)
+        assert dev.hashes() == o.hashes(), (n, params, d, g)
+        host.fill()
+        assert _result(host) == rd, (n, params, d, g)
+    finally:
+        dev.close()
+        host.close()
+        o.close()
