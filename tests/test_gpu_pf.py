@@ -192,3 +192,47 @@ def test_pf_kernel_timing_and_work_model():
         assert w["k_pf_level"] >= 84 * ccj_amd.num_cells(60) and all(v > 0 for v in w.values())
     finally:
         pf.close()
+
+
+PF_FUZZ = int(os.environ.get("CCJ_PF_FUZZ", "0"))
+PF_DRV = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "pf_driver")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(PF_FUZZ <= 0 or not os.path.exists(PF_DRV),
+                    reason="opt-in randomized campaign against the reference's own part_func.cc: CCJ_PF_FUZZ=<cases>")
+@pytest.mark.parametrize("k", range(max(PF_FUZZ, 1)))
+def test_pf_fuzz_against_reference_driver(k):
+    """Opt-in randomized campaign (round 6): a random sequence (n 6-50, dangles 0/1/2, the reference's
+    default parameters) through oracle/_ref/pf_driver (the reference's W_final_pf, built here from its
+    own sources with -ffp-contract=off) and through the GPU: the energy, the IEEE bits of W and every
+    matrix hash identical."""
+    import random
+    import struct
+    import subprocess
+
+    import ccj_amd
+    r = random.Random(70000 + k)
+    n = r.randint(6, 50)
+    seq = "".join(r.choice(r.choice(["ACGU", "GGCCAU", "GCAU"])) for _ in range(n))
+    d = r.choice([0, 1, 2])
+    p = subprocess.run([PF_DRV, seq, "-d", str(d)], capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-400:]
+    ref = {"h2": {}, "h4": {}}
+    for line in p.stdout.splitlines():
+        w = line.split()
+        if w and w[0] == "ENERGY":
+            ref["energy"] = w[1]
+        elif w and w[0] == "WBITS":
+            ref["wbits"] = w[1:]
+        elif w and w[0] in ("H2", "H4"):
+            ref[w[0].lower()][w[1]] = w[2]
+    pf = ccj_amd.W_final_pf(seq, dangle=d, params="default")
+    try:
+        e = pf.ccj_pf()
+        assert repr(e) == repr(float(ref["energy"])) or (e != e and ref["energy"] == "nan"), (seq, d)
+        assert ["%016x" % struct.unpack("<Q", struct.pack("<d", w))[0] for w in pf.W()] == ref["wbits"], (seq, d)
+        h = pf.hashes()
+        assert not {k2: v for k2, v in {**ref["h2"], **ref["h4"]}.items() if h[k2] != v}, (seq, d)
+    finally:
+        pf.close()
