@@ -185,3 +185,61 @@ def test_fuzz_random_folds(k):
         dev.close()
         host.close()
         o.close()
+
+
+REF_FUZZ = int(__import__("os").environ.get("CCJ_REF_FUZZ", "0"))
+REF_DRV = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))),
+                                     "oracle", "_ref", "ref_driver")
+
+
+@pytest.mark.skipif(REF_FUZZ <= 0 or not __import__("os").path.exists(REF_DRV),
+                    reason="opt-in randomized campaign against the reference's own build: CCJ_REF_FUZZ=<cases>")
+def test_fuzz_against_reference_driver():
+    """Opt-in randomized campaign (round 6) against the real reference: random sequences (n 10-70,
+    three alphabets, four parameter sets, dangles 0/1/2, noGU) through oracle/_ref/ref_driver (the
+    reference's own fill, built here from its sources; 16 at a time on the host) and through the GPU:
+    all 31 matrix hashes and W(n) identical."""
+    import concurrent.futures
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cases = []
+    for k in range(REF_FUZZ):
+        r = random.Random(80000 + k)
+        n = r.randint(10, 70)
+        seq = _rseq(81000 + k, n, r.choice(["ACGU", "GGCCAU", "GCAU"]))
+        cases.append((seq, r.choice(["Turner04", "DirksPierce09", "DirksPierce03", "CaoChen09"]), r.choice([0, 1, 2]),
+                      r.random() < 0.25))
+
+    def ref(c):
+        seq, params, d, g = c
+        cmd = [REF_DRV, "hash", "--blob", os.path.join(root, "ccj_amd", "params", params + ".ccjp"), "-d", str(d)]
+        p = subprocess.run(cmd + (["--noGU"] if g else []) + [seq], capture_output=True, text=True, timeout=600)
+        h, mfe = {}, None
+        for line in p.stdout.splitlines():
+            w = line.split()
+            if w and w[0] == "HASH":
+                h[w[1]] = w[2]
+            elif w and w[0] == "MFE":
+                mfe = int(w[1])
+        return p.returncode, h, mfe
+
+    with concurrent.futures.ThreadPoolExecutor(16) as ex:
+        refs = list(ex.map(ref, cases))
+    bad = []
+    for c, (rc, h, mfe) in zip(cases, refs):
+        assert rc == 0 and len(h) == 31, c
+        wf = _wf(*c)
+        try:
+            wf.fill()
+            try:
+                wf.result()  # W is computed here (before any backtrack exit of the reference's)
+            except Exception:
+                pass
+            got = wf.hashes()
+            if any(got[x] != h[x] for x in h) or (mfe is not None and wf.W(len(c[0])) != mfe):
+                bad.append(c)
+        finally:
+            wf.close()
+    print(f"{len(cases)} random folds against the reference driver, {len(bad)} differ")
+    assert not bad, bad[:5]
