@@ -195,7 +195,8 @@ REF_DRV = __import__("os").path.join(__import__("os").path.dirname(__import__("o
 @pytest.mark.skipif(REF_FUZZ <= 0 or not __import__("os").path.exists(REF_DRV),
                     reason="opt-in randomized campaign against the reference's own build: CCJ_REF_FUZZ=<cases>")
 def test_fuzz_against_reference_driver():
-    """Opt-in randomized campaign (round 6) against the real reference: random sequences (n 10-70,
+    """Opt-in randomized campaign (round 6) against the real reference: random sequences (n 10-70, or up
+    to CCJ_REF_FUZZ_NMAX,
     three alphabets, four parameter sets, dangles 0/1/2, noGU) through oracle/_ref/ref_driver (the
     reference's own fill, built here from its sources; 16 at a time on the host) and through the GPU:
     all 31 matrix hashes and W(n) identical."""
@@ -206,7 +207,7 @@ def test_fuzz_against_reference_driver():
     cases = []
     for k in range(REF_FUZZ):
         r = random.Random(80000 + k)
-        n = r.randint(10, 70)
+        n = r.randint(10, int(os.environ.get("CCJ_REF_FUZZ_NMAX", "70")))
         seq = _rseq(81000 + k, n, r.choice(["ACGU", "GGCCAU", "GCAU"]))
         cases.append((seq, r.choice(["Turner04", "DirksPierce09", "DirksPierce03", "CaoChen09"]), r.choice([0, 1, 2]),
                       r.random() < 0.25))
@@ -224,8 +225,13 @@ def test_fuzz_against_reference_driver():
                 mfe = int(w[1])
         return p.returncode, h, mfe
 
+    refs = [None] * len(cases)
     with concurrent.futures.ThreadPoolExecutor(16) as ex:
-        refs = list(ex.map(ref, cases))
+        futs = {ex.submit(ref, c): i for i, c in enumerate(cases)}
+        for done, f in enumerate(concurrent.futures.as_completed(futs), 1):
+            refs[futs[f]] = f.result()
+            if done % 16 == 0:
+                print(f"reference folds done: {done}/{len(cases)}", flush=True)
     bad = []
     for c, (rc, h, mfe) in zip(cases, refs):
         assert rc == 0 and len(h) == 31, c
